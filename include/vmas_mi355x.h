@@ -1,0 +1,234 @@
+/*
+ * vmas_mi355x.h -- C ABI of the MI355X-native VMAS physics engine.
+ *
+ * The reference (robj0nes/VectorizedMultiAgentSimulator, pure Python + PyTorch) has no FFI; its
+ * hot path is a sequence of PyTorch tensor ops behind three Python seams.  Each entry point below
+ * replaces one of those seams (file:line relative to the reference checkout):
+ *
+ *   vmas_world_step      <- World.step                         vmas/simulator/core.py:1971-2014
+ *                           (force/torque accumulation 2017-2101, broadphase + 6 narrowphases +
+ *                            joints 2103-2838, semi-implicit Euler 2859-2907)
+ *   vmas_cast_rays       <- World.cast_rays / World.cast_ray     vmas/simulator/core.py:1627-1785
+ *                           (Lidar.measure, vmas/simulator/sensors.py:100-122)
+ *   vmas_distance        <- World.get_distance_from_point / get_distance / is_overlapping
+ *                                                                vmas/simulator/core.py:1787-1968
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; every float is IEEE fp32 (the reference computes in
+ *     torch.float32, core.py:304-315).
+ *   - `device` >= 0 selects a HIP device (gfx950); pointers are then device pointers and the call
+ *     is stream-ordered on `stream` (a hipStream_t, NULL = default stream).  `device` == -1 runs
+ *     the same arithmetic on host threads over host pointers (`stream` ignored).
+ *   - Every call returns 0 on success or a negative VMAS_E_* code; nothing throws across the ABI.
+ *   - The library allocates device memory only in vmas_world_create (tables, broadphase flag
+ *     scratch) and in a process-wide pinned staging ring used to upload the per-call pointer
+ *     tables; per-call it allocates nothing.
+ *   - State tensors are addressed through per-call pointer tables with explicit element strides,
+ *     so the caller's tensors (views, user-replaced tensors, in-place mutated tensors) are read
+ *     exactly where they live.  Outputs go to caller-provided fresh buffers, mirroring the
+ *     reference's "every integrated field is a new tensor" semantics (core.py:2866-2907).
+ */
+#ifndef VMAS_MI355X_H
+#define VMAS_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VMAS_ABI_VERSION 1
+
+/* error codes */
+#define VMAS_OK 0
+#define VMAS_E_INVALID (-1)
+#define VMAS_E_HIP (-2)
+#define VMAS_E_NOMEM (-3)
+#define VMAS_E_NOCONVERGE (-4)
+
+/* shapes: vmas/simulator/core.py:102-202 */
+#define VMAS_SPHERE 0
+#define VMAS_BOX 1
+#define VMAS_LINE 2
+
+/* pair classes in the reference's dispatch order (core.py:2174-2188) */
+#define VMAS_PAIR_JOINT 0
+#define VMAS_PAIR_SS 1
+#define VMAS_PAIR_LS 2 /* (line, sphere)  canonicalised as core.py:2134-2139 */
+#define VMAS_PAIR_LL 3
+#define VMAS_PAIR_BS 4 /* (box, sphere)   core.py:2150-2155 */
+#define VMAS_PAIR_BL 5 /* (box, line)     core.py:2162-2167 */
+#define VMAS_PAIR_BB 6
+
+/* entity flags */
+#define VMAS_F_MOVABLE (1u << 0)
+#define VMAS_F_ROTATABLE (1u << 1)
+#define VMAS_F_HOLLOW (1u << 2)
+#define VMAS_F_AGENT (1u << 3)
+#define VMAS_F_MAX_F (1u << 4)
+#define VMAS_F_F_RANGE (1u << 5)
+#define VMAS_F_MAX_T (1u << 6)
+#define VMAS_F_T_RANGE (1u << 7)
+#define VMAS_F_MAX_SPEED (1u << 8)
+#define VMAS_F_V_RANGE (1u << 9)
+#define VMAS_F_LIN_FRIC (1u << 10) /* linear friction applies (entity value or world > 0) */
+#define VMAS_F_ANG_FRIC (1u << 11)
+#define VMAS_F_GRAVITY (1u << 12) /* entity gravity tensor present (core.py:2048-2051) */
+
+/* broadphase semantics */
+#define VMAS_BROADPHASE_BATCH 0 /* reference: pair simulated iff ANY env in range (core.py:2796) */
+#define VMAS_BROADPHASE_ENV 1   /* every static candidate pair simulated in every env */
+
+/* Static per-entity parameters (host array; uploaded once by vmas_world_create). */
+typedef struct VmasEntityDesc {
+    int32_t shape;         /* VMAS_SPHERE / VMAS_BOX / VMAS_LINE */
+    uint32_t flags;        /* VMAS_F_* */
+    int32_t agent_index;   /* index into VmasStepIO.agents, -1 for landmarks */
+    int32_t out_lin;       /* slot in out_pos/out_vel, -1 if not movable */
+    int32_t out_rot;       /* slot in out_rot/out_ang_vel, -1 if not rotatable */
+    int32_t out_force;     /* slot in out_force (agent force clamps write back), -1 if none */
+    int32_t out_torque;    /* slot in out_torque, -1 if none */
+    float radius;          /* f32(Sphere.radius) */
+    float half_length;     /* f32(length) / 2  (box / line) */
+    float half_width;      /* f32(width) / 2   (box) */
+    float mass;            /* f32(mass) */
+    float inertia;         /* f32(moment_of_inertia(mass)) computed in double (core.py:122-187) */
+    float one_minus_drag;  /* f32(1 - (entity.drag or world.drag)) (core.py:2864-2868) */
+    float lin_fric;        /* f32(linear friction coefficient) */
+    float ang_fric;        /* f32(angular friction coefficient) */
+    float max_speed, v_range, max_f, f_range, max_t, t_range;
+} VmasEntityDesc;
+
+/* Static candidate pair (host array in the reference's accumulation order). */
+typedef struct VmasPairDesc {
+    int32_t cls;       /* VMAS_PAIR_* */
+    int32_t ea, eb;    /* entity indices; for joints: JointConstraint.entity_a / entity_b */
+    int32_t joint;     /* joint index for VMAS_PAIR_JOINT, else -1 */
+    float bp_radius;   /* f32(circumscribed_radius(a) + circumscribed_radius(b)) (core.py:2796-2800) */
+    float dmin;        /* class part of dist_min: SS f32(ra)+f32(rb); LS/BS f32(r)+f32(LINE_MIN_DIST);
+                          LL/BL/BB f32(LINE_MIN_DIST); joints f32(dist) */
+} VmasPairDesc;
+
+/* Static joint constraint (joints.py:147-215, core.py:2200-2291). */
+typedef struct VmasJointDesc {
+    float delta_a_x, delta_a_y; /* shape.get_delta_from_anchor(anchor_a) as f32 */
+    float delta_b_x, delta_b_y;
+    float dist;
+    int32_t rotate;
+    float fixed_rotation;       /* used when VmasJointIO.fixed_rotation is NULL */
+    int32_t pad;
+} VmasJointDesc;
+
+/* World-level constants (World.__init__, core.py:1090-1149). */
+typedef struct VmasWorldConfig {
+    int32_t n_entities, n_agents, n_pairs, n_joints;
+    int32_t batch;            /* num_envs */
+    int32_t device;           /* HIP ordinal, or -1 for host */
+    int32_t n_out_lin, n_out_rot, n_out_force, n_out_torque;
+    float contact_margin, collision_force, joint_force, torque_constraint_force;
+    float gravity_x, gravity_y;
+    int32_t has_world_gravity; /* not (gravity == 0).all()  (core.py:2044) */
+    float x_semidim, y_semidim;
+    int32_t has_x_semidim, has_y_semidim;
+    int32_t max_substeps;     /* capacity of the broadphase flag scratch */
+} VmasWorldConfig;
+
+/* Per-call input pointers.  Strides are in elements (torch .stride()). */
+typedef struct VmasEntityIO {
+    const float* pos;     /* [B,2] */
+    const float* vel;     /* [B,2] */
+    const float* rot;     /* [B,1] */
+    const float* ang_vel; /* [B,1] */
+    const float* gravity; /* entity gravity broadcast to [B,2] (strides may be 0), or NULL */
+    int32_t pos_s0, pos_s1, vel_s0, vel_s1;
+    int32_t rot_s0, ang_s0, grav_s0, grav_s1;
+} VmasEntityIO;
+
+typedef struct VmasAgentIO {
+    const float* force;  /* agent.state.force  [B,2] */
+    const float* torque; /* agent.state.torque [B,1] */
+    int32_t force_s0, force_s1, torque_s0, pad;
+} VmasAgentIO;
+
+typedef struct VmasJointIO {
+    const float* fixed_rotation; /* per-env [B,1] tensor (Joint.notify), or NULL */
+    int32_t s0, pad;
+} VmasJointIO;
+
+typedef struct VmasStepIO {
+    const VmasEntityIO* entities; /* host array [n_entities] */
+    const VmasAgentIO* agents;    /* host array [n_agents] */
+    const VmasJointIO* joints;    /* host array [n_joints] or NULL */
+    float* out_pos;    /* [n_out_lin][B][2] */
+    float* out_vel;    /* [n_out_lin][B][2] */
+    float* out_rot;    /* [n_out_rot][B] */
+    float* out_ang_vel;/* [n_out_rot][B] */
+    float* out_force;  /* [n_out_force][B][2] */
+    float* out_torque; /* [n_out_torque][B] */
+    int32_t substeps;
+    float sub_dt;      /* f32(dt / substeps) */
+    int32_t broadphase;/* VMAS_BROADPHASE_* */
+    int32_t pad;
+} VmasStepIO;
+
+typedef struct VmasWorld VmasWorld;
+
+/* Ray target (one filtered entity of World.cast_rays, core.py:1677-1690). */
+typedef struct VmasRayTarget {
+    int32_t shape;
+    float radius, length, width; /* f32 of the python shape sizes */
+    const float* pos;            /* [B,2] */
+    const float* rot;            /* [B,1] */
+    int32_t pos_s0, pos_s1, rot_s0, pad;
+} VmasRayTarget;
+
+/* Distance query operand (core.py:1787-1968). */
+typedef struct VmasShapeRef {
+    int32_t shape;
+    int32_t pad0;
+    float radius, length, width; /* f32 of the python shape sizes */
+    float radius_lmd;            /* f32(radius + LINE_MIN_DIST) summed in double (core.py:1960) */
+    const float* pos;
+    const float* rot;
+    int32_t pos_s0, pos_s1, rot_s0, pad;
+} VmasShapeRef;
+
+#define VMAS_DIST_POINT 0   /* get_distance_from_point(a, test_point) */
+#define VMAS_DIST_PAIR 1    /* get_distance(a, b) */
+#define VMAS_OVERLAP_PAIR 2 /* is_overlapping(a, b) -> out_dist holds 1.0f / 0.0f */
+
+int32_t vmas_abi_version(void);
+/* Number of HIP devices visible (0 if none / no driver). */
+int32_t vmas_device_count(void);
+const char* vmas_last_error(void);
+
+int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                          const VmasPairDesc* pairs, const VmasJointDesc* joints,
+                          VmasWorld** out_world);
+int32_t vmas_world_destroy(VmasWorld* world);
+
+/* One World.step(): all substeps.  Under VMAS_BROADPHASE_BATCH the call returns after the
+ * broadphase fixed point has been verified (one host<->device handshake per iteration);
+ * *iterations (may be NULL) receives the number of kernel passes used. */
+int32_t vmas_world_step(VmasWorld* world, const VmasStepIO* io, void* stream, int32_t* iterations);
+
+/* World.cast_rays(entity, angles, max_range, entity_filter) with the filter already applied:
+ * out[b, r] = min(max_range, min over targets of the ray distance).  angle[b, r] =
+ * angles[b*ang_s0 + r*ang_s1] (+ rot_offset[b*rot_s0] when rot_offset != NULL, the Lidar's
+ * `self._angles + agent.state.rot`). */
+int32_t vmas_cast_rays(int32_t device, int32_t batch, int32_t n_rays, const float* origin,
+                       int32_t origin_s0, int32_t origin_s1, const float* angles, int32_t ang_s0,
+                       int32_t ang_s1, const float* rot_offset, int32_t rot_s0,
+                       const VmasRayTarget* targets, int32_t n_targets, float max_range,
+                       float* out, void* stream);
+
+/* Distance queries; out has B floats, or B bytes of 0/1 (torch.bool) for VMAS_OVERLAP_PAIR. */
+int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
+                      const VmasShapeRef* b, const float* test_point, int32_t tp_s0,
+                      int32_t tp_s1, void* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VMAS_MI355X_H */

@@ -1,0 +1,276 @@
+"""ctypes binding of the C ABI declared in ``include/vmas_mi355x.h``.
+
+The shared library ``libvmas_mi355x.so`` is built in-tree by ``__graft_entry__.build()`` (hipcc,
+``--offload-arch=gfx950``).  It contains both the gfx950 kernels and the host (``device == -1``)
+backend compiled from the same ``csrc/vmas_physics.hpp``.  There is no Python fallback: if the
+library is missing, importing the simulator raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_NAME = "libvmas_mi355x.so"
+LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+
+# ------------------------------------------------------------------------------------------------
+# constants mirrored from include/vmas_mi355x.h
+VMAS_ABI_VERSION = 1
+VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
+(
+    VMAS_PAIR_JOINT,
+    VMAS_PAIR_SS,
+    VMAS_PAIR_LS,
+    VMAS_PAIR_LL,
+    VMAS_PAIR_BS,
+    VMAS_PAIR_BL,
+    VMAS_PAIR_BB,
+) = range(7)
+F_MOVABLE = 1 << 0
+F_ROTATABLE = 1 << 1
+F_HOLLOW = 1 << 2
+F_AGENT = 1 << 3
+F_MAX_F = 1 << 4
+F_F_RANGE = 1 << 5
+F_MAX_T = 1 << 6
+F_T_RANGE = 1 << 7
+F_MAX_SPEED = 1 << 8
+F_V_RANGE = 1 << 9
+F_LIN_FRIC = 1 << 10
+F_ANG_FRIC = 1 << 11
+F_GRAVITY = 1 << 12
+BROADPHASE_BATCH = 0
+BROADPHASE_ENV = 1
+DIST_POINT, DIST_PAIR, OVERLAP_PAIR = 0, 1, 2
+
+# exported symbols (tests check the library exports every one of them)
+EXPORTED_SYMBOLS = (
+    "vmas_abi_version",
+    "vmas_device_count",
+    "vmas_last_error",
+    "vmas_world_create",
+    "vmas_world_destroy",
+    "vmas_world_step",
+    "vmas_cast_rays",
+    "vmas_distance",
+)
+
+_i32 = ctypes.c_int32
+_u32 = ctypes.c_uint32
+_f32 = ctypes.c_float
+_vp = ctypes.c_void_p
+
+
+class VmasEntityDesc(ctypes.Structure):
+    _fields_ = [
+        ("shape", _i32),
+        ("flags", _u32),
+        ("agent_index", _i32),
+        ("out_lin", _i32),
+        ("out_rot", _i32),
+        ("out_force", _i32),
+        ("out_torque", _i32),
+        ("radius", _f32),
+        ("half_length", _f32),
+        ("half_width", _f32),
+        ("mass", _f32),
+        ("inertia", _f32),
+        ("one_minus_drag", _f32),
+        ("lin_fric", _f32),
+        ("ang_fric", _f32),
+        ("max_speed", _f32),
+        ("v_range", _f32),
+        ("max_f", _f32),
+        ("f_range", _f32),
+        ("max_t", _f32),
+        ("t_range", _f32),
+    ]
+
+
+class VmasPairDesc(ctypes.Structure):
+    _fields_ = [
+        ("cls", _i32),
+        ("ea", _i32),
+        ("eb", _i32),
+        ("joint", _i32),
+        ("bp_radius", _f32),
+        ("dmin", _f32),
+    ]
+
+
+class VmasJointDesc(ctypes.Structure):
+    _fields_ = [
+        ("delta_a_x", _f32),
+        ("delta_a_y", _f32),
+        ("delta_b_x", _f32),
+        ("delta_b_y", _f32),
+        ("dist", _f32),
+        ("rotate", _i32),
+        ("fixed_rotation", _f32),
+        ("pad", _i32),
+    ]
+
+
+class VmasWorldConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_entities", _i32),
+        ("n_agents", _i32),
+        ("n_pairs", _i32),
+        ("n_joints", _i32),
+        ("batch", _i32),
+        ("device", _i32),
+        ("n_out_lin", _i32),
+        ("n_out_rot", _i32),
+        ("n_out_force", _i32),
+        ("n_out_torque", _i32),
+        ("contact_margin", _f32),
+        ("collision_force", _f32),
+        ("joint_force", _f32),
+        ("torque_constraint_force", _f32),
+        ("gravity_x", _f32),
+        ("gravity_y", _f32),
+        ("has_world_gravity", _i32),
+        ("x_semidim", _f32),
+        ("y_semidim", _f32),
+        ("has_x_semidim", _i32),
+        ("has_y_semidim", _i32),
+        ("max_substeps", _i32),
+    ]
+
+
+class VmasStepIO(ctypes.Structure):
+    _fields_ = [
+        ("entities", _vp),
+        ("agents", _vp),
+        ("joints", _vp),
+        ("out_pos", _vp),
+        ("out_vel", _vp),
+        ("out_rot", _vp),
+        ("out_ang_vel", _vp),
+        ("out_force", _vp),
+        ("out_torque", _vp),
+        ("substeps", _i32),
+        ("sub_dt", _f32),
+        ("broadphase", _i32),
+        ("pad", _i32),
+    ]
+
+
+class VmasShapeRef(ctypes.Structure):
+    _fields_ = [
+        ("shape", _i32),
+        ("pad0", _i32),
+        ("radius", _f32),
+        ("length", _f32),
+        ("width", _f32),
+        ("radius_lmd", _f32),
+        ("pos", _vp),
+        ("rot", _vp),
+        ("pos_s0", _i32),
+        ("pos_s1", _i32),
+        ("rot_s0", _i32),
+        ("pad", _i32),
+    ]
+
+
+# Per-call pointer tables are built as numpy structured arrays (one row per entity/agent/joint);
+# their layouts must match VmasEntityIO / VmasAgentIO / VmasJointIO / VmasRayTarget.
+ENTITY_IO_DTYPE = np.dtype(
+    [
+        ("pos", "<u8"),
+        ("vel", "<u8"),
+        ("rot", "<u8"),
+        ("ang", "<u8"),
+        ("grav", "<u8"),
+        ("pos_s0", "<i4"),
+        ("pos_s1", "<i4"),
+        ("vel_s0", "<i4"),
+        ("vel_s1", "<i4"),
+        ("rot_s0", "<i4"),
+        ("ang_s0", "<i4"),
+        ("grav_s0", "<i4"),
+        ("grav_s1", "<i4"),
+    ]
+)
+AGENT_IO_DTYPE = np.dtype(
+    [
+        ("force", "<u8"),
+        ("torque", "<u8"),
+        ("force_s0", "<i4"),
+        ("force_s1", "<i4"),
+        ("torque_s0", "<i4"),
+        ("pad", "<i4"),
+    ]
+)
+JOINT_IO_DTYPE = np.dtype([("fixed_rotation", "<u8"), ("s0", "<i4"), ("pad", "<i4")])
+RAY_TARGET_DTYPE = np.dtype(
+    [
+        ("shape", "<i4"),
+        ("radius", "<f4"),
+        ("length", "<f4"),
+        ("width", "<f4"),
+        ("pos", "<u8"),
+        ("rot", "<u8"),
+        ("pos_s0", "<i4"),
+        ("pos_s1", "<i4"),
+        ("rot_s0", "<i4"),
+        ("pad", "<i4"),
+    ]
+)
+assert ENTITY_IO_DTYPE.itemsize == 72
+assert AGENT_IO_DTYPE.itemsize == 32
+assert JOINT_IO_DTYPE.itemsize == 16
+assert RAY_TARGET_DTYPE.itemsize == 48
+assert ctypes.sizeof(VmasEntityDesc) == 84
+assert ctypes.sizeof(VmasShapeRef) == 56
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load (once) and return the native library.  Raises NativeLibraryError if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise NativeLibraryError(
+            f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the MI355X engine has no Python fallback)"
+        )
+    lib = ctypes.CDLL(str(p))
+    lib.vmas_abi_version.restype = _i32
+    lib.vmas_device_count.restype = _i32
+    lib.vmas_last_error.restype = ctypes.c_char_p
+    lib.vmas_world_create.restype = _i32
+    lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
+    lib.vmas_world_destroy.restype = _i32
+    lib.vmas_world_destroy.argtypes = [_vp]
+    lib.vmas_world_step.restype = _i32
+    lib.vmas_world_step.argtypes = [_vp, _vp, _vp, _vp]
+    lib.vmas_cast_rays.restype = _i32
+    lib.vmas_cast_rays.argtypes = [
+        _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
+    ]
+    lib.vmas_distance.restype = _i32
+    lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
+    ver = lib.vmas_abi_version()
+    if ver != VMAS_ABI_VERSION:
+        raise NativeLibraryError(f"ABI version mismatch: library {ver}, python {VMAS_ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().vmas_last_error().decode(errors="replace")
+        raise NativeLibraryError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,1171 @@
+// vmas_kernels.hip -- MI355X (gfx950) kernels + host backend + C ABI for the VMAS physics step.
+//
+// Layout of the work:
+//   * one workgroup = 64 environments (one env per lane) x NW waves;
+//   * the environment's entity state lives in LDS as [entity][field][lane] fp32 rows, so every
+//     LDS access of a wave is 64 consecutive dwords (conflict free) and every HBM access is a
+//     coalesced 256/512-B line;
+//   * per substep: "pair phase" -- waves stride over the candidate pairs of a chunk (a pair is one
+//     wave-uniform task: same narrowphase class for all 64 lanes, no divergence) and store
+//     (force on a, torque on a, torque on b) rows in LDS; barrier; "entity phase" -- waves stride
+//     over the dynamic entities, accumulate action/friction/gravity and then the pair results in
+//     the reference's order (bit-identical summation order, no atomics), integrate; barrier;
+//   * all substeps run inside one launch; the reference's batch-global broadphase (a pair is
+//     simulated iff ANY env has it in range, core.py:2796) is honoured exactly by a fixed-point
+//     iteration over a [substep][pair] activity mask (see vmas_world_step).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "vmas_physics.hpp"
+
+using namespace vmas;
+
+// ------------------------------------------------------------------------------------------------
+// error reporting
+static thread_local std::string g_err;
+static int32_t fail(int32_t code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIP_TRY(x)                                                                        \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            return fail(VMAS_E_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// host thread pool for the device == -1 backend
+class Pool {
+  public:
+    static Pool& get() {
+        static Pool p;
+        return p;
+    }
+    int size() const { return (int)workers_.size() + 1; }
+    // run fn(chunk_index) for chunk_index in [0, n)
+    void run(int n, const std::function<void(int)>& fn) {
+        if (n <= 1 || workers_.empty()) {
+            for (int i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(m_);
+        job_ = &fn;
+        njobs_ = n;
+        next_.store(0);
+        done_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        lk.unlock();
+        work();
+        lk.lock();
+        cv_done_.wait(lk, [&] { return done_ == (int)workers_.size(); });
+        job_ = nullptr;
+    }
+
+  private:
+    Pool() {
+        int n = (int)std::thread::hardware_concurrency();
+        if (const char* s = getenv("OMP_NUM_THREADS")) n = std::max(1, atoi(s));
+        if (const char* s = getenv("VMAS_HOST_THREADS")) n = std::max(1, atoi(s));
+        n = std::min(n, 64);
+        for (int i = 0; i + 1 < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void work() {
+        for (;;) {
+            int i = next_.fetch_add(1);
+            if (i >= njobs_) break;
+            (*job_)(i);
+        }
+    }
+    void loop() {
+        long seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            lk.unlock();
+            work();
+            lk.lock();
+            ++done_;
+            cv_done_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, cv_done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int njobs_ = 0, done_ = 0;
+    long gen_ = 0;
+    bool stop_ = false;
+    std::atomic<int> next_{0};
+};
+
+// ------------------------------------------------------------------------------------------------
+// Pinned staging ring: per-call pointer tables are copied host -> pinned slot -> device slot with
+// one stream-ordered hipMemcpyAsync; slots are recycled in segments guarded by events.
+namespace {
+constexpr size_t kSlot = 16384;   // bytes per slot
+constexpr int kSlots = 256;
+constexpr int kSegs = 8;          // kSlots / kSegs slots per segment
+struct Ring {
+    int device = -1;
+    char* host = nullptr;
+    char* dev = nullptr;
+    hipEvent_t ev[kSegs];
+    bool ev_live[kSegs] = {};
+    int next = 0;
+};
+std::mutex g_ring_mu;
+std::vector<Ring*> g_rings;
+
+int32_t ring_upload(int device, const void* src, size_t n, hipStream_t stream, const void** out) {
+    if (n > kSlot) return fail(VMAS_E_INVALID, "pointer table of %zu bytes exceeds %zu", n, kSlot);
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    Ring* r = nullptr;
+    for (Ring* x : g_rings)
+        if (x->device == device) r = x;
+    if (!r) {
+        r = new Ring();
+        r->device = device;
+        HIP_TRY(hipHostMalloc((void**)&r->host, kSlot * kSlots, hipHostMallocDefault));
+        HIP_TRY(hipMalloc((void**)&r->dev, kSlot * kSlots));
+        for (int i = 0; i < kSegs; ++i) HIP_TRY(hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming));
+        g_rings.push_back(r);
+    }
+    const int per = kSlots / kSegs;
+    const int slot = r->next;
+    const int seg = slot / per;
+    if (slot % per == 0 && r->ev_live[seg]) HIP_TRY(hipEventSynchronize(r->ev[seg]));
+    memcpy(r->host + (size_t)slot * kSlot, src, n);
+    HIP_TRY(hipMemcpyAsync(r->dev + (size_t)slot * kSlot, r->host + (size_t)slot * kSlot, n,
+                           hipMemcpyHostToDevice, stream));
+    if (slot % per == per - 1) {
+        HIP_TRY(hipEventRecord(r->ev[seg], stream));
+        r->ev_live[seg] = true;
+    }
+    r->next = (slot + 1) % kSlots;
+    *out = r->dev + (size_t)slot * kSlot;
+    return VMAS_OK;
+}
+
+int32_t use_device(int device) {
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != device) HIP_TRY(hipSetDevice(device));
+    return VMAS_OK;
+}
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// World: static tables (host copies + device copies) and broadphase scratch.
+struct VmasWorld {
+    VmasWorldConfig cfg;
+    std::vector<VmasEntityDesc> ed;
+    std::vector<VmasPairDesc> pd;
+    std::vector<VmasJointDesc> jd;
+    std::vector<int32_t> dyn;         // dynamic entity indices
+    std::vector<int32_t> trig_slot;   // [E], -1 = no trig row
+    int n_trig = 0;
+    // per-dynamic-entity contribution items ((pair << 2) | (side << 1) | torque), reference order
+    std::vector<std::vector<int32_t>> items;
+    // GPU launch geometry
+    int nw = 8, chunk = 0, n_chunks = 1;
+    std::vector<int32_t> contrib;      // flattened items
+    std::vector<int32_t> contrib_off;  // [n_dyn][n_chunks + 1]
+    size_t lds_state_floats = 0;       // per block, in floats (state/trig/results/acc/agent rows)
+    bool global_scratch = false;
+    // device allocations
+    char* d_tables = nullptr;
+    const VmasEntityDesc* d_ed = nullptr;
+    const VmasPairDesc* d_pd = nullptr;
+    const VmasJointDesc* d_jd = nullptr;
+    const int32_t* d_dyn = nullptr;
+    const int32_t* d_trig = nullptr;
+    const int32_t* d_contrib = nullptr;
+    const int32_t* d_contrib_off = nullptr;
+    uint32_t* d_mask = nullptr;      // [max_substeps][W]
+    uint32_t* d_blk = nullptr;       // [nblk][2][max_substeps][W]
+    uint32_t* d_viol = nullptr;      // 1 word
+    uint32_t* h_viol = nullptr;      // pinned
+    float* d_scratch = nullptr;      // global-memory state rows when LDS is too small
+    int W = 1, nblk = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+// device-side parameter block
+struct StepK {
+    const VmasEntityDesc* ed;
+    const VmasPairDesc* pd;
+    const VmasJointDesc* jd;
+    const int32_t* dyn;
+    const int32_t* trig;
+    const int32_t* contrib;
+    const int32_t* contrib_off;
+    const VmasEntityIO* eio;
+    const VmasAgentIO* aio;
+    const VmasJointIO* jio;
+    float* out_pos;
+    float* out_vel;
+    float* out_rot;
+    float* out_ang;
+    float* out_force;
+    float* out_torque;
+    const uint32_t* mask;
+    uint32_t* blk;
+    float* scratch;
+    int B, E, A, P, W, S, n_dyn, n_trig, chunk, n_chunks;
+    size_t scratch_floats;
+    float sdt;
+    WorldK wk;
+    float gx, gy, xs, ys;
+    int has_g, has_xs, has_ys;
+};
+
+__device__ __forceinline__ V2 load2(const float* p, int s0, int s1, int b) {
+    if (s0 == 2 && s1 == 1) {
+        const float2 v = reinterpret_cast<const float2*>(p)[b];
+        return mk(v.x, v.y);
+    }
+    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);
+}
+
+// LDS (or global scratch) row accessor for the kernel
+struct RowsK {
+    float* SB;
+    float* TR;
+    const int32_t* trig;
+    int lane;
+    __device__ __forceinline__ V2 pos(int e) const {
+        return mk(SB[(e * 6 + 0) * 64 + lane], SB[(e * 6 + 1) * 64 + lane]);
+    }
+    __device__ __forceinline__ float rot(int e) const { return SB[(e * 6 + 4) * 64 + lane]; }
+    __device__ __forceinline__ Trig tr(int e) const {
+        const int s = trig[e];
+        const float* t = TR + s * 4 * 64 + lane;
+        return Trig{t[0], t[64], t[128], t[192]};
+    }
+};
+
+// Evaluate one candidate pair (shared by the kernel and the host backend)
+template <class G>
+__host__ __device__ __forceinline__ PairOut eval_pair(const VmasPairDesc& pd,
+                                                      const VmasEntityDesc* ed,
+                                                      const VmasJointDesc* jd, const G& g,
+                                                      const WorldK& w, float fixed_rot) {
+    const int ea = pd.ea, eb = pd.eb;
+    switch (pd.cls) {
+        case VMAS_PAIR_SS:
+            return pair_ss(g.pos(ea), g.pos(eb), pd.dmin, w);
+        case VMAS_PAIR_LS:
+            return pair_ls(g.pos(ea), g.tr(ea), ed[ea].half_length, g.pos(eb), pd.dmin, w);
+        case VMAS_PAIR_LL:
+            return pair_ll(g.pos(ea), g.tr(ea), ed[ea].half_length, g.pos(eb), g.tr(eb),
+                           ed[eb].half_length, pd.dmin, w);
+        case VMAS_PAIR_BS:
+            return pair_bs(g.pos(ea), g.tr(ea), ed[ea].half_length, ed[ea].half_width,
+                           (ed[ea].flags & VMAS_F_HOLLOW) != 0, g.pos(eb), pd.dmin, w);
+        case VMAS_PAIR_BL:
+            return pair_bl(g.pos(ea), g.tr(ea), ed[ea].half_length, ed[ea].half_width,
+                           (ed[ea].flags & VMAS_F_HOLLOW) != 0, g.pos(eb), g.tr(eb),
+                           ed[eb].half_length, pd.dmin, w);
+        case VMAS_PAIR_BB:
+            return pair_bb(g.pos(ea), g.tr(ea), ed[ea].half_length, ed[ea].half_width,
+                           (ed[ea].flags & VMAS_F_HOLLOW) != 0, g.pos(eb), g.tr(eb),
+                           ed[eb].half_length, ed[eb].half_width,
+                           (ed[eb].flags & VMAS_F_HOLLOW) != 0, pd.dmin, w);
+        default: {  // VMAS_PAIR_JOINT
+            const VmasJointDesc j = jd[pd.joint];
+            return pair_joint(g.pos(ea), g.rot(ea), g.tr(ea), g.pos(eb), g.rot(eb), g.tr(eb),
+                              mk(j.delta_a_x, j.delta_a_y), mk(j.delta_b_x, j.delta_b_y), j.dist,
+                              j.rotate != 0, fixed_rot, w);
+        }
+    }
+}
+
+// Action force/torque clamps + friction + gravity of one entity (core.py:1994-2003, 2017-2101).
+// af/at: the agent's current state.force/torque (updated in place: the reference writes the
+// clamped value back to agent.state.force each substep).
+__host__ __device__ __forceinline__ void pre_forces(const VmasEntityDesc& d, bool is_agent, V2& af,
+                                                    float& at, V2 vel, float w, V2 eg,
+                                                    bool has_eg, float gx, float gy, bool has_g,
+                                                    float sdt, float& fx, float& fy, float& tq) {
+    fx = 0.f;
+    fy = 0.f;
+    tq = 0.f;
+    const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+    if (is_agent) {
+        if (mov) {
+            V2 f = af;
+            if (d.flags & VMAS_F_MAX_F) f = clamp_with_norm(f, d.max_f);
+            if (d.flags & VMAS_F_F_RANGE) f = mk(tclamp(f.x, -d.f_range, d.f_range), tclamp(f.y, -d.f_range, d.f_range));
+            af = f;
+            fx = fx + f.x;
+            fy = fy + f.y;
+        }
+        if (rotb) {
+            float t = at;
+            if (d.flags & VMAS_F_MAX_T) t = clamp_with_norm1(t, d.max_t);
+            if (d.flags & VMAS_F_T_RANGE) t = tclamp(t, -d.t_range, d.t_range);
+            at = t;
+            tq = tq + t;
+        }
+    }
+    if (d.flags & VMAS_F_LIN_FRIC) {
+        const V2 f = friction2(vel, d.lin_fric, d.mass, sdt);
+        fx = fx + f.x;
+        fy = fy + f.y;
+    }
+    if (d.flags & VMAS_F_ANG_FRIC) tq = tq + friction1(w, d.ang_fric, d.inertia, sdt);
+    if (mov) {
+        if (has_g) {
+            fx = fx + d.mass * gx;
+            fy = fy + d.mass * gy;
+        }
+        if (has_eg) {
+            fx = fx + d.mass * eg.x;
+            fy = fy + d.mass * eg.y;
+        }
+    }
+}
+
+// _integrate_state (core.py:2859-2907)
+__host__ __device__ __forceinline__ void integrate(const VmasEntityDesc& d, int substep, float sdt,
+                                                   float fx, float fy, float tq, bool has_xs,
+                                                   float xs, bool has_ys, float ys, V2& p, V2& v,
+                                                   float& rot, float& w) {
+    if (d.flags & VMAS_F_MOVABLE) {
+        if (substep == 0) v = mk(v.x * d.one_minus_drag, v.y * d.one_minus_drag);
+        const V2 acc = mk(fx / d.mass, fy / d.mass);
+        v = mk(v.x + acc.x * sdt, v.y + acc.y * sdt);
+        if (d.flags & VMAS_F_MAX_SPEED) v = clamp_with_norm(v, d.max_speed);
+        if (d.flags & VMAS_F_V_RANGE) v = mk(tclamp(v.x, -d.v_range, d.v_range), tclamp(v.y, -d.v_range, d.v_range));
+        V2 np = mk(p.x + v.x * sdt, p.y + v.y * sdt);
+        if (has_xs) np.x = tclamp(np.x, -xs, xs);
+        if (has_ys) np.y = tclamp(np.y, -ys, ys);
+        p = np;
+    }
+    if (d.flags & VMAS_F_ROTATABLE) {
+        if (substep == 0) w = w * d.one_minus_drag;
+        w = w + (tq / d.inertia) * sdt;
+        rot = rot + w * sdt;
+    }
+}
+
+__device__ __forceinline__ bool mask_bit(const uint32_t* m, int W, int s, int p) {
+    return (m[s * W + (p >> 5)] >> (p & 31)) & 1u;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused step kernel.
+__global__ void __launch_bounds__(512) k_step(StepK k) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    const int b = blockIdx.x * 64 + lane;
+    const bool valid = b < k.B;
+    const int bb = valid ? b : (k.B - 1);
+
+    uint32_t* FL = reinterpret_cast<uint32_t*>(lds);
+    const int nfl = 2 * k.S * k.W;
+    float* base = k.scratch ? (k.scratch + (size_t)blockIdx.x * k.scratch_floats)
+                            : (lds + ((nfl + 3) & ~3));
+    float* SB = base;
+    float* TR = SB + k.E * 6 * 64;
+    float* RS = TR + k.n_trig * 4 * 64;
+    float* AC = RS + k.chunk * 4 * 64;
+    float* AF = AC + k.n_dyn * 3 * 64;
+    const RowsK g{SB, TR, k.trig, lane};
+
+    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;
+    // ---- load state rows
+    for (int e = wave; e < k.E; e += nw) {
+        const VmasEntityIO io = k.eio[e];
+        const V2 p = load2(io.pos, io.pos_s0, io.pos_s1, bb);
+        const V2 v = load2(io.vel, io.vel_s0, io.vel_s1, bb);
+        const float r = io.rot[(long)bb * io.rot_s0];
+        const float w = io.ang_vel[(long)bb * io.ang_s0];
+        float* s = SB + e * 6 * 64 + lane;
+        s[0] = p.x; s[64] = p.y; s[128] = v.x; s[192] = v.y; s[256] = r; s[320] = w;
+        const int ts = k.trig[e];
+        if (ts >= 0) {
+            const Trig t = make_trig(r);
+            float* tt = TR + ts * 4 * 64 + lane;
+            tt[0] = t.c0; tt[64] = t.s0; tt[128] = t.c1; tt[192] = t.s1;
+        }
+    }
+    for (int a = wave; a < k.A; a += nw) {
+        const VmasAgentIO io = k.aio[a];
+        const V2 f = load2(io.force, io.force_s0, io.force_s1, bb);
+        float* s = AF + a * 3 * 64 + lane;
+        s[0] = f.x; s[64] = f.y; s[128] = io.torque[(long)bb * io.torque_s0];
+    }
+    __syncthreads();
+
+    for (int s = 0; s < k.S; ++s) {
+        for (int c = 0; c < k.n_chunks; ++c) {
+            const int p0 = c * k.chunk;
+            const int p1 = min(k.P, p0 + k.chunk);
+            // ---- pair phase
+            for (int p = p0 + wave; p < p1; p += nw) {
+                const VmasPairDesc pd = k.pd[p];
+                bool inr = true;
+                if (pd.cls != VMAS_PAIR_JOINT) inr = norm(g.pos(pd.ea) - g.pos(pd.eb)) <= pd.bp_radius;
+                if (k.blk) {
+                    const unsigned long long bal = __ballot(inr && valid);
+                    if (lane == 0 && bal) atomicOr(&FL[s * k.W + (p >> 5)], 1u << (p & 31));
+                }
+                if (!mask_bit(k.mask, k.W, s, p)) continue;
+                float fixed_rot = 0.f;
+                if (pd.cls == VMAS_PAIR_JOINT) {
+                    const VmasJointIO jio = k.jio[pd.joint];
+                    fixed_rot = jio.fixed_rotation ? jio.fixed_rotation[(long)bb * jio.s0]
+                                                   : k.jd[pd.joint].fixed_rotation;
+                }
+                const PairOut o = eval_pair(pd, k.ed, k.jd, g, k.wk, fixed_rot);
+                float* r = RS + (p - p0) * 4 * 64 + lane;
+                r[0] = o.fa.x; r[64] = o.fa.y; r[128] = o.ta; r[192] = o.tb;
+                if (k.blk && pd.cls != VMAS_PAIR_JOINT) {
+                    const bool nz = valid && !inr &&
+                                    (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || o.tb != 0.f);
+                    const unsigned long long bal = __ballot(nz);
+                    if (lane == 0 && bal)
+                        atomicOr(&FL[(k.S + s) * k.W + (p >> 5)], 1u << (p & 31));
+                }
+            }
+            __syncthreads();
+            // ---- entity phase
+            for (int i = wave; i < k.n_dyn; i += nw) {
+                const int e = k.dyn[i];
+                const VmasEntityDesc d = k.ed[e];
+                float fx, fy, tq;
+                float* acc = AC + i * 3 * 64 + lane;
+                float* sb = SB + e * 6 * 64 + lane;
+                if (c == 0) {
+                    V2 af = mk(0.f, 0.f);
+                    float at = 0.f;
+                    float* afp = nullptr;
+                    if (d.agent_index >= 0) {
+                        afp = AF + d.agent_index * 3 * 64 + lane;
+                        af = mk(afp[0], afp[64]);
+                        at = afp[128];
+                    }
+                    V2 eg = mk(0.f, 0.f);
+                    const bool has_eg = (d.flags & VMAS_F_GRAVITY) != 0;
+                    if (has_eg) {
+                        const VmasEntityIO io = k.eio[e];
+                        eg = load2(io.gravity, io.grav_s0, io.grav_s1, bb);
+                    }
+                    pre_forces(d, d.agent_index >= 0, af, at, mk(sb[128], sb[192]), sb[320], eg,
+                               has_eg, k.gx, k.gy, k.has_g != 0, k.sdt, fx, fy, tq);
+                    if (afp) { afp[0] = af.x; afp[64] = af.y; afp[128] = at; }
+                } else {
+                    fx = acc[0]; fy = acc[64]; tq = acc[128];
+                }
+                const int j0 = k.contrib_off[i * (k.n_chunks + 1) + c];
+                const int j1 = k.contrib_off[i * (k.n_chunks + 1) + c + 1];
+                const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+                for (int j = j0; j < j1; ++j) {
+                    const int it = k.contrib[j];
+                    const int p = it >> 2;
+                    if (!mask_bit(k.mask, k.W, s, p)) continue;
+                    const float* r = RS + (p - p0) * 4 * 64 + lane;
+                    const bool side = (it >> 1) & 1;
+                    if (mov) {
+                        const float rx = r[0], ry = r[64];
+                        fx = fx + (side ? -rx : rx);
+                        fy = fy + (side ? -ry : ry);
+                    }
+                    if (rotb && (it & 1)) tq = tq + (side ? r[192] : r[128]);
+                }
+                if (c + 1 < k.n_chunks) {
+                    acc[0] = fx; acc[64] = fy; acc[128] = tq;
+                } else {
+                    V2 p = mk(sb[0], sb[64]), v = mk(sb[128], sb[192]);
+                    float rot = sb[256], w = sb[320];
+                    integrate(d, s, k.sdt, fx, fy, tq, k.has_xs != 0, k.xs, k.has_ys != 0, k.ys,
+                              p, v, rot, w);
+                    sb[0] = p.x; sb[64] = p.y; sb[128] = v.x; sb[192] = v.y; sb[256] = rot; sb[320] = w;
+                    const int ts = k.trig[e];
+                    if (ts >= 0 && (d.flags & VMAS_F_ROTATABLE)) {
+                        const Trig t = make_trig(rot);
+                        float* tt = TR + ts * 4 * 64 + lane;
+                        tt[0] = t.c0; tt[64] = t.s0; tt[128] = t.c1; tt[192] = t.s1;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // ---- write back the integrated fields into fresh tensors
+    if (valid) {
+        for (int i = wave; i < k.n_dyn; i += nw) {
+            const int e = k.dyn[i];
+            const VmasEntityDesc d = k.ed[e];
+            const float* sb = SB + e * 6 * 64 + lane;
+            if (d.out_lin >= 0) {
+                reinterpret_cast<float2*>(k.out_pos)[(size_t)d.out_lin * k.B + b] = make_float2(sb[0], sb[64]);
+                reinterpret_cast<float2*>(k.out_vel)[(size_t)d.out_lin * k.B + b] = make_float2(sb[128], sb[192]);
+            }
+            if (d.out_rot >= 0) {
+                k.out_rot[(size_t)d.out_rot * k.B + b] = sb[256];
+                k.out_ang[(size_t)d.out_rot * k.B + b] = sb[320];
+            }
+            if (d.agent_index >= 0) {
+                const float* af = AF + d.agent_index * 3 * 64 + lane;
+                if (d.out_force >= 0)
+                    reinterpret_cast<float2*>(k.out_force)[(size_t)d.out_force * k.B + b] = make_float2(af[0], af[64]);
+                if (d.out_torque >= 0) k.out_torque[(size_t)d.out_torque * k.B + b] = af[128];
+            }
+        }
+    }
+    if (k.blk) {
+        __syncthreads();
+        uint32_t* dst = k.blk + (size_t)blockIdx.x * nfl;
+        for (int i = threadIdx.x; i < nfl; i += blockDim.x) dst[i] = FL[i];
+    }
+}
+
+// OR the per-block activity words, decide whether the mask was a fixed point, update it if not.
+// blk: [nblk][2][S][W]  (R words then Z words).  One workgroup.
+__global__ void __launch_bounds__(256) k_flags_reduce(const uint32_t* blk, int nblk, int S, int W,
+                                                      uint32_t* mask, uint32_t* viol_out) {
+    __shared__ uint32_t R[1024], Z[1024];
+    __shared__ uint32_t viol;
+    const int nwords = S * W;
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) { R[w] = 0u; Z[w] = 0u; }
+    if (threadIdx.x == 0) viol = 0u;
+    __syncthreads();
+    for (int w = 0; w < nwords; ++w) {
+        uint32_t r = 0u, z = 0u;
+        for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+            r |= blk[(size_t)i * 2 * nwords + w];
+            z |= blk[(size_t)i * 2 * nwords + nwords + w];
+        }
+        if (r) atomicOr(&R[w], r);
+        if (z) atomicOr(&Z[w], z);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        const uint32_t m = mask[w];
+        if ((m & ~R[w] & Z[w]) | (~m & R[w])) atomicOr(&viol, 1u);
+    }
+    __syncthreads();
+    if (viol)
+        for (int w = threadIdx.x; w < nwords; w += blockDim.x) mask[w] = R[w];
+    if (threadIdx.x == 0) *viol_out = viol;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host backend: identical arithmetic, one environment at a time.
+struct RowsH {
+    const V2* P;
+    const float* ROT;
+    const Trig* T;
+    V2 pos(int e) const { return P[e]; }
+    float rot(int e) const { return ROT[e]; }
+    Trig tr(int e) const { return T[e]; }
+};
+
+static inline V2 hload2(const float* p, int s0, int s1, int b) {
+    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);
+}
+
+static void host_step_env(const VmasWorld& W, const VmasStepIO& io, const uint32_t* mask,
+                          uint32_t* R, uint32_t* Z, int b, std::vector<float>& scratch) {
+    const int E = W.cfg.n_entities, A = W.cfg.n_agents, P = W.cfg.n_pairs;
+    const int S = io.substeps;
+    scratch.resize((size_t)E * 16 + (size_t)A * 3 + (size_t)P * 4);
+    V2* pos = reinterpret_cast<V2*>(scratch.data());
+    V2* vel = pos + E;
+    float* rot = reinterpret_cast<float*>(vel + E);
+    float* ang = rot + E;
+    Trig* tr = reinterpret_cast<Trig*>(ang + E);
+    float* af = reinterpret_cast<float*>(tr + E);  // [A][3]
+    PairOut* res = reinterpret_cast<PairOut*>(af + A * 3);
+    const WorldK wk{W.cfg.contact_margin, W.cfg.collision_force, W.cfg.joint_force,
+                    W.cfg.torque_constraint_force};
+    for (int e = 0; e < E; ++e) {
+        const VmasEntityIO& x = io.entities[e];
+        pos[e] = hload2(x.pos, x.pos_s0, x.pos_s1, b);
+        vel[e] = hload2(x.vel, x.vel_s0, x.vel_s1, b);
+        rot[e] = x.rot[(long)b * x.rot_s0];
+        ang[e] = x.ang_vel[(long)b * x.ang_s0];
+        if (W.trig_slot[e] >= 0) tr[e] = make_trig(rot[e]);
+    }
+    for (int a = 0; a < A; ++a) {
+        const VmasAgentIO& x = io.agents[a];
+        const V2 f = hload2(x.force, x.force_s0, x.force_s1, b);
+        af[a * 3 + 0] = f.x;
+        af[a * 3 + 1] = f.y;
+        af[a * 3 + 2] = x.torque[(long)b * x.torque_s0];
+    }
+    const RowsH g{pos, rot, tr};
+    const int Wd = W.W;
+    for (int s = 0; s < S; ++s) {
+        for (int p = 0; p < P; ++p) {
+            const VmasPairDesc& pd = W.pd[p];
+            bool inr = true;
+            if (pd.cls != VMAS_PAIR_JOINT) inr = norm(pos[pd.ea] - pos[pd.eb]) <= pd.bp_radius;
+            if (R && inr) R[s * Wd + (p >> 5)] |= 1u << (p & 31);
+            if (!((mask[s * Wd + (p >> 5)] >> (p & 31)) & 1u)) continue;
+            float fixed_rot = 0.f;
+            if (pd.cls == VMAS_PAIR_JOINT) {
+                const VmasJointIO* j = io.joints ? &io.joints[pd.joint] : nullptr;
+                fixed_rot = (j && j->fixed_rotation) ? j->fixed_rotation[(long)b * j->s0]
+                                                     : W.jd[pd.joint].fixed_rotation;
+            }
+            const PairOut o = eval_pair(pd, W.ed.data(), W.jd.data(), g, wk, fixed_rot);
+            res[p] = o;
+            if (Z && pd.cls != VMAS_PAIR_JOINT && !inr &&
+                (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || o.tb != 0.f))
+                Z[s * Wd + (p >> 5)] |= 1u << (p & 31);
+        }
+        for (size_t i = 0; i < W.dyn.size(); ++i) {
+            const int e = W.dyn[i];
+            const VmasEntityDesc& d = W.ed[e];
+            V2 a2 = mk(0.f, 0.f);
+            float at = 0.f;
+            if (d.agent_index >= 0) {
+                a2 = mk(af[d.agent_index * 3], af[d.agent_index * 3 + 1]);
+                at = af[d.agent_index * 3 + 2];
+            }
+            V2 eg = mk(0.f, 0.f);
+            const bool has_eg = (d.flags & VMAS_F_GRAVITY) != 0;
+            if (has_eg) {
+                const VmasEntityIO& x = io.entities[e];
+                eg = hload2(x.gravity, x.grav_s0, x.grav_s1, b);
+            }
+            float fx, fy, tq;
+            pre_forces(d, d.agent_index >= 0, a2, at, vel[e], ang[e], eg, has_eg,
+                       W.cfg.gravity_x, W.cfg.gravity_y, W.cfg.has_world_gravity != 0, io.sub_dt,
+                       fx, fy, tq);
+            if (d.agent_index >= 0) {
+                af[d.agent_index * 3] = a2.x;
+                af[d.agent_index * 3 + 1] = a2.y;
+                af[d.agent_index * 3 + 2] = at;
+            }
+            const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+            for (int it : W.items[i]) {
+                const int p = it >> 2;
+                if (!((mask[s * Wd + (p >> 5)] >> (p & 31)) & 1u)) continue;
+                const bool side = (it >> 1) & 1;
+                if (mov) {
+                    fx = fx + (side ? -res[p].fa.x : res[p].fa.x);
+                    fy = fy + (side ? -res[p].fa.y : res[p].fa.y);
+                }
+                if (rotb && (it & 1)) tq = tq + (side ? res[p].tb : res[p].ta);
+            }
+            // integration must not disturb other entities' substep-start state: stage it
+            V2 p2 = pos[e], v2 = vel[e];
+            float r2 = rot[e], w2 = ang[e];
+            integrate(d, s, io.sub_dt, fx, fy, tq, W.cfg.has_x_semidim != 0, W.cfg.x_semidim,
+                      W.cfg.has_y_semidim != 0, W.cfg.y_semidim, p2, v2, r2, w2);
+            // pairs of this substep are already evaluated; entity pre-forces read only own state
+            pos[e] = p2;
+            vel[e] = v2;
+            rot[e] = r2;
+            ang[e] = w2;
+            if (W.trig_slot[e] >= 0 && (d.flags & VMAS_F_ROTATABLE)) tr[e] = make_trig(r2);
+        }
+    }
+    const int B = W.cfg.batch;
+    for (size_t i = 0; i < W.dyn.size(); ++i) {
+        const int e = W.dyn[i];
+        const VmasEntityDesc& d = W.ed[e];
+        if (d.out_lin >= 0) {
+            io.out_pos[((size_t)d.out_lin * B + b) * 2] = pos[e].x;
+            io.out_pos[((size_t)d.out_lin * B + b) * 2 + 1] = pos[e].y;
+            io.out_vel[((size_t)d.out_lin * B + b) * 2] = vel[e].x;
+            io.out_vel[((size_t)d.out_lin * B + b) * 2 + 1] = vel[e].y;
+        }
+        if (d.out_rot >= 0) {
+            io.out_rot[(size_t)d.out_rot * B + b] = rot[e];
+            io.out_ang_vel[(size_t)d.out_rot * B + b] = ang[e];
+        }
+        if (d.agent_index >= 0) {
+            if (d.out_force >= 0) {
+                io.out_force[((size_t)d.out_force * B + b) * 2] = af[d.agent_index * 3];
+                io.out_force[((size_t)d.out_force * B + b) * 2 + 1] = af[d.agent_index * 3 + 1];
+            }
+            if (d.out_torque >= 0) io.out_torque[(size_t)d.out_torque * B + b] = af[d.agent_index * 3 + 2];
+        }
+    }
+}
+
+static int32_t host_step(VmasWorld& W, const VmasStepIO& io, int32_t* iterations) {
+    const int B = W.cfg.batch, S = io.substeps, Wd = W.W;
+    const int nwords = S * Wd;
+    std::vector<uint32_t> mask(nwords, 0xFFFFFFFFu);
+    const bool batch_bp = io.broadphase == VMAS_BROADPHASE_BATCH;
+    Pool& pool = Pool::get();
+    const int nchunks = std::min(B, pool.size() * 4);
+    const int per = (B + nchunks - 1) / nchunks;
+    std::vector<uint32_t> RZ((size_t)nchunks * 2 * nwords);
+    const int max_it = S + 2;
+    for (int it = 0; it < max_it; ++it) {
+        std::fill(RZ.begin(), RZ.end(), 0u);
+        pool.run(nchunks, [&](int c) {
+            std::vector<float> scratch;
+            uint32_t* R = batch_bp ? &RZ[(size_t)c * 2 * nwords] : nullptr;
+            uint32_t* Z = batch_bp ? R + nwords : nullptr;
+            const int b0 = c * per, b1 = std::min(B, b0 + per);
+            for (int b = b0; b < b1; ++b) host_step_env(W, io, mask.data(), R, Z, b, scratch);
+        });
+        if (iterations) *iterations = it + 1;
+        if (!batch_bp) return VMAS_OK;
+        std::vector<uint32_t> Rt(nwords, 0u), Zt(nwords, 0u);
+        for (int c = 0; c < nchunks; ++c)
+            for (int w = 0; w < nwords; ++w) {
+                Rt[w] |= RZ[(size_t)c * 2 * nwords + w];
+                Zt[w] |= RZ[(size_t)c * 2 * nwords + nwords + w];
+            }
+        bool viol = false;
+        for (int w = 0; w < nwords; ++w)
+            if ((mask[w] & ~Rt[w] & Zt[w]) | (~mask[w] & Rt[w])) viol = true;
+        if (!viol) return VMAS_OK;
+        mask = Rt;
+    }
+    return fail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
+}
+
+// ------------------------------------------------------------------------------------------------
+// Ray casting: one thread per (env, ray)
+struct RayK {
+    const VmasRayTarget* tg;
+    int nt, B, R;
+    const float* origin;
+    int o_s0, o_s1;
+    const float* ang;
+    int a_s0, a_s1;
+    const float* rot;
+    int r_s0;
+    float max_range;
+    float* out;
+};
+
+__host__ __device__ __forceinline__ float cast_one(const VmasRayTarget* tg, int nt, V2 o, float ang,
+                                                   int b, float max_range) {
+    const float dc = cosf(ang), ds = sinf(ang);
+    float best = max_range;
+    for (int t = 0; t < nt; ++t) {
+        const VmasRayTarget& x = tg[t];
+        const V2 tp = mk(x.pos[(long)b * x.pos_s0], x.pos[(long)b * x.pos_s0 + x.pos_s1]);
+        float d;
+        if (x.shape == VMAS_SPHERE) {
+            d = ray_sphere(o, dc, ds, tp, x.radius, max_range);
+        } else if (x.shape == VMAS_BOX) {
+            d = ray_box(o, ang, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, x.width, max_range);
+        } else {
+            d = ray_line(o, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, max_range);
+        }
+        best = tmin(best, d);
+    }
+    return best;
+}
+
+__global__ void __launch_bounds__(256) k_cast_rays(RayK k) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)k.B * k.R) return;
+    const int b = (int)(idx / k.R), r = (int)(idx - (long)b * k.R);
+    const V2 o = mk(k.origin[(long)b * k.o_s0], k.origin[(long)b * k.o_s0 + k.o_s1]);
+    float a = k.ang[(long)b * k.a_s0 + (long)r * k.a_s1];
+    if (k.rot) a = a + k.rot[(long)b * k.r_s0];
+    k.out[idx] = cast_one(k.tg, k.nt, o, a, b, k.max_range);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Distance queries: one thread per env
+__host__ __device__ __forceinline__ V2 ref_pos(const VmasShapeRef& s, int b) {
+    return mk(s.pos[(long)b * s.pos_s0], s.pos[(long)b * s.pos_s0 + s.pos_s1]);
+}
+__host__ __device__ __forceinline__ float ref_rot(const VmasShapeRef& s, int b) {
+    return s.rot ? s.rot[(long)b * s.rot_s0] : 0.f;
+}
+
+// get_distance_from_point (core.py:1787-1819)
+__host__ __device__ __forceinline__ float dist_point(const VmasShapeRef& a, int b, V2 tp) {
+    const V2 p = ref_pos(a, b);
+    if (a.shape == VMAS_SPHERE) return norm(p - tp) - a.radius;
+    if (a.shape == VMAS_BOX) {
+        const V2 cp = closest_point_box(p, make_trig(ref_rot(a, b)), a.length / 2.f, a.width / 2.f, tp);
+        return norm(tp - cp) - kLineMinDist;
+    }
+    const float r = ref_rot(a, b);
+    const V2 cp = closest_point_line(p, mk(cosf(r), sinf(r)), a.length / 2.f, tp, true);
+    return norm(tp - cp) - kLineMinDist;
+}
+
+// is_overlapping for (box, sphere) (core.py:1932-1963)
+__host__ __device__ __forceinline__ bool overlap_box_sphere(const VmasShapeRef& bx, const VmasShapeRef& sp, int b) {
+    const V2 pb = ref_pos(bx, b), ps = ref_pos(sp, b);
+    const V2 cp = closest_point_box(pb, make_trig(ref_rot(bx, b)), bx.length / 2.f, bx.width / 2.f, ps);
+    const float dsc = norm(ps - cp), dsb = norm(ps - pb), dcb = norm(pb - cp);
+    return (dsb < dcb) || (dsc < sp.radius_lmd);
+}
+
+// get_distance (core.py:1821-1904); a/b are canonicalised by the caller as the reference does
+__host__ __device__ __forceinline__ float dist_pair(const VmasShapeRef& a, const VmasShapeRef& bref, int b) {
+    const int sa = a.shape, sb = bref.shape;
+    if (sa == VMAS_SPHERE && sb == VMAS_SPHERE) return dist_point(a, b, ref_pos(bref, b)) - bref.radius;
+    if (sa == VMAS_BOX && sb == VMAS_SPHERE) {
+        float d = dist_point(a, b, ref_pos(bref, b)) - bref.radius;
+        if (overlap_box_sphere(a, bref, b)) d = -1.f;
+        return d;
+    }
+    if (sa == VMAS_LINE && sb == VMAS_SPHERE) return dist_point(a, b, ref_pos(bref, b)) - bref.radius;
+    const float ra = ref_rot(a, b), rb = ref_rot(bref, b);
+    const V2 pa = ref_pos(a, b), pb = ref_pos(bref, b);
+    V2 qa, qb;
+    if (sa == VMAS_LINE && sb == VMAS_LINE) {
+        closest_points_line_line(Seg{pa, mk(cosf(ra), sinf(ra)), a.length / 2.f},
+                                 Seg{pb, mk(cosf(rb), sinf(rb)), bref.length / 2.f}, &qa, &qb);
+    } else if (sa == VMAS_BOX && sb == VMAS_LINE) {
+        closest_line_box(pa, make_trig(ra), a.length / 2.f, a.width / 2.f,
+                         Seg{pb, mk(cosf(rb), sinf(rb)), bref.length / 2.f}, &qa, &qb);
+    } else {  // box, box
+        closest_box_box(pa, make_trig(ra), a.length / 2.f, a.width / 2.f, pb, make_trig(rb),
+                        bref.length / 2.f, bref.width / 2.f, &qa, &qb);
+    }
+    return norm(qa - qb) - kLineMinDist;
+}
+
+__host__ __device__ __forceinline__ float distance_query(int kind, const VmasShapeRef& a,
+                                                         const VmasShapeRef& bref, const float* tp,
+                                                         int tp_s0, int tp_s1, int b) {
+    if (kind == VMAS_DIST_POINT) return dist_point(a, b, mk(tp[(long)b * tp_s0], tp[(long)b * tp_s0 + tp_s1]));
+    if (kind == VMAS_DIST_PAIR) return dist_pair(a, bref, b);
+    // overlap
+    if (a.shape == VMAS_BOX && bref.shape == VMAS_SPHERE) return overlap_box_sphere(a, bref, b) ? 1.f : 0.f;
+    return (dist_pair(a, bref, b) < 0.f) ? 1.f : 0.f;
+}
+
+__host__ __device__ __forceinline__ void store_query(void* out, int kind, int b, float v) {
+    if (kind == VMAS_OVERLAP_PAIR) reinterpret_cast<uint8_t*>(out)[b] = v != 0.f;  // torch.bool
+    else reinterpret_cast<float*>(out)[b] = v;
+}
+
+__global__ void __launch_bounds__(256) k_distance(int B, int kind, VmasShapeRef a, VmasShapeRef bref,
+                                                  const float* tp, int tp_s0, int tp_s1, void* out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    store_query(out, kind, b, distance_query(kind, a, bref, tp, tp_s0, tp_s1, b));
+}
+
+// ================================================================================================
+// C ABI
+extern "C" {
+
+int32_t vmas_abi_version(void) { return VMAS_ABI_VERSION; }
+
+int32_t vmas_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* vmas_last_error(void) { return g_err.c_str(); }
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                          const VmasPairDesc* pairs, const VmasJointDesc* joints,
+                          VmasWorld** out_world) {
+    if (!cfg || !out_world) return fail(VMAS_E_INVALID, "null argument");
+    if (cfg->batch <= 0 || cfg->n_entities < 0 || cfg->n_pairs < 0 || cfg->n_agents < 0 ||
+        cfg->n_joints < 0 || cfg->max_substeps <= 0)
+        return fail(VMAS_E_INVALID, "bad world config");
+    auto* W = new VmasWorld();
+    W->cfg = *cfg;
+    W->ed.assign(entities, entities + cfg->n_entities);
+    W->pd.assign(pairs, pairs + cfg->n_pairs);
+    if (cfg->n_joints) W->jd.assign(joints, joints + cfg->n_joints);
+    const int E = cfg->n_entities, P = cfg->n_pairs;
+    for (int p = 0; p < P; ++p) {
+        const VmasPairDesc& pd = W->pd[p];
+        if (pd.ea < 0 || pd.ea >= E || pd.eb < 0 || pd.eb >= E || pd.cls < 0 || pd.cls > 6 ||
+            (pd.cls == VMAS_PAIR_JOINT && (pd.joint < 0 || pd.joint >= cfg->n_joints))) {
+            delete W;
+            return fail(VMAS_E_INVALID, "bad pair %d", p);
+        }
+    }
+    W->trig_slot.assign(E, -1);
+    auto need_trig = [&](int e) {
+        if (W->trig_slot[e] < 0) W->trig_slot[e] = W->n_trig++;
+    };
+    for (int e = 0; e < E; ++e)
+        if (W->ed[e].shape != VMAS_SPHERE) need_trig(e);
+    for (int p = 0; p < P; ++p)
+        if (W->pd[p].cls == VMAS_PAIR_JOINT) { need_trig(W->pd[p].ea); need_trig(W->pd[p].eb); }
+    for (int e = 0; e < E; ++e)
+        if (W->ed[e].flags & (VMAS_F_MOVABLE | VMAS_F_ROTATABLE)) W->dyn.push_back(e);
+    // contribution lists in pair order
+    W->items.resize(W->dyn.size());
+    for (size_t i = 0; i < W->dyn.size(); ++i) {
+        const int e = W->dyn[i];
+        for (int p = 0; p < P; ++p) {
+            const VmasPairDesc& pd = W->pd[p];
+            for (int side = 0; side < 2; ++side) {
+                if ((side ? pd.eb : pd.ea) != e) continue;
+                // which side carries a torque (spheres in SS/LS/BS receive torque 0, core.py:2330-2338,2383-2391,2543-2551)
+                int tq = 1;
+                if (pd.cls == VMAS_PAIR_SS) tq = 0;
+                if ((pd.cls == VMAS_PAIR_LS || pd.cls == VMAS_PAIR_BS) && side == 1) tq = 0;
+                W->items[i].push_back((p << 2) | (side << 1) | tq);
+            }
+        }
+    }
+    W->W = std::max(1, (P + 31) / 32);
+    if ((size_t)cfg->max_substeps * W->W > 1024) {
+        delete W;
+        return fail(VMAS_E_INVALID, "max_substeps * ceil(pairs/32) must be <= 1024");
+    }
+    const int B = cfg->batch;
+    const int n_dyn = (int)W->dyn.size();
+    if (cfg->device >= 0) {
+        if (int32_t rc = use_device(cfg->device)) { delete W; return rc; }
+        // launch geometry: chunk of pairs whose result rows fit the LDS budget
+        W->nw = 8;
+        const size_t fixed_rows = (size_t)E * 6 + (size_t)W->n_trig * 4 + (size_t)n_dyn * 3 +
+                                  (size_t)cfg->n_agents * 3;
+        const size_t flags_bytes = align_up((size_t)2 * cfg->max_substeps * W->W * 4, 16);
+        const size_t budget = 96 * 1024;
+        int chunk = std::max(1, P);
+        while (chunk > 8 && (fixed_rows + (size_t)chunk * 4) * 256 + flags_bytes > budget) chunk = (chunk + 1) / 2;
+        W->chunk = chunk;
+        W->n_chunks = std::max(1, (P + chunk - 1) / chunk);
+        W->lds_state_floats = (fixed_rows + (size_t)chunk * 4) * 64;
+        W->global_scratch = W->lds_state_floats * 4 + flags_bytes > 160 * 1024 - 1024;
+        // per-(dyn entity, chunk) item ranges
+        W->contrib_off.assign((size_t)n_dyn * (W->n_chunks + 1), 0);
+        for (int i = 0; i < n_dyn; ++i) {
+            const auto& it = W->items[i];
+            size_t j = 0;
+            for (int c = 0; c <= W->n_chunks; ++c) {
+                const int plim = std::min(P, c * chunk);
+                while (j < it.size() && (it[j] >> 2) < plim) ++j;
+                W->contrib_off[(size_t)i * (W->n_chunks + 1) + c] = (int32_t)(W->contrib.size() + j);
+            }
+            W->contrib.insert(W->contrib.end(), it.begin(), it.end());
+        }
+        // one allocation for all tables
+        size_t off = 0;
+        const size_t o_ed = off; off = align_up(off + sizeof(VmasEntityDesc) * std::max(E, 1), 64);
+        const size_t o_pd = off; off = align_up(off + sizeof(VmasPairDesc) * std::max(P, 1), 64);
+        const size_t o_jd = off; off = align_up(off + sizeof(VmasJointDesc) * std::max(cfg->n_joints, 1), 64);
+        const size_t o_dyn = off; off = align_up(off + 4 * std::max(n_dyn, 1), 64);
+        const size_t o_trig = off; off = align_up(off + 4 * std::max(E, 1), 64);
+        const size_t o_c = off; off = align_up(off + 4 * std::max<size_t>(W->contrib.size(), 1), 64);
+        const size_t o_co = off; off = align_up(off + 4 * std::max<size_t>(W->contrib_off.size(), 1), 64);
+        std::vector<char> h(off, 0);
+        memcpy(h.data() + o_ed, W->ed.data(), sizeof(VmasEntityDesc) * E);
+        memcpy(h.data() + o_pd, W->pd.data(), sizeof(VmasPairDesc) * P);
+        if (cfg->n_joints) memcpy(h.data() + o_jd, W->jd.data(), sizeof(VmasJointDesc) * cfg->n_joints);
+        memcpy(h.data() + o_dyn, W->dyn.data(), 4 * n_dyn);
+        memcpy(h.data() + o_trig, W->trig_slot.data(), 4 * E);
+        memcpy(h.data() + o_c, W->contrib.data(), 4 * W->contrib.size());
+        memcpy(h.data() + o_co, W->contrib_off.data(), 4 * W->contrib_off.size());
+        auto cleanup = [&](int32_t rc) { vmas_world_destroy(W); return rc; };
+        if (hipMalloc((void**)&W->d_tables, off) != hipSuccess) return cleanup(fail(VMAS_E_NOMEM, "hipMalloc tables"));
+        if (hipMemcpy(W->d_tables, h.data(), off, hipMemcpyHostToDevice) != hipSuccess)
+            return cleanup(fail(VMAS_E_HIP, "hipMemcpy tables"));
+        W->d_ed = (const VmasEntityDesc*)(W->d_tables + o_ed);
+        W->d_pd = (const VmasPairDesc*)(W->d_tables + o_pd);
+        W->d_jd = (const VmasJointDesc*)(W->d_tables + o_jd);
+        W->d_dyn = (const int32_t*)(W->d_tables + o_dyn);
+        W->d_trig = (const int32_t*)(W->d_tables + o_trig);
+        W->d_contrib = (const int32_t*)(W->d_tables + o_c);
+        W->d_contrib_off = (const int32_t*)(W->d_tables + o_co);
+        W->nblk = (B + 63) / 64;
+        const size_t nwords = (size_t)cfg->max_substeps * W->W;
+        if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
+            hipMalloc((void**)&W->d_blk, (size_t)W->nblk * 2 * nwords * 4) != hipSuccess ||
+            hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
+            hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
+            return cleanup(fail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
+        if (W->global_scratch) {
+            if (hipMalloc((void**)&W->d_scratch, (size_t)W->nblk * W->lds_state_floats * 4) != hipSuccess)
+                return cleanup(fail(VMAS_E_NOMEM, "hipMalloc state scratch"));
+        }
+        // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); harmless if refused
+        (void)hipFuncSetAttribute((const void*)k_step, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipGetLastError();
+    }
+    *out_world = W;
+    return VMAS_OK;
+}
+
+int32_t vmas_world_destroy(VmasWorld* W) {
+    if (!W) return VMAS_OK;
+    if (W->cfg.device >= 0) {
+        use_device(W->cfg.device);
+        if (W->d_tables) (void)hipFree(W->d_tables);
+        if (W->d_mask) (void)hipFree(W->d_mask);
+        if (W->d_blk) (void)hipFree(W->d_blk);
+        if (W->d_viol) (void)hipFree(W->d_viol);
+        if (W->h_viol) (void)hipHostFree(W->h_viol);
+        if (W->d_scratch) (void)hipFree(W->d_scratch);
+    }
+    delete W;
+    return VMAS_OK;
+}
+
+int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32_t* iterations) {
+    if (!W || !io) return fail(VMAS_E_INVALID, "null argument");
+    const VmasWorldConfig& cfg = W->cfg;
+    if (io->substeps <= 0 || io->substeps > cfg.max_substeps)
+        return fail(VMAS_E_INVALID, "substeps %d outside [1, %d]", io->substeps, cfg.max_substeps);
+    if (cfg.n_entities == 0) return VMAS_OK;
+    if (cfg.device < 0) return host_step(*W, *io, iterations);
+
+    hipStream_t stream = (hipStream_t)stream_;
+    if (int32_t rc = use_device(cfg.device)) return rc;
+    // upload the per-call pointer tables in one slot
+    const int E = cfg.n_entities, A = cfg.n_agents, J = cfg.n_joints;
+    const size_t be = sizeof(VmasEntityIO) * E, ba = sizeof(VmasAgentIO) * A, bj = sizeof(VmasJointIO) * J;
+    const size_t oa = align_up(be, 16), oj = align_up(oa + ba, 16), tot = std::max<size_t>(oj + bj, 16);
+    char buf[kSlot];
+    if (tot > kSlot) return fail(VMAS_E_INVALID, "too many entities for one pointer table");
+    memcpy(buf, io->entities, be);
+    if (A) memcpy(buf + oa, io->agents, ba);
+    if (J) memcpy(buf + oj, io->joints, bj);
+    const void* dtab = nullptr;
+    if (int32_t rc = ring_upload(cfg.device, buf, tot, stream, &dtab)) return rc;
+
+    StepK k{};
+    k.ed = W->d_ed; k.pd = W->d_pd; k.jd = W->d_jd; k.dyn = W->d_dyn; k.trig = W->d_trig;
+    k.contrib = W->d_contrib; k.contrib_off = W->d_contrib_off;
+    k.eio = (const VmasEntityIO*)dtab;
+    k.aio = (const VmasAgentIO*)((const char*)dtab + oa);
+    k.jio = (const VmasJointIO*)((const char*)dtab + oj);
+    k.out_pos = io->out_pos; k.out_vel = io->out_vel; k.out_rot = io->out_rot;
+    k.out_ang = io->out_ang_vel; k.out_force = io->out_force; k.out_torque = io->out_torque;
+    k.mask = W->d_mask;
+    const bool batch_bp = io->broadphase == VMAS_BROADPHASE_BATCH;
+    k.blk = batch_bp ? W->d_blk : nullptr;
+    k.scratch = W->global_scratch ? W->d_scratch : nullptr;
+    k.scratch_floats = W->lds_state_floats;
+    k.B = cfg.batch; k.E = E; k.A = A; k.P = cfg.n_pairs; k.W = W->W; k.S = io->substeps;
+    k.n_dyn = (int)W->dyn.size(); k.n_trig = W->n_trig; k.chunk = W->chunk; k.n_chunks = W->n_chunks;
+    k.sdt = io->sub_dt;
+    k.wk = WorldK{cfg.contact_margin, cfg.collision_force, cfg.joint_force, cfg.torque_constraint_force};
+    k.gx = cfg.gravity_x; k.gy = cfg.gravity_y; k.has_g = cfg.has_world_gravity;
+    k.xs = cfg.x_semidim; k.ys = cfg.y_semidim; k.has_xs = cfg.has_x_semidim; k.has_ys = cfg.has_y_semidim;
+
+    const size_t flags_bytes = align_up((size_t)2 * io->substeps * W->W * 4, 16);
+    const size_t lds = flags_bytes + (W->global_scratch ? 0 : W->lds_state_floats * 4);
+    const size_t nwords = (size_t)io->substeps * W->W;
+    HIP_TRY(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
+    const int max_it = batch_bp ? io->substeps + 2 : 1;
+    for (int it = 0; it < max_it; ++it) {
+        hipLaunchKernelGGL(k_step, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
+        HIP_TRY(hipGetLastError());
+        if (iterations) *iterations = it + 1;
+        if (!batch_bp) return VMAS_OK;
+        hipLaunchKernelGGL(k_flags_reduce, dim3(1), dim3(256), 0, stream, (const uint32_t*)W->d_blk,
+                           W->nblk, io->substeps, W->W, W->d_mask, W->d_viol);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(W->h_viol, W->d_viol, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (*W->h_viol == 0u) return VMAS_OK;
+    }
+    return fail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
+}
+
+int32_t vmas_cast_rays(int32_t device, int32_t batch, int32_t n_rays, const float* origin,
+                       int32_t origin_s0, int32_t origin_s1, const float* angles, int32_t ang_s0,
+                       int32_t ang_s1, const float* rot_offset, int32_t rot_s0,
+                       const VmasRayTarget* targets, int32_t n_targets, float max_range,
+                       float* out, void* stream_) {
+    if (batch <= 0 || n_rays <= 0) return VMAS_OK;
+    if (!origin || !angles || !out || (n_targets > 0 && !targets)) return fail(VMAS_E_INVALID, "null argument");
+    RayK k{};
+    k.nt = n_targets; k.B = batch; k.R = n_rays; k.origin = origin; k.o_s0 = origin_s0; k.o_s1 = origin_s1;
+    k.ang = angles; k.a_s0 = ang_s0; k.a_s1 = ang_s1; k.rot = rot_offset; k.r_s0 = rot_s0;
+    k.max_range = max_range; k.out = out;
+    if (device < 0) {
+        const long n = (long)batch * n_rays;
+        Pool& pool = Pool::get();
+        const int nch = (int)std::min<long>(n, pool.size() * 4);
+        const long per = (n + nch - 1) / nch;
+        pool.run(nch, [&](int c) {
+            for (long idx = c * per; idx < std::min(n, (c + 1) * per); ++idx) {
+                const int b = (int)(idx / n_rays), r = (int)(idx % n_rays);
+                const V2 o = mk(origin[(long)b * origin_s0], origin[(long)b * origin_s0 + origin_s1]);
+                float a = angles[(long)b * ang_s0 + (long)r * ang_s1];
+                if (rot_offset) a = a + rot_offset[(long)b * rot_s0];
+                out[idx] = cast_one(targets, n_targets, o, a, b, max_range);
+            }
+        });
+        return VMAS_OK;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    if (int32_t rc = use_device(device)) return rc;
+    const void* dt = nullptr;
+    if (n_targets > 0) {
+        if (int32_t rc = ring_upload(device, targets, sizeof(VmasRayTarget) * n_targets, stream, &dt)) return rc;
+    }
+    k.tg = (const VmasRayTarget*)dt;
+    const long n = (long)batch * n_rays;
+    hipLaunchKernelGGL(k_cast_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, k);
+    HIP_TRY(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
+                      const VmasShapeRef* b, const float* test_point, int32_t tp_s0,
+                      int32_t tp_s1, void* out, void* stream_) {
+    if (batch <= 0) return VMAS_OK;
+    if (!a || !out || (kind == VMAS_DIST_POINT && !test_point) || (kind != VMAS_DIST_POINT && !b))
+        return fail(VMAS_E_INVALID, "null argument");
+    VmasShapeRef bb{};
+    if (b) bb = *b;
+    if (device < 0) {
+        Pool& pool = Pool::get();
+        const int nch = std::min(batch, pool.size() * 4);
+        const int per = (batch + nch - 1) / nch;
+        pool.run(nch, [&](int c) {
+            for (int i = c * per; i < std::min(batch, (c + 1) * per); ++i)
+                store_query(out, kind, i, distance_query(kind, *a, bb, test_point, tp_s0, tp_s1, i));
+        });
+        return VMAS_OK;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    if (int32_t rc = use_device(device)) return rc;
+    hipLaunchKernelGGL(k_distance, dim3((batch + 255) / 256), dim3(256), 0, stream, batch, kind, *a,
+                       bb, test_point, tp_s0, tp_s1, out);
+    HIP_TRY(hipGetLastError());
+    return VMAS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,413 @@
+// vmas_physics.hpp -- scalar fp32 physics of one environment, compiled for both gfx950 (kernels in
+// vmas_kernels.hip) and the host (the device == -1 backend in the same translation unit).
+//
+// Every function restates a PyTorch op sequence of the reference in the same left-to-right order
+// and with the same fp32 roundings (python scalars are cast to fp32 before they meet a tensor, as
+// torch's wrapped-number promotion does), so that with -ffp-contract=off the only differences
+// from torch-CPU are the last-ulp differences of sin/cos/exp/log1p/sqrt-of-reductions.
+// Citations are file:line in the reference checkout.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/vmas_mi355x.h"
+
+#define VHD __host__ __device__ __forceinline__
+
+namespace vmas {
+
+// utils.py:27 LINE_MIN_DIST = 4 / 6e2, as the f32 value torch uses when it meets a f32 tensor
+constexpr float kLineMinDist = (float)(4.0 / 6e2);
+constexpr float kHalfPi = (float)(3.141592653589793 / 2.0);  // torch.pi / 2 -> f32
+
+struct V2 {
+    float x, y;
+};
+VHD V2 mk(float x, float y) { return V2{x, y}; }
+VHD V2 operator+(V2 a, V2 b) { return V2{a.x + b.x, a.y + b.y}; }
+VHD V2 operator-(V2 a, V2 b) { return V2{a.x - b.x, a.y - b.y}; }
+VHD V2 operator-(V2 a) { return V2{-a.x, -a.y}; }
+VHD V2 operator*(V2 a, float s) { return V2{a.x * s, a.y * s}; }
+VHD V2 operator*(float s, V2 a) { return V2{s * a.x, s * a.y}; }
+VHD V2 operator/(V2 a, float s) { return V2{a.x / s, a.y / s}; }
+
+// torch.linalg.vector_norm(v, dim=-1) of a length-2 vector
+VHD float norm(V2 v) { return sqrtf(v.x * v.x + v.y * v.y); }
+// TorchUtils.cross (utils.py:194-197): a.x*b.y - a.y*b.x
+VHD float cross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
+// torch.sign: (0 < x) - (x < 0); NaN -> 0
+VHD float tsign(float x) { return (float)((0.f < x) - (x < 0.f)); }
+// torch.minimum / torch.maximum / torch.min(dim) / torch.max(dim): NaN propagating
+VHD float tmin(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
+VHD float tmax(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+// torch.clamp(x, lo, hi)
+VHD float tclamp(float x, float lo, float hi) { return tmin(tmax(x, lo), hi); }
+
+// Angle trig of one entity: cos/sin(rot) and cos/sin(rot + pi/2) (physics.py:299-301)
+struct Trig {
+    float c0, s0, c1, s1;
+};
+VHD Trig make_trig(float rot) {
+    const float r2 = rot + kHalfPi;
+    return Trig{cosf(rot), sinf(rot), cosf(r2), sinf(r2)};
+}
+
+// TorchUtils.clamp_with_norm (utils.py:168-173)
+VHD V2 clamp_with_norm(V2 t, float max_norm) {
+    const float n = norm(t);
+    const V2 nt = (t / n) * max_norm;
+    return (n > max_norm) ? nt : t;
+}
+VHD float clamp_with_norm1(float t, float max_norm) {  // [B,1] variant: norm = |t|
+    const float n = fabsf(t);
+    const float nt = (t / n) * max_norm;
+    return (n > max_norm) ? nt : t;
+}
+
+// torch.logaddexp(0, x) (ATen logaddexp kernel: m + log1p(exp(-|a-b|)))
+VHD float logaddexp0(float x) {
+    const float m = tmax(0.f, x);
+    return m + log1pf(expf(-fabsf(0.f - x)));
+}
+
+// World._get_constraint_forces (core.py:2804-2838).  Returns the force on a; b gets -force.
+// `sc` = f32(sign * force_multiplier) (a python float product), `k` = f32(contact_margin).
+VHD V2 constraint_force(V2 pa, V2 pb, float dmin, float sc, float k, bool attractive) {
+    const V2 delta = pa - pb;
+    const float dist = norm(delta);
+    const float x = attractive ? (-(dmin - dist)) / k : (dmin - dist) / k;  // (dmin-dist)*sign/k
+    const float pen = logaddexp0(x) * k;
+    const float dsafe = (dist > 0.f) ? dist : 1e-8f;
+    V2 f = mk(((sc * delta.x) / dsafe) * pen, ((sc * delta.y) / dsafe) * pen);
+    if (dist < 1e-6f) f = mk(0.f, 0.f);
+    if (!attractive) {
+        if (dist > dmin) f = mk(0.f, 0.f);
+    } else {
+        if (dist < dmin) f = mk(0.f, 0.f);
+    }
+    return f;
+}
+
+// physics._get_closest_point_line (physics.py:399-428); dir = (cos, sin) of the line rot.
+VHD V2 closest_point_line(V2 lp, V2 dir, float half, V2 tp, bool limit) {
+    const V2 d = lp - tp;
+    const float dot = d.x * dir.x + d.y * dir.y;
+    const float sg = tsign(dot);
+    const float dfc = limit ? tmin(fabsf(dot), half) : fabsf(dot);
+    const float m = sg * dfc;
+    return lp - dir * m;
+}
+
+// One side of a box as a line (physics._get_all_lines_box, physics.py:297-324)
+struct Seg {
+    V2 p;       // centre
+    V2 dir;     // (cos, sin) of the side's rot
+    float half; // half length
+};
+VHD Seg box_side(V2 pos, Trig t, float hl, float hw, int i) {
+    const V2 rv = mk(t.c0, t.s0);
+    const V2 rv2 = mk(t.c1, t.s1);
+    switch (i) {
+        case 0: return Seg{pos + rv * hl, rv2, hw};
+        case 1: return Seg{pos - rv * hl, rv2, hw};
+        case 2: return Seg{pos + rv2 * hw, rv, hl};
+        default: return Seg{pos - rv2 * hw, rv, hl};
+    }
+}
+
+// physics._get_closest_point_box (physics.py:262-294): first strict minimum over the 4 sides.
+VHD V2 closest_point_box(V2 pos, Trig t, float hl, float hw, V2 tp) {
+    V2 best = mk(INFINITY, INFINITY);
+    float bd = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const Seg s = box_side(pos, t, hl, hw, i);
+        const V2 p = closest_point_line(s.p, s.dir, s.half, tp, true);
+        const float d = norm(tp - p);
+        if (d < bd) {
+            bd = d;
+            best = p;
+        }
+    }
+    return best;
+}
+
+// physics._get_inner_point_box (physics.py:12-22)
+VHD V2 inner_point_box(V2 outside, V2 surface, V2 box_pos, float* dmag) {
+    const V2 v = surface - outside;
+    const V2 u = box_pos - surface;
+    const float vn = norm(v);
+    float xm = (v.x * u.x + v.y * u.y) / vn;
+    V2 x = (v / vn) * xm;
+    if (vn == 0.f) {
+        x = surface;  // reference quirk: x = surface_point when v_norm == 0
+        xm = 0.f;
+    }
+    *dmag = fabsf(xm);
+    return surface + x;
+}
+
+// physics._get_closest_points_line_line (physics.py:143-218) incl. _get_line_extrema and
+// _get_intersection_point_line_line (physics.py:131-140, 221-259).  Line 1 = (p1,dir1,h1).
+VHD void closest_points_line_line(Seg l1, Seg l2, V2* out1, V2* out2) {
+    const V2 xy1 = mk(l1.half * l1.dir.x, l1.half * l1.dir.y);
+    const V2 xy2 = mk(l2.half * l2.dir.x, l2.half * l2.dir.y);
+    const V2 a1 = l1.p + xy1, a2 = l1.p - xy1;  // line 1 extrema
+    const V2 b1 = l2.p + xy2, b2 = l2.p - xy2;  // line 2 extrema
+    // intersection
+    const V2 r = a2 - a1, s = b2 - b1;
+    const V2 qp = b1 - a1;
+    const float cqpr = cross(qp, r), cqps = cross(qp, s), crs = cross(r, s);
+    const float u = cqpr / crs, t = cqps / crs;
+    const bool cond = (crs != 0.f) && (0.f <= u) && (u <= 1.f) && (0.f <= t) && (t <= 1.f);
+    // end points projected on the other segment
+    const V2 a1b = closest_point_line(l2.p, l2.dir, l2.half, a1, true);
+    const V2 a2b = closest_point_line(l2.p, l2.dir, l2.half, a2, true);
+    const V2 b1a = closest_point_line(l1.p, l1.dir, l1.half, b1, true);
+    const V2 b2a = closest_point_line(l1.p, l1.dir, l1.half, b2, true);
+    V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
+    float md = INFINITY, d;
+    d = norm(a1 - a1b);
+    if (d < md) { md = d; c1 = a1; c2 = a1b; }
+    d = norm(a2 - a2b);
+    if (d < md) { md = d; c1 = a2; c2 = a2b; }
+    d = norm(b1a - b1);
+    if (d < md) { md = d; c1 = b1a; c2 = b1; }
+    d = norm(b2a - b2);
+    if (d < md) { md = d; c1 = b2a; c2 = b2; }
+    if (cond) {
+        const V2 pi = a1 + r * t;  // p + t * r
+        c1 = pi;
+        c2 = pi;
+    }
+    *out1 = c1;
+    *out2 = c2;
+}
+
+// physics._get_closest_line_box (physics.py:327-381): returns (point on box, point on line)
+VHD void closest_line_box(V2 bpos, Trig bt, float hl, float hw, Seg line, V2* pbox, V2* pline) {
+    V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
+    float bd = INFINITY;
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        V2 q1, q2;
+        closest_points_line_line(box_side(bpos, bt, hl, hw, i), line, &q1, &q2);
+        const float d = norm(q1 - q2);
+        if (d < bd) {
+            bd = d;
+            c1 = q1;
+            c2 = q2;
+        }
+    }
+    *pbox = c1;
+    *pline = c2;
+}
+
+// physics._get_closest_box_box (physics.py:25-128): (point on A, point on B)
+VHD void closest_box_box(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, float hlb,
+                         float hwb, V2* out_a, V2* out_b) {
+    V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
+    float bd = INFINITY;
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+        V2 p1, p2;
+        if (i < 4) {  // side i of A vs box B: closest_line_box(B, sideA) -> (on B, on A side)
+            closest_line_box(pb, tb, hlb, hwb, box_side(pa, ta, hla, hwa, i), &p2, &p1);
+        } else {      // box A vs side j of B: closest_line_box(A, sideB) -> (on A, on B side)
+            closest_line_box(pa, ta, hla, hwa, box_side(pb, tb, hlb, hwb, i - 4), &p1, &p2);
+        }
+        const float d = norm(p1 - p2);
+        if (d < bd) {
+            bd = d;
+            c1 = p1;
+            c2 = p2;
+        }
+    }
+    *out_a = c1;
+    *out_b = c2;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pair narrowphases.  Result convention: force on entity a (entity b receives exactly -fa, as
+// _get_constraint_forces returns (force, -force)), torque on a, torque on b.
+struct PairOut {
+    V2 fa;
+    float ta, tb;
+};
+
+struct Body {  // one entity's state in one env plus its static shape numbers
+    V2 p, v;
+    float rot, w;
+};
+
+struct WorldK {  // f32 world constants used by the narrowphases
+    float k;     // contact_margin
+    float c;     // collision_force
+    float cj;    // joint_force
+    float ct;    // torque_constraint_force
+};
+
+// _sphere_sphere_vectorized_collision (core.py:2293-2338)
+VHD PairOut pair_ss(V2 pa, V2 pb, float dmin, const WorldK& w) {
+    return PairOut{constraint_force(pa, pb, dmin, w.c, w.k, false), 0.f, 0.f};
+}
+
+// _sphere_line_vectorized_collision (core.py:2340-2391); a = line, b = sphere
+VHD PairOut pair_ls(V2 pl, Trig tl, float hl, V2 ps, float dmin, const WorldK& w) {
+    const V2 cp = closest_point_line(pl, mk(tl.c0, tl.s0), hl, ps, true);
+    const V2 fs = constraint_force(ps, cp, dmin, w.c, w.k, false);
+    const V2 fl = -fs;
+    const V2 r = cp - pl;
+    return PairOut{fl, cross(r, fl), 0.f};
+}
+
+// _line_line_vectorized_collision (core.py:2393-2456)
+VHD PairOut pair_ll(V2 pa, Trig ta, float hla, V2 pb, Trig tb, float hlb, float dmin,
+                    const WorldK& w) {
+    V2 qa, qb;
+    closest_points_line_line(Seg{pa, mk(ta.c0, ta.s0), hla}, Seg{pb, mk(tb.c0, tb.s0), hlb}, &qa, &qb);
+    const V2 fa = constraint_force(qa, qb, dmin, w.c, w.k, false);
+    const V2 fb = -fa;
+    return PairOut{fa, cross(qa - pa, fa), cross(qb - pb, fb)};
+}
+
+// _box_sphere_vectorized_collision (core.py:2458-2551); a = box, b = sphere
+VHD PairOut pair_bs(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 ps, float dmin_rl,
+                    const WorldK& w) {
+    const V2 cpb = closest_point_box(pbx, tbx, hl, hw, ps);
+    V2 inner = cpb;
+    float d = 0.f;
+    if (!hollow) inner = inner_point_box(ps, cpb, pbx, &d);
+    const V2 fs = constraint_force(ps, inner, dmin_rl + d, w.c, w.k, false);
+    const V2 fb = -fs;
+    return PairOut{fb, cross(cpb - pbx, fb), 0.f};
+}
+
+// _box_line_vectorized_collision (core.py:2553-2652); a = box, b = line
+VHD PairOut pair_bl(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 pl, Trig tl, float hll,
+                    float dmin, const WorldK& w) {
+    V2 pb, plp;
+    closest_line_box(pbx, tbx, hl, hw, Seg{pl, mk(tl.c0, tl.s0), hll}, &pb, &plp);
+    V2 inner = pb;
+    float d = 0.f;
+    if (!hollow) inner = inner_point_box(plp, pb, pbx, &d);
+    const V2 fbox = constraint_force(inner, plp, dmin + d, w.c, w.k, false);
+    const V2 fline = -fbox;
+    return PairOut{fbox, cross(pb - pbx, fbox), cross(plp - pl, fline)};
+}
+
+// _box_box_vectorized_collision (core.py:2654-2785)
+VHD PairOut pair_bb(V2 pa, Trig ta, float hla, float hwa, bool hol_a, V2 pb, Trig tb, float hlb,
+                    float hwb, bool hol_b, float dmin, const WorldK& w) {
+    V2 qa, qb;
+    closest_box_box(pa, ta, hla, hwa, pb, tb, hlb, hwb, &qa, &qb);
+    V2 ia = qa, ib = qb;
+    float da = 0.f, db = 0.f;
+    if (!hol_a) ia = inner_point_box(qb, qa, pa, &da);
+    if (!hol_b) ib = inner_point_box(qa, qb, pb, &db);
+    const V2 fa = constraint_force(ia, ib, (da + db) + dmin, w.c, w.k, false);
+    const V2 fb = -fa;
+    return PairOut{fa, cross(qa - pa, fa), cross(qb - pb, fb)};
+}
+
+// TorchUtils.rotate_vector (utils.py:176-191) with precomputed cos/sin of the angle
+VHD V2 rotate(V2 v, float c, float s) { return mk(v.x * c - v.y * s, v.x * s + v.y * c); }
+
+// _vectorized_joint_constraints + _get_constraint_torques (core.py:2200-2291, 2840-2857)
+// fixed_rot = JointConstraint.fixed_rotation for this env.
+VHD PairOut pair_joint(V2 pa, float rota, Trig ta, V2 pb, float rotb, Trig tb, V2 da, V2 db,
+                       float dist, bool rotate_ok, float fixed_rot, const WorldK& w) {
+    const V2 pja = pa + rotate(da, ta.c0, ta.s0);
+    const V2 pjb = pb + rotate(db, tb.c0, tb.s0);
+    const V2 fat = constraint_force(pja, pjb, dist, -w.cj, w.k, true);
+    const V2 far = constraint_force(pja, pjb, dist, w.cj, w.k, false);
+    const V2 fa = fat + far;
+    const V2 fb = (-fat) + (-far);
+    float tra = cross(pja - pa, fa);
+    float trb = cross(pjb - pb, fb);
+    if (!rotate_ok) {
+        const float delta = rota - (rotb + fixed_rot);
+        const float ad = fabsf(delta);
+        const float pen = expf(ad) - 1.f;
+        float tq = (w.ct * tsign(delta)) * pen;
+        if (ad < 1e-9f) tq = 0.f;
+        tra = tra + (-tq);
+        trb = trb + tq;
+    }
+    return PairOut{fa, tra, trb};
+}
+
+// get_friction_force (core.py:2054-2072) for a 2-vector
+VHD V2 friction2(V2 v, float coeff, float mass, float sdt) {
+    const float speed = norm(v);
+    const float ffc = coeff * mass;
+    const float den = (speed == 0.f) ? 1e-8f : speed;
+    V2 f = mk(-(v.x / den) * tmin(ffc, (fabsf(v.x) / sdt) * mass),
+              -(v.y / den) * tmin(ffc, (fabsf(v.y) / sdt) * mass));
+    if (speed == 0.f) f = mk(0.f, 0.f);
+    return f;
+}
+VHD float friction1(float v, float coeff, float mass, float sdt) {
+    const float speed = fabsf(v);
+    const float ffc = coeff * mass;
+    const float den = (speed == 0.f) ? 1e-8f : speed;
+    float f = -(v / den) * tmin(ffc, (fabsf(v) / sdt) * mass);
+    if (speed == 0.f) f = 0.f;
+    return f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ray casts (core.py:1280-1625), one ray against one target.  `o` ray origin, (dc, ds) ray dir.
+VHD float ray_box(V2 o, float ang, float dc, float ds, V2 bp, float brot, float L, float W,
+                  float max_range) {
+    const V2 po = o - bp;
+    const float nc = cosf(-brot), ns = sinf(-brot);
+    const V2 pa = rotate(po, nc, ns);
+    const V2 da = rotate(mk(dc, ds), nc, ns);
+    (void)ang;
+    const float tx1 = ((-L) / 2.f - pa.x) / da.x;
+    const float tx2 = (L / 2.f - pa.x) / da.x;
+    float tmn = tmin(tx1, tx2), tmx = tmax(tx1, tx2);
+    const float ty1 = ((-W) / 2.f - pa.y) / da.y;
+    const float ty2 = (W / 2.f - pa.y) / da.y;
+    const float tymn = tmin(ty1, ty2), tymx = tmax(ty1, ty2);
+    tmn = tmax(tmn, tymn);
+    tmx = tmin(tmx, tymx);
+    const V2 ia = da * tmn + pa;  // tmin * dir_aabb + pos_aabb
+    const V2 iw = rotate(ia, cosf(brot), sinf(brot)) + bp;
+    const bool hit = (tmx >= tmn) && (tmn > 0.f);
+    const float d = norm(o - iw);
+    return hit ? d : max_range;
+}
+
+VHD float ray_sphere(V2 o, float dc, float ds, V2 sp, float r, float max_range) {
+    const V2 dir = mk(dc, ds);
+    const V2 lp = o + dir * (max_range / 2.f);
+    const V2 cp = closest_point_line(lp, dir, 0.f, sp, false);
+    const float dn = norm(sp - cp);
+    const bool inter = dn < r;
+    const float a = r * r - dn * dn;
+    const float m = sqrtf((a > 0.f) ? a : 1e-8f);
+    const V2 u = sp - o;
+    const V2 u1 = cp - o;
+    const float udot = u.x * dir.x + u.y * dir.y;
+    const bool front = udot > 0.f;
+    const float d = norm(u1) - m;
+    return (inter && front) ? d : max_range;
+}
+
+VHD float ray_line(V2 o, float dc, float ds, V2 lp, float lrot, float L, float max_range) {
+    const V2 r = mk(cosf(lrot) * L, sinf(lrot) * L);
+    const V2 s = mk(dc, ds);
+    const float rxs = cross(r, s);
+    const V2 qp = o - lp;
+    const float t = cross(qp, s / rxs);
+    const float u = cross(qp, r / rxs);
+    const float d = norm(mk(u * s.x, u * s.y));
+    const bool miss = (rxs == 0.f) || (t > 0.5f) || (t < -0.5f) || (u < 0.f);
+    return miss ? max_range : d;
+}
+
+}  // namespace vmas

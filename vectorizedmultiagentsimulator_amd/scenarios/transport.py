@@ -1,0 +1,193 @@
+"""Transport: agents push heavy box packages onto a goal.
+
+Workload of BASELINE config C3.  Restates vmas/scenarios/transport.py:15-190 (layout, reset,
+reward, observation, done) and its dribbling heuristic policy (transport.py:193-350).
+Entities: goal (sphere r=0.15, no collide), packages (movable boxes), agents (spheres).
+"""
+import torch
+
+from vectorizedmultiagentsimulator_amd.simulator.core import Agent, Box, Landmark, Sphere, World
+from vectorizedmultiagentsimulator_amd.simulator.heuristic_policy import BaseHeuristicPolicy
+from vectorizedmultiagentsimulator_amd.simulator.scenario import BaseScenario
+from vectorizedmultiagentsimulator_amd.simulator.utils import Color, ScenarioUtils
+
+
+class Scenario(BaseScenario):
+    def make_world(self, batch_dim: int, device: torch.device, **kwargs):
+        n_agents = kwargs.pop("n_agents", 4)
+        self.n_packages = kwargs.pop("n_packages", 1)
+        self.package_width = kwargs.pop("package_width", 0.15)
+        self.package_length = kwargs.pop("package_length", 0.15)
+        self.package_mass = kwargs.pop("package_mass", 50)
+        ScenarioUtils.check_kwargs_consumed(kwargs)
+
+        self.shaping_factor = 100
+        self.world_semidim = 1
+        self.agent_radius = 0.03
+        bound = self.world_semidim + 2 * self.agent_radius + max(self.package_length, self.package_width)
+        world = World(batch_dim, device, x_semidim=bound, y_semidim=bound)
+        for i in range(n_agents):
+            world.add_agent(Agent(name=f"agent_{i}", shape=Sphere(self.agent_radius), u_multiplier=0.6))
+        goal = Landmark(name="goal", collide=False, shape=Sphere(radius=0.15), color=Color.LIGHT_GREEN)
+        world.add_landmark(goal)
+        self.packages = []
+        for i in range(self.n_packages):
+            package = Landmark(
+                name=f"package {i}", collide=True, movable=True, mass=self.package_mass,
+                shape=Box(length=self.package_length, width=self.package_width), color=Color.RED,
+            )
+            package.goal = goal
+            self.packages.append(package)
+            world.add_landmark(package)
+        return world
+
+    def reset_world_at(self, env_index: int = None):
+        w = self.world
+        bounds = (-self.world_semidim, self.world_semidim)
+        ScenarioUtils.spawn_entities_randomly(
+            w.agents, w, env_index, min_dist_between_entities=self.agent_radius * 2,
+            x_bounds=bounds, y_bounds=bounds,
+        )
+        occupied = torch.stack([agent.state.pos for agent in w.agents], dim=1)
+        if env_index is not None:
+            occupied = occupied[env_index].unsqueeze(0)
+        goal = w.landmarks[0]
+        ScenarioUtils.spawn_entities_randomly(
+            [goal] + self.packages, w, env_index,
+            min_dist_between_entities=max(
+                p.shape.circumscribed_radius() + goal.shape.radius + 0.01 for p in self.packages
+            ),
+            x_bounds=bounds, y_bounds=bounds, occupied_positions=occupied,
+        )
+        for package in self.packages:
+            package.on_goal = w.is_overlapping(package, package.goal)
+            dist = torch.linalg.vector_norm(package.state.pos - package.goal.state.pos, dim=1)
+            if env_index is None:
+                package.global_shaping = dist * self.shaping_factor
+            else:
+                package.global_shaping[env_index] = dist[env_index] * self.shaping_factor
+
+    def reward(self, agent: Agent):
+        w = self.world
+        if agent == w.agents[0]:
+            self.rew = torch.zeros(w.batch_dim, device=w.device, dtype=torch.float32)
+            for package in self.packages:
+                package.dist_to_goal = torch.linalg.vector_norm(package.state.pos - package.goal.state.pos, dim=1)
+                package.on_goal = w.is_overlapping(package, package.goal)
+                package.color = torch.tensor(Color.RED.value, device=w.device, dtype=torch.float32).repeat(
+                    w.batch_dim, 1
+                )
+                package.color[package.on_goal] = torch.tensor(Color.GREEN.value, device=w.device, dtype=torch.float32)
+                package_shaping = package.dist_to_goal * self.shaping_factor
+                off = ~package.on_goal
+                self.rew[off] += package.global_shaping[off] - package_shaping[off]
+                package.global_shaping = package_shaping
+        return self.rew
+
+    def observation(self, agent: Agent):
+        package_obs = []
+        for package in self.packages:
+            package_obs.append(package.state.pos - package.goal.state.pos)
+            package_obs.append(package.state.pos - agent.state.pos)
+            package_obs.append(package.state.vel)
+            package_obs.append(package.on_goal.unsqueeze(-1))
+        return torch.cat([agent.state.pos, agent.state.vel, *package_obs], dim=-1)
+
+    def done(self):
+        return torch.all(torch.stack([package.on_goal for package in self.packages], dim=1), dim=-1)
+
+
+class HeuristicPolicy(BaseHeuristicPolicy):
+    """Hermite-spline "dribbling" towards a hit point behind the package."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.lookahead = 0.0
+        self.start_vel_dist_from_target_ratio = 0.5
+        self.start_vel_behind_ratio = 0.5
+        self.start_vel_mag = 1.0
+        self.hit_vel_mag = 1.0
+        self.package_radius = 0.15 / 2
+        self.agent_radius = -0.02
+        self.dribble_slowdown_dist = 0.0
+        self.speed = 0.95
+
+    def compute_action(self, observation: torch.Tensor, u_range: float) -> torch.Tensor:
+        self.n_env = observation.shape[0]
+        self.device = observation.device
+        agent_pos = observation[:, :2]
+        package_pos = observation[:, 6:8] + agent_pos
+        goal_pos = -observation[:, 4:6] + package_pos
+        control = self.dribble(agent_pos, package_pos, goal_pos)
+        control *= self.speed * u_range
+        return torch.clamp(control, -u_range, u_range)
+
+    def dribble(self, agent_pos, package_pos, goal_pos, agent_vel=None):
+        package_disp = goal_pos - package_pos
+        ball_dist = package_disp.norm(dim=-1)
+        direction = package_disp / ball_dist[:, None]
+        hit_pos = package_pos - direction * (self.package_radius + self.agent_radius)
+        hit_vel = direction * self.hit_vel_mag
+        start_vel = self.get_start_vel(hit_pos, hit_vel, agent_pos, self.start_vel_mag * 2)
+        slowdown_mask = ball_dist <= self.dribble_slowdown_dist
+        hit_vel[slowdown_mask, :] *= ball_dist[slowdown_mask, None] / self.dribble_slowdown_dist
+        return self.get_action(target_pos=hit_pos, target_vel=hit_vel, curr_pos=agent_pos,
+                               curr_vel=agent_vel, start_vel=start_vel)
+
+    @staticmethod
+    def _npr(n, r):
+        if r > n:
+            return 0
+        ans = 1
+        for k in range(n, max(1, n - r), -1):
+            ans = ans * k
+        return ans
+
+    def hermite(self, p0, p1, p0dot, p1dot, u=0.0, deriv=0):
+        u = u.reshape((-1,))
+        U = torch.stack(
+            [self._npr(3 - i, deriv) * (u ** max(0, 3 - i - deriv)) for i in range(4)], dim=1
+        ).float()
+        A = torch.tensor(
+            [[2.0, -2.0, 1.0, 1.0], [-3.0, 3.0, -2.0, -1.0], [0.0, 0.0, 1.0, 0.0], [1.0, 0.0, 0.0, 0.0]],
+            device=U.device,
+        )
+        P = torch.stack([p0, p1, p0dot, p1dot], dim=1)
+        return (U[:, None, :] @ A[None, :, :] @ P).squeeze(1)
+
+    def get_start_vel(self, pos, vel, start_pos, start_vel_mag):
+        start_vel_mag = torch.as_tensor(start_vel_mag, device=self.device).view(-1)
+        goal_disp = pos - start_pos
+        goal_dist = goal_disp.norm(dim=-1)
+        vel_mag = vel.norm(dim=-1)
+        vel_dir = vel.clone()
+        vel_dir[vel_mag > 0] /= vel_mag[vel_mag > 0, None]
+        goal_dir = goal_disp / goal_dist[:, None]
+        vel_dir_normal = torch.stack([-vel_dir[:, 1], vel_dir[:, 0]], dim=1)
+        dot_prod = (goal_dir * vel_dir_normal).sum(dim=1)
+        vel_dir_normal[dot_prod > 0, :] *= -1
+        dist_behind_target = self.start_vel_dist_from_target_ratio * goal_dist
+        point_dir = -vel_dir * self.start_vel_behind_ratio + vel_dir_normal * (1 - self.start_vel_behind_ratio)
+        target_pos = pos + point_dir * dist_behind_target[:, None]
+        target_disp = target_pos - start_pos
+        target_dist = target_disp.norm(dim=1)
+        start_vel_aug_dir = target_disp
+        start_vel_aug_dir[target_dist > 0] /= target_dist[target_dist > 0, None]
+        return start_vel_aug_dir * start_vel_mag[:, None]
+
+    def get_action(self, target_pos, target_vel=None, start_pos=None, start_vel=None, curr_pos=None,
+                   curr_vel=None):
+        if curr_pos is None:
+            curr_pos = torch.zeros(target_pos.shape, device=self.device)
+        if curr_vel is None:
+            curr_vel = torch.zeros(target_pos.shape, device=self.device)
+        if start_pos is None:
+            start_pos = curr_pos
+        if target_vel is None:
+            target_vel = torch.zeros(target_pos.shape, device=self.device)
+        if start_vel is None:
+            start_vel = self.get_start_vel(target_pos, target_vel, start_pos, self.start_vel_mag * 2)
+        u_start = torch.ones(curr_pos.shape[0], device=self.device) * self.lookahead
+        des_curr_pos = self.hermite(start_pos, target_pos, start_vel, target_vel, u=u_start, deriv=0)
+        des_curr_vel = self.hermite(start_pos, target_pos, start_vel, target_vel, u=u_start, deriv=1)
+        return 0.5 * (des_curr_pos - curr_pos) + 0.5 * (des_curr_vel - curr_vel)

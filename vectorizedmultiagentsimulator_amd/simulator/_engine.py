@@ -1,0 +1,542 @@
+"""Bridge between the Python World and the native engine (``libvmas_mi355x.so``).
+
+Per world it builds the static tables of the C ABI (entities, candidate pairs in the reference's
+accumulation order, joints) and re-creates them whenever the world's configuration signature
+changes.  Per ``World.step`` it gathers the current state tensors of every entity as raw pointers
++ strides (so views, user-replaced and in-place-mutated tensors are all read where they live),
+allocates ONE fresh output buffer, calls ``vmas_world_step`` and re-points the integrated fields
+of the entities at views of that buffer -- the reference's "integration creates new tensors"
+semantics (core.py:2866-2907) without any copy.
+
+Device ``cuda:i`` (ROCm) -> gfx950 kernels on the current torch stream; device ``cpu`` -> the
+host backend of the same library (same arithmetic).  There is no PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, List
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from .utils import LINE_MIN_DIST
+
+_LMD32 = np.float32(LINE_MIN_DIST)
+
+
+def _f32(x) -> float:
+    return float(np.float32(x))
+
+
+def _shape_code(shape) -> int:
+    from .core import Box, Line, Sphere
+
+    if isinstance(shape, Sphere):
+        return N.VMAS_SPHERE
+    if isinstance(shape, Box):
+        return N.VMAS_BOX
+    if isinstance(shape, Line):
+        return N.VMAS_LINE
+    raise RuntimeError(f"Shape {shape} currently not handled by the engine")
+
+
+def _check_grad(tensors) -> None:
+    if torch.is_grad_enabled():
+        for t in tensors:
+            if t is not None and t.requires_grad:
+                raise NotImplementedError(
+                    "The MI355X engine has no backward pass: World.step / cast_rays / distance "
+                    "queries cannot run on tensors that require grad (grad_enabled=True)."
+                )
+
+
+class PhysicsEngine:
+    def __init__(self, world):
+        self.world = world
+        self.lib = N.load_library()
+        self._sig = None
+        self._handle = None
+        self._dev_index = -1
+        self.last_iterations = 0
+        self.steps = 0
+
+    def __del__(self):
+        try:
+            if self._handle is not None:
+                self.lib.vmas_world_destroy(self._handle)
+        except Exception:
+            pass
+
+    # ---- device helpers ---------------------------------------------------------------------------
+    def _device(self) -> torch.device:
+        dev = torch.device(self.world.device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        return dev
+
+    def _native_device(self, dev: torch.device) -> int:
+        if dev.type == "cpu":
+            return -1
+        if dev.type == "cuda":
+            return dev.index
+        raise RuntimeError(f"device {dev} is not supported by the MI355X engine")
+
+    def _stream(self, dev: torch.device):
+        if dev.type == "cuda":
+            return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        return None
+
+    def _prep(self, t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+        if t.device != dev or t.dtype != torch.float32:
+            t = t.to(device=dev, dtype=torch.float32)
+        return t
+
+    # ---- static tables ----------------------------------------------------------------------------
+    def _signature(self):
+        w = self.world
+        ents = w.entities
+        es = []
+        for e in ents:
+            shape = e._shape
+            es.append(
+                (
+                    id(e), id(shape), getattr(shape, "hollow", None), e._movable, e._rotatable,
+                    e._collide, id(e._collision_filter), e._mass, e._drag, e._linear_friction,
+                    e._angular_friction, e._gravity is None, e._max_speed, e._v_range,
+                    getattr(e, "_max_f", None), getattr(e, "_f_range", None),
+                    getattr(e, "_max_t", None), getattr(e, "_t_range", None),
+                )
+            )
+        js = []
+        for j in w._joints.values():
+            fr = j.fixed_rotation
+            js.append((id(j), j.dist, j.rotate, fr if not isinstance(fr, torch.Tensor) else "tensor"))
+        return (
+            tuple(es), tuple(js), w._drag, w._linear_friction, w._angular_friction, w._x_semidim,
+            w._y_semidim, w._collision_force, w._joint_force, w._torque_constraint_force,
+            w._contact_margin, id(w._gravity), id(w._collidable_pairs), w.batch_dim, str(w.device),
+        )
+
+    def _build(self, sig, max_substeps: int):
+        w = self.world
+        dev = self._device()
+        self._dev = dev
+        self._dev_index = self._native_device(dev)
+        ents = list(w.entities)
+        E = len(ents)
+        index = {id(e): i for i, e in enumerate(ents)}
+        agents = [e for e in ents if hasattr(e, "_action")]
+        agent_index = {id(a): i for i, a in enumerate(agents)}
+
+        # --- candidate pairs in the reference's order (core.py:2103-2188)
+        joints, ss, ls, ll, bs, bl, bb = [], [], [], [], [], [], []
+        for a in range(E):
+            ea = ents[a]
+            for b in range(a + 1, E):
+                eb = ents[b]
+                jc = w._joints.get(frozenset({ea.name, eb.name}), None)
+                if jc is not None:
+                    joints.append(jc)
+                    if jc.dist == 0:
+                        continue
+                if not w._collides_static(ea, eb):
+                    continue
+                ca, cb = _shape_code(ea.shape), _shape_code(eb.shape)
+                S, B_, L = N.VMAS_SPHERE, N.VMAS_BOX, N.VMAS_LINE
+                if ca == S and cb == S:
+                    ss.append((ea, eb))
+                elif {ca, cb} == {L, S}:
+                    ls.append((ea, eb) if cb == S else (eb, ea))
+                elif ca == L and cb == L:
+                    ll.append((ea, eb))
+                elif {ca, cb} == {B_, S}:
+                    bs.append((ea, eb) if cb == S else (eb, ea))
+                elif {ca, cb} == {B_, L}:
+                    bl.append((ea, eb) if cb == L else (eb, ea))
+                elif ca == B_ and cb == B_:
+                    bb.append((ea, eb))
+                else:
+                    raise AssertionError()
+        self.joint_list = joints
+        pairs = []
+        for ji, jc in enumerate(joints):
+            pairs.append((N.VMAS_PAIR_JOINT, jc.entity_a, jc.entity_b, ji, 0.0, _f32(jc.dist)))
+
+        def cr(e):
+            return e.shape.circumscribed_radius()
+
+        for ea, eb in ss:
+            pairs.append((N.VMAS_PAIR_SS, ea, eb, -1, _f32(cr(ea) + cr(eb)),
+                          float(np.float32(ea.shape.radius) + np.float32(eb.shape.radius))))
+        for ea, eb in ls:
+            pairs.append((N.VMAS_PAIR_LS, ea, eb, -1, _f32(cr(ea) + cr(eb)),
+                          float(np.float32(eb.shape.radius) + _LMD32)))
+        for ea, eb in ll:
+            pairs.append((N.VMAS_PAIR_LL, ea, eb, -1, _f32(cr(ea) + cr(eb)), float(_LMD32)))
+        for ea, eb in bs:
+            pairs.append((N.VMAS_PAIR_BS, ea, eb, -1, _f32(cr(ea) + cr(eb)),
+                          float(np.float32(eb.shape.radius) + _LMD32)))
+        for ea, eb in bl:
+            pairs.append((N.VMAS_PAIR_BL, ea, eb, -1, _f32(cr(ea) + cr(eb)), float(_LMD32)))
+        for ea, eb in bb:
+            pairs.append((N.VMAS_PAIR_BB, ea, eb, -1, _f32(cr(ea) + cr(eb)), float(_LMD32)))
+        P = len(pairs)
+        pd = (N.VmasPairDesc * max(P, 1))()
+        for i, (cls, ea, eb, ji, bpr, dmin) in enumerate(pairs):
+            pd[i].cls, pd[i].ea, pd[i].eb, pd[i].joint = cls, index[id(ea)], index[id(eb)], ji
+            pd[i].bp_radius, pd[i].dmin = bpr, dmin
+        self.pairs = pairs
+
+        # --- joints
+        jd = (N.VmasJointDesc * max(len(joints), 1))()
+        for i, jc in enumerate(joints):
+            da = jc.delta_anchor(jc.entity_a)
+            db = jc.delta_anchor(jc.entity_b)
+            jd[i].delta_a_x, jd[i].delta_a_y = _f32(da[0]), _f32(da[1])
+            jd[i].delta_b_x, jd[i].delta_b_y = _f32(db[0]), _f32(db[1])
+            jd[i].dist = _f32(jc.dist)
+            jd[i].rotate = int(bool(jc.rotate))
+            fr = jc.fixed_rotation
+            if fr is None:
+                raise RuntimeError("JointConstraint.fixed_rotation is None (Joint.notify never ran)")
+            jd[i].fixed_rotation = 0.0 if isinstance(fr, torch.Tensor) else _f32(fr)
+
+        # --- entities
+        ed = (N.VmasEntityDesc * max(E, 1))()
+        n_lin = n_rot = n_force = n_torque = 0
+        self.lin_slots, self.rot_slots, self.force_slots, self.torque_slots = [], [], [], []
+        for i, e in enumerate(ents):
+            d = ed[i]
+            d.shape = _shape_code(e.shape)
+            flags = 0
+            if e.movable:
+                flags |= N.F_MOVABLE
+            if e.rotatable:
+                flags |= N.F_ROTATABLE
+            if d.shape == N.VMAS_BOX and e.shape.hollow:
+                flags |= N.F_HOLLOW
+            is_agent = id(e) in agent_index
+            d.agent_index = agent_index[id(e)] if is_agent else -1
+            d.out_lin = d.out_rot = d.out_force = d.out_torque = -1
+            if e.movable:
+                d.out_lin = n_lin
+                self.lin_slots.append(e)
+                n_lin += 1
+            if e.rotatable:
+                d.out_rot = n_rot
+                self.rot_slots.append(e)
+                n_rot += 1
+            if is_agent:
+                flags |= N.F_AGENT
+                if e.movable and (e.max_f is not None or e.f_range is not None):
+                    d.out_force = n_force
+                    self.force_slots.append(e)
+                    n_force += 1
+                if e.rotatable and (e.max_t is not None or e.t_range is not None):
+                    d.out_torque = n_torque
+                    self.torque_slots.append(e)
+                    n_torque += 1
+                if e.max_f is not None:
+                    flags |= N.F_MAX_F
+                    d.max_f = _f32(e.max_f)
+                if e.f_range is not None:
+                    flags |= N.F_F_RANGE
+                    d.f_range = _f32(e.f_range)
+                if e.max_t is not None:
+                    flags |= N.F_MAX_T
+                    d.max_t = _f32(e.max_t)
+                if e.t_range is not None:
+                    flags |= N.F_T_RANGE
+                    d.t_range = _f32(e.t_range)
+            if d.shape == N.VMAS_SPHERE:
+                d.radius = _f32(e.shape.radius)
+            else:
+                d.half_length = float(np.float32(e.shape.length) / np.float32(2))
+                if d.shape == N.VMAS_BOX:
+                    d.half_width = float(np.float32(e.shape.width) / np.float32(2))
+            d.mass = _f32(e.mass)
+            d.inertia = _f32(e.moment_of_inertia)
+            drag = e.drag if e.drag is not None else w._drag
+            d.one_minus_drag = _f32(1 - drag)
+            if e.linear_friction is not None:
+                flags |= N.F_LIN_FRIC
+                d.lin_fric = _f32(e.linear_friction)
+            elif w._linear_friction > 0:
+                flags |= N.F_LIN_FRIC
+                d.lin_fric = _f32(w._linear_friction)
+            if e.angular_friction is not None:
+                flags |= N.F_ANG_FRIC
+                d.ang_fric = _f32(e.angular_friction)
+            elif w._angular_friction > 0:
+                flags |= N.F_ANG_FRIC
+                d.ang_fric = _f32(w._angular_friction)
+            if e.max_speed is not None:
+                flags |= N.F_MAX_SPEED
+                d.max_speed = _f32(e.max_speed)
+            if e.v_range is not None:
+                flags |= N.F_V_RANGE
+                d.v_range = _f32(e.v_range)
+            if e.gravity is not None:
+                flags |= N.F_GRAVITY
+            d.flags = flags
+
+        cfg = N.VmasWorldConfig()
+        cfg.n_entities, cfg.n_agents, cfg.n_pairs, cfg.n_joints = E, len(agents), P, len(joints)
+        cfg.batch = w.batch_dim
+        cfg.device = self._dev_index
+        cfg.n_out_lin, cfg.n_out_rot, cfg.n_out_force, cfg.n_out_torque = n_lin, n_rot, n_force, n_torque
+        cfg.contact_margin = _f32(w._contact_margin)
+        cfg.collision_force = _f32(w._collision_force)
+        cfg.joint_force = _f32(w._joint_force)
+        cfg.torque_constraint_force = _f32(w._torque_constraint_force)
+        g = w._gravity.detach().to("cpu", torch.float32).reshape(-1).tolist()
+        cfg.gravity_x, cfg.gravity_y = g[0], g[1]
+        cfg.has_world_gravity = int(not (g[0] == 0.0 and g[1] == 0.0))
+        cfg.has_x_semidim = int(w._x_semidim is not None)
+        cfg.has_y_semidim = int(w._y_semidim is not None)
+        cfg.x_semidim = _f32(w._x_semidim) if w._x_semidim is not None else 0.0
+        cfg.y_semidim = _f32(w._y_semidim) if w._y_semidim is not None else 0.0
+        cfg.max_substeps = max_substeps
+        handle = ctypes.c_void_p()
+        N.check(self.lib.vmas_world_create(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(handle)),
+                "vmas_world_create")
+        if self._handle is not None:
+            self.lib.vmas_world_destroy(self._handle)
+        self._handle = handle
+        self._cfg = cfg
+        self._max_substeps = max_substeps
+        self.entities = ents
+        self.agents = agents
+        self.n_out = (n_lin, n_rot, n_force, n_torque)
+        self._eio = np.zeros(E, dtype=N.ENTITY_IO_DTYPE)
+        self._aio = np.zeros(max(len(agents), 1), dtype=N.AGENT_IO_DTYPE)
+        self._jio = np.zeros(max(len(joints), 1), dtype=N.JOINT_IO_DTYPE)
+        self._io = N.VmasStepIO()
+        self._sig = sig
+
+    def _ensure(self):
+        sub = int(self.world._substeps)
+        sig = self._signature()
+        if sig != self._sig or self._handle is None or sub > self._max_substeps:
+            self._build(sig, max(sub, 16))
+
+    # ---- the step ---------------------------------------------------------------------------------
+    def step(self):
+        self._ensure()
+        w = self.world
+        dev = self._dev
+        B = w.batch_dim
+        ents, agents = self.entities, self.agents
+        keep = []  # tensors converted for the call, kept alive until it returns
+        eio = self._eio
+        for i, e in enumerate(ents):
+            st = e._state
+            pos, vel, rot, ang = st._pos, st._vel, st._rot, st._ang_vel
+            _check_grad((pos, vel, rot, ang))
+            pos, vel, rot, ang = (self._prep(pos, dev), self._prep(vel, dev), self._prep(rot, dev),
+                                  self._prep(ang, dev))
+            keep += [pos, vel, rot, ang]
+            ps, vs = pos.stride(), vel.stride()
+            row = eio[i]
+            row["pos"], row["vel"], row["rot"], row["ang"] = (
+                pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr())
+            row["pos_s0"], row["pos_s1"], row["vel_s0"], row["vel_s1"] = ps[0], ps[1], vs[0], vs[1]
+            row["rot_s0"], row["ang_s0"] = rot.stride(0), ang.stride(0)
+            g = e._gravity
+            if g is not None:
+                g = self._prep(g, dev).expand(B, 2)
+                keep.append(g)
+                row["grav"] = g.data_ptr()
+                row["grav_s0"], row["grav_s1"] = g.stride(0), g.stride(1)
+            else:
+                row["grav"] = 0
+        aio = self._aio
+        for i, a in enumerate(agents):
+            st = a._state
+            f, t = st._force, st._torque
+            _check_grad((f, t))
+            f, t = self._prep(f, dev), self._prep(t, dev)
+            keep += [f, t]
+            fs = f.stride()
+            aio[i]["force"], aio[i]["torque"] = f.data_ptr(), t.data_ptr()
+            aio[i]["force_s0"], aio[i]["force_s1"], aio[i]["torque_s0"] = fs[0], fs[1], t.stride(0)
+        jio = self._jio
+        for i, jc in enumerate(self.joint_list):
+            fr = jc.fixed_rotation
+            if isinstance(fr, torch.Tensor):
+                fr = self._prep(fr, dev)
+                if fr.dim() == 0 or fr.shape[0] != B:
+                    fr = fr.reshape(-1)[:1].expand(B, 1) if fr.numel() == 1 else fr.expand(B, 1)
+                keep.append(fr)
+                jio[i]["fixed_rotation"] = fr.data_ptr()
+                jio[i]["s0"] = fr.stride(0)
+            else:
+                jio[i]["fixed_rotation"] = 0
+
+        n_lin, n_rot, n_force, n_torque = self.n_out
+        total = B * (4 * n_lin + 2 * n_rot + 2 * n_force + n_torque)
+        out = torch.empty(max(total, 1), device=dev, dtype=torch.float32)
+        o = 0
+        views = []
+        for n, width in ((n_lin, 2), (n_lin, 2), (n_rot, 1), (n_rot, 1), (n_force, 2), (n_torque, 1)):
+            views.append(out.narrow(0, o, n * B * width).view(n, B, width) if n else None)
+            o += n * B * width
+        base = out.data_ptr()
+        io = self._io
+        io.entities, io.agents, io.joints = eio.ctypes.data, aio.ctypes.data, jio.ctypes.data
+        off = 0
+        ptrs = []
+        for n, width in ((n_lin, 2), (n_lin, 2), (n_rot, 1), (n_rot, 1), (n_force, 2), (n_torque, 1)):
+            ptrs.append(base + 4 * off)
+            off += n * B * width
+        io.out_pos, io.out_vel, io.out_rot, io.out_ang_vel, io.out_force, io.out_torque = ptrs
+        sub = int(w._substeps)
+        io.substeps = sub
+        io.sub_dt = _f32(w._dt / w._substeps)
+        io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
+        iters = ctypes.c_int32(0)
+        N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
+                                         ctypes.byref(iters)), "vmas_world_step")
+        self.last_iterations = iters.value
+        self.steps += 1
+        del keep
+        # re-point the integrated fields at the fresh buffer (new tensor objects, as the reference)
+        if n_lin:
+            pv, vv = views[0].unbind(0), views[1].unbind(0)
+            for k, e in enumerate(self.lin_slots):
+                e._state._pos = pv[k]
+                e._state._vel = vv[k]
+        if n_rot:
+            rv, av = views[2].unbind(0), views[3].unbind(0)
+            for k, e in enumerate(self.rot_slots):
+                e._state._rot = rv[k]
+                e._state._ang_vel = av[k]
+        if n_force:
+            fv = views[4].unbind(0)
+            for k, a in enumerate(self.force_slots):
+                a._state._force = fv[k]
+        if n_torque:
+            tv = views[5].unbind(0)
+            for k, a in enumerate(self.torque_slots):
+                a._state._torque = tv[k]
+
+    # ---- ray casting ------------------------------------------------------------------------------
+    def cast_rays(self, entity, angles: torch.Tensor, max_range: float,
+                  entity_filter: Callable, rot_offset: torch.Tensor = None) -> torch.Tensor:
+        w = self.world
+        dev = self._device()
+        B = w.batch_dim
+        targets: List = []
+        for e in w.entities:
+            if entity is e or not entity_filter(e):
+                continue
+            assert e.collides(entity) and entity.collides(e), "Rays are only casted among collidables"
+            targets.append(e)
+        keep = []
+        origin = self._prep(entity.state.pos, dev)
+        ang = self._prep(angles, dev)
+        _check_grad((origin, ang, rot_offset))
+        if ang.dim() == 1:
+            ang = ang.unsqueeze(-1)
+        R = ang.shape[-1]
+        assert ang.shape[0] == B
+        tg = np.zeros(max(len(targets), 1), dtype=N.RAY_TARGET_DTYPE)
+        for i, e in enumerate(targets):
+            code = _shape_code(e.shape)
+            p = self._prep(e.state.pos, dev)
+            r = self._prep(e.state.rot, dev)
+            _check_grad((p, r))
+            keep += [p, r]
+            row = tg[i]
+            row["shape"] = code
+            if code == N.VMAS_SPHERE:
+                row["radius"] = _f32(e.shape.radius)
+            else:
+                row["length"] = _f32(e.shape.length)
+                row["width"] = _f32(e.shape.width) if code == N.VMAS_BOX else 0.0
+            row["pos"], row["rot"] = p.data_ptr(), r.data_ptr()
+            row["pos_s0"], row["pos_s1"], row["rot_s0"] = p.stride(0), p.stride(1), r.stride(0)
+        out = torch.empty((B, R), device=dev, dtype=torch.float32)
+        rot_ptr, rot_s0 = None, 0
+        if rot_offset is not None:
+            ro = self._prep(rot_offset, dev)
+            keep.append(ro)
+            rot_ptr, rot_s0 = ro.data_ptr(), ro.stride(0)
+        N.check(
+            self.lib.vmas_cast_rays(
+                self._native_device(dev), B, R, origin.data_ptr(), origin.stride(0), origin.stride(1),
+                ang.data_ptr(), ang.stride(0), ang.stride(1), rot_ptr, rot_s0, tg.ctypes.data,
+                len(targets), _f32(max_range), out.data_ptr(), self._stream(dev),
+            ),
+            "vmas_cast_rays",
+        )
+        return out
+
+    # ---- distance queries -------------------------------------------------------------------------
+    def _ref(self, e, dev, keep) -> N.VmasShapeRef:
+        r = N.VmasShapeRef()
+        r.shape = _shape_code(e.shape)
+        p = self._prep(e.state.pos, dev)
+        rot = self._prep(e.state.rot, dev)
+        _check_grad((p, rot))
+        keep += [p, rot]
+        if r.shape == N.VMAS_SPHERE:
+            r.radius = _f32(e.shape.radius)
+            r.radius_lmd = _f32(e.shape.radius + LINE_MIN_DIST)
+        else:
+            r.length = _f32(e.shape.length)
+            if r.shape == N.VMAS_BOX:
+                r.width = _f32(e.shape.width)
+        r.pos, r.rot = p.data_ptr(), rot.data_ptr()
+        r.pos_s0, r.pos_s1, r.rot_s0 = p.stride(0), p.stride(1), rot.stride(0)
+        return r
+
+    def _query(self, kind, a, b=None, tp=None):
+        w = self.world
+        dev = self._device()
+        B = w.batch_dim
+        keep = []
+        ra = self._ref(a, dev, keep)
+        rb = self._ref(b, dev, keep) if b is not None else None
+        tptr, t0, t1 = None, 0, 0
+        if tp is not None:
+            tp = self._prep(torch.as_tensor(tp), dev)
+            _check_grad((tp,))
+            if tp.dim() == 1:
+                tp = tp.unsqueeze(0)
+            tp = tp.expand(B, 2)
+            keep.append(tp)
+            tptr, t0, t1 = tp.data_ptr(), tp.stride(0), tp.stride(1)
+        out = torch.empty(B, device=dev, dtype=torch.bool if kind == N.OVERLAP_PAIR else torch.float32)
+        N.check(
+            self.lib.vmas_distance(
+                self._native_device(dev), B, kind, ctypes.byref(ra),
+                ctypes.byref(rb) if rb is not None else None, tptr, t0, t1, out.data_ptr(),
+                self._stream(dev),
+            ),
+            "vmas_distance",
+        )
+        return out
+
+    @staticmethod
+    def _canonical(a, b):
+        """Order a pair as the reference's distance branches do (box/line first, sphere last)."""
+        ca, cb = _shape_code(a.shape), _shape_code(b.shape)
+        S, B_, L = N.VMAS_SPHERE, N.VMAS_BOX, N.VMAS_LINE
+        if ca == S and cb != S:
+            return b, a
+        if ca == L and cb == B_:
+            return b, a
+        return a, b
+
+    def distance_from_point(self, entity, test_point):
+        return self._query(N.DIST_POINT, entity, tp=test_point)
+
+    def distance(self, a, b):
+        a, b = self._canonical(a, b)
+        return self._query(N.DIST_PAIR, a, b)
+
+    def overlap(self, a, b):
+        a, b = self._canonical(a, b)
+        return self._query(N.OVERLAP_PAIR, a, b)

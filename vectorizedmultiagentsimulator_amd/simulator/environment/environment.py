@@ -1,0 +1,445 @@
+"""The vectorized Environment (restates vmas/simulator/environment/environment.py:49-1070).
+
+Differences from the reference are limited to host-synchronisation placement (§8f row 1 of
+SURVEY.md); results and exceptions are the same:
+  * all agents' continuous actions are validated (NaN / range) with ONE device->host sync per
+    step instead of two per agent (environment.py:621-623, 653-655);
+  * random actions take their bounds from the python ``u_range`` values (the same fp32 numbers
+    the reference reads back from ``u_range_tensor`` with a sync per call).
+Rendering is outside the scope of the MI355X engine.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import random
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from ..core import Agent, TorchVectorizedObject
+from ..scenario import BaseScenario
+from ..utils import AGENT_OBS_TYPE, DEVICE_TYPING, TorchUtils, override
+from . import spaces
+
+
+@contextlib.contextmanager
+def local_seed(vmas_random_state):
+    """Swap in the simulator's RNG states for torch(CPU)/numpy/python (environment.py:30-46)."""
+    torch_state = torch.random.get_rng_state()
+    np_state = np.random.get_state()
+    py_state = random.getstate()
+    torch.random.set_rng_state(vmas_random_state[0])
+    np.random.set_state(vmas_random_state[1])
+    random.setstate(vmas_random_state[2])
+    yield
+    vmas_random_state[0] = torch.random.get_rng_state()
+    vmas_random_state[1] = np.random.get_state()
+    vmas_random_state[2] = random.getstate()
+    torch.random.set_rng_state(torch_state)
+    np.random.set_state(np_state)
+    random.setstate(py_state)
+
+
+def _f32(x) -> float:
+    return float(np.float32(x))
+
+
+class Environment(TorchVectorizedObject):
+    metadata = {"render.modes": ["human", "rgb_array"], "runtime.vectorized": True}
+    vmas_random_state = [torch.random.get_rng_state(), np.random.get_state(), random.getstate()]
+
+    @local_seed(vmas_random_state)
+    def __init__(
+        self,
+        scenario: BaseScenario,
+        num_envs: int = 32,
+        device: DEVICE_TYPING = "cpu",
+        max_steps: Optional[int] = None,
+        continuous_actions: bool = True,
+        seed: Optional[int] = None,
+        dict_spaces: bool = False,
+        multidiscrete_actions: bool = False,
+        clamp_actions: bool = False,
+        grad_enabled: bool = False,
+        terminated_truncated: bool = False,
+        **kwargs,
+    ):
+        if multidiscrete_actions:
+            assert not continuous_actions, (
+                "When asking for multidiscrete_actions, make sure continuous_actions=False"
+            )
+        self.scenario = scenario
+        self.num_envs = num_envs
+        TorchVectorizedObject.__init__(self, num_envs, torch.device(device))
+        self.world = self.scenario.env_make_world(self.num_envs, self.device, **kwargs)
+        self.agents = self.world.policy_agents
+        self.n_agents = len(self.agents)
+        self.max_steps = max_steps
+        self.continuous_actions = continuous_actions
+        self.dict_spaces = dict_spaces
+        self.clamp_action = clamp_actions
+        self.grad_enabled = grad_enabled
+        self.terminated_truncated = terminated_truncated
+        observations = self._reset(seed=seed)
+        self.multidiscrete_actions = multidiscrete_actions
+        self.action_space = self.get_action_space()
+        self.observation_space = self.get_observation_space(observations)
+        self.viewer = None
+        self.headless = None
+        self.visible_display = None
+        self.text_lines = None
+
+    @local_seed(vmas_random_state)
+    def reset(self, seed: Optional[int] = None, return_observations: bool = True,
+              return_info: bool = False, return_dones: bool = False):
+        """Resets the environment in a vectorized way; returns observations for all envs/agents."""
+        return self._reset(seed=seed, return_observations=return_observations,
+                           return_info=return_info, return_dones=return_dones)
+
+    @local_seed(vmas_random_state)
+    def reset_at(self, index: int, return_observations: bool = True, return_info: bool = False,
+                 return_dones: bool = False):
+        """Resets the environment at ``index``."""
+        return self._reset_at(index=index, return_observations=return_observations,
+                              return_info=return_info, return_dones=return_dones)
+
+    @local_seed(vmas_random_state)
+    def get_from_scenario(self, get_observations: bool, get_rewards: bool, get_infos: bool,
+                          get_dones: bool, dict_agent_names: Optional[bool] = None):
+        return self._get_from_scenario(get_observations=get_observations, get_rewards=get_rewards,
+                                       get_infos=get_infos, get_dones=get_dones,
+                                       dict_agent_names=dict_agent_names)
+
+    @local_seed(vmas_random_state)
+    def seed(self, seed=None):
+        return self._seed(seed=seed)
+
+    @local_seed(vmas_random_state)
+    def done(self):
+        return self._done()
+
+    def _reset(self, seed=None, return_observations=True, return_info=False, return_dones=False):
+        if seed is not None:
+            self._seed(seed)
+        self.scenario.env_reset_world_at(env_index=None)
+        self.steps = torch.zeros(self.num_envs, device=self.device)
+        result = self._get_from_scenario(get_observations=return_observations, get_infos=return_info,
+                                         get_rewards=False, get_dones=return_dones)
+        return result[0] if result and len(result) == 1 else result
+
+    def _reset_at(self, index, return_observations=True, return_info=False, return_dones=False):
+        self._check_batch_index(index)
+        self.scenario.env_reset_world_at(index)
+        self.steps[index] = 0
+        result = self._get_from_scenario(get_observations=return_observations, get_infos=return_info,
+                                         get_rewards=False, get_dones=return_dones)
+        return result[0] if result and len(result) == 1 else result
+
+    def _get_from_scenario(self, get_observations, get_rewards, get_infos, get_dones,
+                           dict_agent_names=None):
+        if not get_infos and not get_dones and not get_rewards and not get_observations:
+            return
+        if dict_agent_names is None:
+            dict_agent_names = self.dict_spaces
+        obs = rewards = infos = terminated = truncated = dones = None
+        if get_observations:
+            obs = {} if dict_agent_names else []
+        if get_rewards:
+            rewards = {} if dict_agent_names else []
+        if get_infos:
+            infos = {} if dict_agent_names else []
+        # order matters: rewards may mutate state that observations read (discovery.py:180-210)
+        if get_rewards:
+            for agent in self.agents:
+                reward = self.scenario.reward(agent).clone()
+                if dict_agent_names:
+                    rewards.update({agent.name: reward})
+                else:
+                    rewards.append(reward)
+        if get_observations:
+            for agent in self.agents:
+                observation = TorchUtils.recursive_clone(self.scenario.observation(agent))
+                if dict_agent_names:
+                    obs.update({agent.name: observation})
+                else:
+                    obs.append(observation)
+        if get_infos:
+            for agent in self.agents:
+                info = TorchUtils.recursive_clone(self.scenario.info(agent))
+                if dict_agent_names:
+                    infos.update({agent.name: info})
+                else:
+                    infos.append(info)
+        if self.terminated_truncated:
+            if get_dones:
+                terminated, truncated = self._done()
+            result = [obs, rewards, terminated, truncated, infos]
+        else:
+            if get_dones:
+                dones = self._done()
+            result = [obs, rewards, dones, infos]
+        return [data for data in result if data is not None]
+
+    def _seed(self, seed=None):
+        if seed is None:
+            seed = 0
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        random.seed(seed)
+        return [seed]
+
+    @local_seed(vmas_random_state)
+    def step(self, actions: Union[List, Dict]):
+        """Performs a vectorized step on all sub environments using ``actions``.
+
+        Returns obs, rewards, dones, infos (or obs, rewards, terminated, truncated, infos).
+        """
+        if isinstance(actions, Dict):
+            actions_dict = actions
+            actions = []
+            for agent in self.agents:
+                try:
+                    actions.append(actions_dict[agent.name])
+                except KeyError:
+                    raise AssertionError(f"Agent '{agent.name}' not contained in action dict")
+            assert len(actions_dict) == self.n_agents, (
+                f"Expecting actions for {self.n_agents}, got {len(actions_dict)} actions"
+            )
+        assert len(actions) == self.n_agents, (
+            f"Expecting actions for {self.n_agents}, got {len(actions)} actions"
+        )
+        for i in range(len(actions)):
+            if not isinstance(actions[i], Tensor):
+                actions[i] = torch.tensor(actions[i], dtype=torch.float32, device=self.device)
+            if len(actions[i].shape) == 1:
+                actions[i].unsqueeze_(-1)
+            assert actions[i].shape[0] == self.num_envs, (
+                f"Actions used in input of env must be of len {self.num_envs}, got {actions[i].shape[0]}"
+            )
+            assert actions[i].shape[1] == self.get_agent_action_size(self.agents[i]), (
+                f"Action for agent {self.agents[i].name} has shape {actions[i].shape[1]},"
+                f" but should have shape {self.get_agent_action_size(self.agents[i])}"
+            )
+        if self.continuous_actions:
+            self._validate_continuous_actions(actions)
+        for i, agent in enumerate(self.agents):
+            self._set_action(actions[i], agent, validated=self.continuous_actions)
+        for agent in self.world.agents:
+            self.scenario.env_process_action(agent)
+        self.scenario.pre_step()
+        self.world.step()
+        self.scenario.post_step()
+        self.steps += 1
+        return self._get_from_scenario(get_observations=True, get_infos=True, get_rewards=True,
+                                       get_dones=True)
+
+    def _done(self):
+        terminated = self.scenario.done().clone()
+        if self.max_steps is not None:
+            truncated = self.steps >= self.max_steps
+        else:
+            truncated = None
+        if self.terminated_truncated:
+            if truncated is None:
+                truncated = torch.zeros_like(terminated)
+            return terminated, truncated
+        if truncated is None:
+            return terminated
+        return terminated + truncated
+
+    # ---- spaces -----------------------------------------------------------------------------------
+    def get_action_space(self):
+        if not self.dict_spaces:
+            return spaces.Tuple([self.get_agent_action_space(agent) for agent in self.agents])
+        return spaces.Dict({agent.name: self.get_agent_action_space(agent) for agent in self.agents})
+
+    def get_observation_space(self, observations: Union[List, Dict]):
+        if not self.dict_spaces:
+            return spaces.Tuple(
+                [self.get_agent_observation_space(agent, observations[i]) for i, agent in enumerate(self.agents)]
+            )
+        return spaces.Dict(
+            {agent.name: self.get_agent_observation_space(agent, observations[agent.name]) for agent in self.agents}
+        )
+
+    def get_agent_action_size(self, agent: Agent):
+        if self.continuous_actions:
+            return agent.action.action_size + (self.world.dim_c if not agent.silent else 0)
+        if self.multidiscrete_actions:
+            return agent.action_size + (1 if not agent.silent and self.world.dim_c != 0 else 0)
+        return 1
+
+    def get_agent_action_space(self, agent: Agent):
+        if self.continuous_actions:
+            n_comm = self.world.dim_c if not agent.silent else 0
+            return spaces.Box(
+                low=np.array((-agent.action.u_range_tensor).tolist() + [0] * n_comm, dtype=np.float32),
+                high=np.array(agent.action.u_range_tensor.tolist() + [1] * n_comm, dtype=np.float32),
+                shape=(self.get_agent_action_size(agent),),
+                dtype=np.float32,
+            )
+        if self.multidiscrete_actions:
+            actions = agent.discrete_action_nvec + (
+                [self.world.dim_c] if not agent.silent and self.world.dim_c != 0 else []
+            )
+            return spaces.MultiDiscrete(actions)
+        return spaces.Discrete(
+            math.prod(agent.discrete_action_nvec)
+            * (self.world.dim_c if not agent.silent and self.world.dim_c != 0 else 1)
+        )
+
+    def get_agent_observation_space(self, agent: Agent, obs: AGENT_OBS_TYPE):
+        if isinstance(obs, Tensor):
+            return spaces.Box(low=-np.float32("inf"), high=np.float32("inf"), shape=obs.shape[1:],
+                              dtype=np.float32)
+        if isinstance(obs, Dict):
+            return spaces.Dict({k: self.get_agent_observation_space(agent, v) for k, v in obs.items()})
+        raise NotImplementedError(f"Invalid type of observation {obs} for agent {agent.name}")
+
+    # ---- actions ----------------------------------------------------------------------------------
+    @staticmethod
+    def _u_range_value(agent: Agent, index: int) -> float:
+        r = agent.action.u_range
+        r = r[index] if isinstance(r, Sequence) else r
+        return _f32(r)
+
+    @local_seed(vmas_random_state)
+    def get_random_action(self, agent: Agent) -> torch.Tensor:
+        """Random action with shape ``(agent.batch_dim, agent.action_size)`` (environment.py:524-582)."""
+        if self.continuous_actions:
+            actions = []
+            for action_index in range(agent.action_size):
+                r = self._u_range_value(agent, action_index)
+                actions.append(
+                    torch.zeros(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(-r, r)
+                )
+            if self.world.dim_c != 0 and not agent.silent:
+                for _ in range(self.world.dim_c):
+                    actions.append(
+                        torch.zeros(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(0, 1)
+                    )
+            return torch.stack(actions, dim=-1)
+        action_space = self.get_agent_action_space(agent)
+        if self.multidiscrete_actions:
+            actions = [
+                torch.randint(low=0, high=int(action_space.nvec[i]), size=(agent.batch_dim,), device=agent.device)
+                for i in range(action_space.shape[0])
+            ]
+            return torch.stack(actions, dim=-1)
+        return torch.randint(low=0, high=action_space.n, size=(agent.batch_dim,), device=agent.device)
+
+    def get_random_actions(self) -> Sequence[torch.Tensor]:
+        return [self.get_random_action(agent) for agent in self.agents]
+
+    def _check_discrete_action(self, action: Tensor, low: int, high: int, type: str):
+        assert torch.all(
+            (action >= torch.tensor(low, device=self.device)) * (action < torch.tensor(high, device=self.device))
+        ), f"Discrete {type} actions are out of bounds, allowed int range [{low},{high})"
+
+    def _validate_continuous_actions(self, actions):
+        """NaN + range checks of every agent with one host sync (environment.py:621-623, 653-655)."""
+        checks = []
+        for action, agent in zip(actions, self.agents):
+            action = action.detach()
+            physical = action[..., : agent.action_size]
+            if self.clamp_action:
+                r = agent.action.u_range_tensor.unsqueeze(0).expand(physical.shape)
+                physical = physical.clamp(-r, r)
+            checks.append(action.isnan().any())
+            checks.append(torch.any(torch.abs(physical) > agent.action.u_range_tensor))
+        flags = torch.stack(checks).tolist()
+        for i, agent in enumerate(self.agents):
+            assert not flags[2 * i]
+            assert not flags[2 * i + 1], (
+                f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
+            )
+
+    def _set_action(self, action, agent, validated: bool = False):
+        action = action.clone()
+        comm_action = None
+        if not self.grad_enabled:
+            action = action.detach()
+        action = action.to(self.device)
+        if not validated:
+            assert not action.isnan().any()
+        agent.action.u = torch.zeros(self.batch_dim, agent.action_size, device=self.device, dtype=torch.float32)
+        assert action.shape[1] == self.get_agent_action_size(agent), (
+            f"Agent {agent.name} has wrong action size, got {action.shape[1]}, "
+            f"expected {self.get_agent_action_size(agent)}"
+        )
+        if self.clamp_action and self.continuous_actions:
+            physical_action = action[..., : agent.action_size]
+            a_range = agent.action.u_range_tensor.unsqueeze(0).expand(physical_action.shape)
+            physical_action = physical_action.clamp(-a_range, a_range)
+            if self.world.dim_c > 0 and not agent.silent:
+                comm_action = action[..., agent.action_size:]
+                action = torch.cat([physical_action, comm_action.clamp(0, 1)], dim=-1)
+            else:
+                action = physical_action
+        action_index = 0
+        if self.continuous_actions:
+            physical_action = action[:, action_index: action_index + agent.action_size]
+            action_index += self.world.dim_p
+            if not validated:
+                assert not torch.any(torch.abs(physical_action) > agent.action.u_range_tensor), (
+                    f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
+                )
+            agent.action.u = physical_action.to(torch.float32)
+        else:
+            if not self.multidiscrete_actions:
+                # flat index of the cartesian product of the discrete spaces -> multi-discrete
+                flat_action = action.squeeze(-1)
+                actions = []
+                nvec = list(agent.discrete_action_nvec) + (
+                    [self.world.dim_c] if not agent.silent and self.world.dim_c != 0 else []
+                )
+                for i in range(len(nvec)):
+                    n = math.prod(nvec[i + 1:])
+                    actions.append(flat_action // n)
+                    flat_action = flat_action % n
+                action = torch.stack(actions, dim=-1)
+            for n in agent.discrete_action_nvec:
+                physical_action = action[:, action_index]
+                self._check_discrete_action(physical_action.unsqueeze(-1), low=0, high=n, type="physical")
+                u_max = agent.action.u_range_tensor[action_index]
+                # odd n: action 0 maps to u = 0 (swap 0 with the middle value)
+                if n % 2 != 0:
+                    stay = physical_action == 0
+                    decrement = (physical_action > 0) & (physical_action <= n // 2)
+                    physical_action[stay] = n // 2
+                    physical_action[decrement] -= 1
+                agent.action.u[:, action_index] = (physical_action / (n - 1)) * (2 * u_max) - u_max
+                action_index += 1
+        agent.action.u *= agent.action.u_multiplier_tensor
+        if agent.action.u_noise > 0:
+            noise = torch.randn(*agent.action.u.shape, device=self.device, dtype=torch.float32) * agent.u_noise
+            agent.action.u += noise
+        if self.world.dim_c > 0 and not agent.silent:
+            if not self.continuous_actions:
+                comm_action = action[:, action_index:]
+                self._check_discrete_action(comm_action, 0, self.world.dim_c, "communication")
+                comm_action = comm_action.long()
+                agent.action.c = torch.zeros(self.num_envs, self.world.dim_c, device=self.device, dtype=torch.float32)
+                agent.action.c.scatter_(1, comm_action, 1)
+            else:
+                if comm_action is None:
+                    comm_action = action[:, action_index:]
+                assert not torch.any(comm_action > 1) and not torch.any(comm_action < 0), (
+                    "Comm actions are out of range [0,1]"
+                )
+                agent.action.c = comm_action
+            if agent.c_noise > 0:
+                noise = torch.randn(*agent.action.c.shape, device=self.device, dtype=torch.float32) * agent.c_noise
+                agent.action.c += noise
+
+    def render(self, *args, **kwargs):
+        raise NotImplementedError("rendering is not part of the MI355X engine")
+
+    @override(TorchVectorizedObject)
+    def to(self, device: DEVICE_TYPING):
+        device = torch.device(device)
+        self.scenario.to(device)
+        super().to(device)

@@ -1,0 +1,92 @@
+"""The Scenario plugin API (restates vmas/simulator/scenario.py:24-451).
+
+Scenarios subclass ``BaseScenario`` and implement ``make_world``, ``reset_world_at``,
+``observation`` and ``reward`` (optionally ``done``, ``info``, ``process_action``,
+``pre_step``, ``post_step``), exactly as with the reference.
+"""
+import typing
+from abc import ABC, abstractmethod
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from .core import Agent, World
+from .utils import AGENT_INFO_TYPE, AGENT_OBS_TYPE, AGENT_REWARD_TYPE, INITIAL_VIEWER_SIZE, VIEWER_DEFAULT_ZOOM
+
+
+class BaseScenario(ABC):
+    def __init__(self):
+        """Do not override."""
+        self._world = None
+        self.viewer_size = INITIAL_VIEWER_SIZE
+        self.viewer_zoom = VIEWER_DEFAULT_ZOOM
+        self.render_origin = (0.0, 0.0)
+        self.plot_grid = False
+        self.grid_spacing = 0.1
+        self.visualize_semidims = True
+
+    @property
+    def world(self):
+        assert self._world is not None, "You first need to set `self._world` in the `make_world` method"
+        return self._world
+
+    def to(self, device: torch.device):
+        for attr, value in self.__dict__.items():
+            if isinstance(value, Tensor):
+                self.__dict__[attr] = value.to(device)
+        self.world.to(device)
+
+    def env_make_world(self, batch_dim: int, device: torch.device, **kwargs) -> World:
+        # Do not override
+        self._world = self.make_world(batch_dim, device, **kwargs)
+        return self._world
+
+    def env_reset_world_at(self, env_index: typing.Optional[int]):
+        # Do not override
+        self.world.reset(env_index)
+        self.reset_world_at(env_index)
+
+    def env_process_action(self, agent: Agent):
+        # Do not override
+        if agent.action_script is not None:
+            agent.action_callback(self.world)
+        self.process_action(agent)
+        agent.dynamics.check_and_process_action()
+
+    @abstractmethod
+    def make_world(self, batch_dim: int, device: torch.device, **kwargs) -> World:
+        raise NotImplementedError()
+
+    @abstractmethod
+    def reset_world_at(self, env_index: Optional[int] = None):
+        raise NotImplementedError()
+
+    @abstractmethod
+    def observation(self, agent: Agent) -> AGENT_OBS_TYPE:
+        raise NotImplementedError()
+
+    @abstractmethod
+    def reward(self, agent: Agent) -> AGENT_REWARD_TYPE:
+        raise NotImplementedError()
+
+    def done(self) -> Tensor:
+        return torch.tensor([False], device=self.world.device).expand(self.world.batch_dim)
+
+    def info(self, agent: Agent) -> AGENT_INFO_TYPE:
+        return {}
+
+    def extra_render(self, env_index: int = 0):
+        return []
+
+    def top_layer_render(self, env_index: int = 0):
+        return []
+
+    def process_action(self, agent: Agent):
+        return
+
+    def pre_step(self):
+        return
+
+    def post_step(self):
+        return

@@ -1,0 +1,236 @@
+"""Constants and helpers of the simulator surface (restates vmas/simulator/utils.py).
+
+Physical constants are the reference's (utils.py:27-34).  ``TorchUtils`` keeps the reference's
+tensor helpers for scenario code; the physics step itself does not use them (it runs in the
+native engine, see ``_engine.py``).
+"""
+from __future__ import annotations
+
+import typing
+import warnings
+from abc import ABC, abstractmethod
+from enum import Enum
+from typing import Dict, List, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+
+X = 0
+Y = 1
+Z = 2
+ALPHABET = "ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+VIEWER_DEFAULT_ZOOM = 1.2
+INITIAL_VIEWER_SIZE = (700, 700)
+LINE_MIN_DIST = 4 / 6e2
+COLLISION_FORCE = 100
+JOINT_FORCE = 130
+TORQUE_CONSTRAINT_FORCE = 1
+
+DRAG = 0.25
+LINEAR_FRICTION = 0.0
+ANGULAR_FRICTION = 0.0
+
+DEVICE_TYPING = Union[torch.device, str, int]
+
+AGENT_OBS_TYPE = Union[Tensor, Dict[str, Tensor]]
+AGENT_INFO_TYPE = Dict[str, Tensor]
+AGENT_REWARD_TYPE = Tensor
+
+OBS_TYPE = Union[List[AGENT_OBS_TYPE], Dict[str, AGENT_OBS_TYPE]]
+INFO_TYPE = Union[List[AGENT_INFO_TYPE], Dict[str, AGENT_INFO_TYPE]]
+REWARD_TYPE = Union[List[AGENT_REWARD_TYPE], Dict[str, AGENT_REWARD_TYPE]]
+DONE_TYPE = Tensor
+
+
+class Color(Enum):
+    # utils.py:49-61 defines YELLOW twice, which makes the reference's Enum raise at import;
+    # the first definition is kept here.
+    YELLOW = (0.75, 0.75, 0.25)
+    RED = (0.75, 0.25, 0.25)
+    GREEN = (0.25, 0.75, 0.25)
+    BLUE = (0.25, 0.25, 0.75)
+    LIGHT_GREEN = (0.45, 0.95, 0.45)
+    WHITE = (0.75, 0.75, 0.75)
+    GRAY = (0.25, 0.25, 0.25)
+    BLACK = (0.15, 0.15, 0.15)
+    ORANGE = (1.00, 0.50, 0)
+    PINK = (0.97, 0.51, 0.75)
+    PURPLE = (0.60, 0.31, 0.64)
+
+
+def override(cls):
+    """Decorator documenting a method override (checks that the name exists on ``cls``)."""
+
+    def check_override(method):
+        if method.__name__ not in dir(cls):
+            raise NameError(f"{method} does not override any method of {cls}")
+        return method
+
+    return check_override
+
+
+class Observable:
+    def __init__(self):
+        self._observers = []
+
+    def subscribe(self, observer):
+        self._observers.append(observer)
+
+    def notify_observers(self, *args, **kwargs):
+        for obs in self._observers:
+            obs.notify(self, *args, **kwargs)
+
+    def unsubscribe(self, observer):
+        self._observers.remove(observer)
+
+
+class Observer(ABC):
+    @abstractmethod
+    def notify(self, observable, *args, **kwargs):
+        raise NotImplementedError
+
+
+def extract_nested_with_index(data: Union[Tensor, Dict[str, Tensor]], index: int):
+    if isinstance(data, Tensor):
+        return data[index]
+    if isinstance(data, Dict):
+        return {k: extract_nested_with_index(v, index) for k, v in data.items()}
+    raise NotImplementedError(f"Invalid type of data {data}")
+
+
+class TorchUtils:
+    @staticmethod
+    def clamp_with_norm(tensor: Tensor, max_norm: float):
+        norm = torch.linalg.vector_norm(tensor, dim=-1)
+        new_tensor = (tensor / norm.unsqueeze(-1)) * max_norm
+        cond = (norm > max_norm).unsqueeze(-1).expand(tensor.shape)
+        return torch.where(cond, new_tensor, tensor)
+
+    @staticmethod
+    def rotate_vector(vector: Tensor, angle: Tensor):
+        if len(angle.shape) == len(vector.shape):
+            angle = angle.squeeze(-1)
+        assert vector.shape[:-1] == angle.shape
+        assert vector.shape[-1] == 2
+        cos = torch.cos(angle)
+        sin = torch.sin(angle)
+        return torch.stack(
+            [vector[..., X] * cos - vector[..., Y] * sin, vector[..., X] * sin + vector[..., Y] * cos],
+            dim=-1,
+        )
+
+    @staticmethod
+    def cross(vector_a: Tensor, vector_b: Tensor):
+        return (vector_a[..., X] * vector_b[..., Y] - vector_a[..., Y] * vector_b[..., X]).unsqueeze(-1)
+
+    @staticmethod
+    def compute_torque(f: Tensor, r: Tensor) -> Tensor:
+        return TorchUtils.cross(r, f)
+
+    @staticmethod
+    def to_numpy(data):
+        if isinstance(data, Tensor):
+            return data.cpu().detach().numpy()
+        if isinstance(data, Dict):
+            return {k: TorchUtils.to_numpy(v) for k, v in data.items()}
+        if isinstance(data, Sequence):
+            return [TorchUtils.to_numpy(v) for v in data]
+        raise NotImplementedError(f"Invalid type of data {data}")
+
+    @staticmethod
+    def recursive_clone(value):
+        if isinstance(value, Tensor):
+            return value.clone()
+        return {k: TorchUtils.recursive_clone(v) for k, v in value.items()}
+
+    @staticmethod
+    def recursive_require_grad_(value):
+        if isinstance(value, Tensor) and torch.is_floating_point(value):
+            value.requires_grad_(True)
+        elif isinstance(value, Dict):
+            for v in value.values():
+                TorchUtils.recursive_require_grad_(v)
+        else:
+            for v in value:
+                TorchUtils.recursive_require_grad_(v)
+
+    @staticmethod
+    def where_from_index(env_index, new_value, old_value):
+        mask = torch.zeros_like(old_value, dtype=torch.bool, device=old_value.device)
+        mask[env_index] = True
+        return torch.where(mask, new_value, old_value)
+
+
+class ScenarioUtils:
+    """Reset-time helpers (utils.py:239-330)."""
+
+    @staticmethod
+    def spawn_entities_randomly(
+        entities,
+        world,
+        env_index: int,
+        min_dist_between_entities: float,
+        x_bounds: Tuple[int, int],
+        y_bounds: Tuple[int, int],
+        occupied_positions: Tensor = None,
+        disable_warn: bool = False,
+    ):
+        batch_size = world.batch_dim if env_index is None else 1
+        if occupied_positions is None:
+            occupied_positions = torch.zeros((batch_size, 0, world.dim_p), device=world.device)
+        for entity in entities:
+            pos = ScenarioUtils.find_random_pos_for_entity(
+                occupied_positions, env_index, world, min_dist_between_entities, x_bounds, y_bounds,
+                disable_warn,
+            )
+            occupied_positions = torch.cat([occupied_positions, pos], dim=1)
+            entity.set_pos(pos.squeeze(1), batch_index=env_index)
+
+    @staticmethod
+    def find_random_pos_for_entity(
+        occupied_positions: Tensor,
+        env_index: int,
+        world,
+        min_dist_between_entities: float,
+        x_bounds: Tuple[int, int],
+        y_bounds: Tuple[int, int],
+        disable_warn: bool = False,
+    ):
+        batch_size = world.batch_dim if env_index is None else 1
+        pos = None
+        tries = 0
+        while True:
+            proposed_pos = torch.cat(
+                [
+                    torch.empty((batch_size, 1, 1), device=world.device, dtype=torch.float32).uniform_(*x_bounds),
+                    torch.empty((batch_size, 1, 1), device=world.device, dtype=torch.float32).uniform_(*y_bounds),
+                ],
+                dim=2,
+            )
+            if pos is None:
+                pos = proposed_pos
+            if occupied_positions.shape[1] == 0:
+                break
+            dist = torch.cdist(occupied_positions, pos)
+            overlaps = torch.any((dist < min_dist_between_entities).squeeze(2), dim=1)
+            if torch.any(overlaps, dim=0):
+                pos[overlaps] = proposed_pos[overlaps]
+            else:
+                break
+            tries += 1
+            if tries > 50_000 and not disable_warn:
+                warnings.warn(
+                    "It is taking many iterations to spawn the entity, make sure the bounds or "
+                    "the min_dist_between_entities are not too tight to fit all entities."
+                    "You can disable this warning by setting disable_warn=True"
+                )
+        return pos
+
+    @staticmethod
+    def check_kwargs_consumed(dictionary_of_kwargs: Dict, warn: bool = True):
+        if len(dictionary_of_kwargs) > 0:
+            message = f"Scenario kwargs: {dictionary_of_kwargs} passed but not used by the scenario."
+            if warn:
+                warnings.warn(message + " This will turn into an error in future versions.")
+            else:
+                raise ValueError(message)
