@@ -1,0 +1,220 @@
+"""Benchmark: env-steps/s of ``env.step(env.get_random_actions())`` (BASELINE.json metric).
+
+Default workload (BASELINE configs[1], C2): 'balance', 32 768 envs per GPU, n_agents=4,
+10 physics substeps, continuous random actions U(-1, 1).  One process per GPU (weak scaling:
+every rank simulates its own 32 768 independent envs, no data-path collective).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus:
+  roofline      -- HBM roofline of the dominant kernel (k_step), timed with HIP events on its
+                   launch stream inside the library; algorithmic bytes per env-step from
+                   SURVEY.md §8d (24*E_all + 24*E_dyn + 12*A)
+  cpu_baseline  -- the CPU oracle (PyTorch restatement of the reference tensor program) driving
+                   the same host layer, timed on this host on a bounded sample (rank 0, N=1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--scenario", default="balance")
+    p.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    p.add_argument("--n-agents", type=int, default=4)
+    p.add_argument("--substeps", type=int, default=10)
+    p.add_argument("--broadphase", default="batch", choices=["batch", "env"])
+    p.add_argument("--cpu-steps", type=int, default=6, help="timed CPU-oracle steps (0 = skip)")
+    p.add_argument("--cpu-envs", type=int, default=32768)
+    p.add_argument("--device", default=None, help="override device (e.g. cpu for plumbing tests)")
+    return p.parse_args()
+
+
+def make_world_env(args, device, seed):
+    from vectorizedmultiagentsimulator_amd import make_env
+
+    kw = {"n_agents": args.n_agents} if args.scenario in ("balance", "transport", "discovery", "flocking") else {}
+    env = make_env(args.scenario, num_envs=args.envs if device != "cpu-baseline" else args.cpu_envs,
+                   device=device if device != "cpu-baseline" else "cpu", seed=seed, **kw)
+    if args.substeps:
+        env.world._substeps = args.substeps
+        env.world._sub_dt = env.world._dt / args.substeps
+    env.world.broadphase = args.broadphase
+    return env
+
+
+def alg_bytes_per_env_step(world) -> int:
+    """read pos/vel/rot/ang_vel of every entity (24 B), write them for every
+    movable-or-rotatable entity (24 B), read every agent's force + torque (12 B)."""
+    ents = world.entities
+    e_dyn = sum(1 for e in ents if e.movable or e.rotatable)
+    n_agents = len(world.agents)
+    return 24 * len(ents) + 24 * e_dyn + 12 * n_agents
+
+
+def load_traffic(workload: str):
+    """HBM bytes per k_step launch from a committed rocprofv3 PMC summary (profiles/), if any."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def cpu_baseline(args):
+    """Oracle physics (torch CPU, reference op sequence) under the same host layer."""
+    from oracle import vmas_oracle
+
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    env = make_world_env(args, "cpu-baseline", seed=0)
+    vmas_oracle.install(env.world)
+    env.step(env.get_random_actions())  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        env.step(env.get_random_actions())
+    dt = time.perf_counter() - t0
+    return {
+        "value": args.cpu_envs * args.cpu_steps / dt,
+        "unit": "env-steps/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"{args.scenario} {args.cpu_envs} envs x {args.cpu_steps} steps (after 1 warm-up), "
+                  f"substeps={args.substeps}, PyTorch-CPU oracle physics",
+        "ms_per_step": 1e3 * dt / args.cpu_steps,
+    }
+
+
+def main():
+    args = parse()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if (torch.cuda.is_available() and args.device != "cpu") else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+    if args.device is not None:
+        device = args.device
+    else:
+        device = f"cuda:{local_rank}" if torch.cuda.is_available() else "cpu"
+    on_gpu = device.startswith("cuda")
+    if on_gpu:
+        torch.cuda.set_device(torch.device(device))
+
+    env = make_world_env(args, device, seed=rank)
+    world = env.world
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            if on_gpu:
+                dist.barrier(device_ids=[torch.device(device).index])
+            else:
+                dist.barrier()
+
+    for _ in range(args.warmup):
+        env.step(env.get_random_actions())
+    if on_gpu:
+        world.engine.set_timing(True)
+        world.engine.get_timing(reset=True)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        env.step(env.get_random_actions())
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    kernel_ms, launches = world.engine.get_timing(reset=True) if on_gpu else (0.0, 0)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_envs = args.envs * world_size
+    value = total_envs * args.steps / elapsed
+    workload = (f"{args.scenario} {args.envs} envs/GPU, n_agents={args.n_agents}, substeps={args.substeps}, "
+                f"broadphase={args.broadphase}")
+    b_env = alg_bytes_per_env_step(world)
+    roofline = None
+    if on_gpu and launches:
+        per_launch_ms = kernel_ms / launches
+        achieved = b_env * args.envs / (per_launch_ms * 1e-3) / 1e9
+        traffic = load_traffic(workload)
+        roofline = {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "kernel": "k_step",
+            "kernel_us_per_launch": round(per_launch_ms * 1e3, 3),
+            "launches_per_step": round(launches / args.steps, 3),
+            "alg_bytes_per_env_step": b_env,
+        }
+    out = {
+        "metric": "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: scenario reset states (seed = rank), random actions U(-u_range, u_range) each step",
+        "config": {
+            "workload": workload,
+            "scenario": args.scenario,
+            "num_envs_per_gpu": args.envs,
+            "global_envs": total_envs,
+            "n_agents": args.n_agents,
+            "substeps": args.substeps,
+            "parallelism": f"replicas x{world_size} (one process per GPU, no collective in the step)",
+        },
+        "roofline": roofline,
+    }
+    if rank == 0 and world_size == 1 and args.cpu_steps > 0:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

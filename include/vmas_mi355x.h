@@ -212,6 +212,12 @@ int32_t vmas_world_destroy(VmasWorld* world);
  * *iterations (may be NULL) receives the number of kernel passes used. */
 int32_t vmas_world_step(VmasWorld* world, const VmasStepIO* io, void* stream, int32_t* iterations);
 
+/* Measurement hooks (no reference counterpart): when enabled, every k_step launch of this world
+ * is bracketed by HIP events on its launch stream; get_timing resolves them (synchronising on the
+ * events) and returns the accumulated kernel milliseconds and launch count. */
+int32_t vmas_world_set_timing(VmasWorld* world, int32_t enable);
+int32_t vmas_world_get_timing(VmasWorld* world, int32_t reset, double* total_ms, int64_t* launches);
+
 /* World.cast_rays(entity, angles, max_range, entity_filter) with the filter already applied:
  * out[b, r] = min(max_range, min over targets of the ray distance).  angle[b, r] =
  * angles[b*ang_s0 + r*ang_s1] (+ rot_offset[b*rot_s0] when rot_offset != NULL, the Lidar's

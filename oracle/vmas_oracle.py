@@ -893,35 +893,63 @@ def load_snapshot(world, snap: Dict[int, dict]) -> None:
             setattr(s, "_" + k, v.to(dev).clone())
 
 
-def compare(a: Dict[int, dict], b: Dict[int, dict], world=None, atol_pos=1e-5, atol_vel=1e-4, rtol=1e-4):
-    """Max abs differences per field and whether they are within the stated fp32 tolerances."""
+def sensitivity_band(world, snap, expected, broadphase="batch", n=2, eps=1.2e-7, seed=1234):
+    """Per-element fp32 conditioning of one step: max |oracle(perturbed) - oracle| over ``n``
+    random relative input perturbations of ~1 ulp (eps = 2**-23).  A stiff system (joints, tiny
+    inertias) amplifies last-bit differences; the parity tolerance must include that band."""
+    g = torch.Generator().manual_seed(seed)
+    band = {i: {k: torch.zeros_like(v) for k, v in d.items()} for i, d in expected.items()}
+    for _ in range(n):
+        pert = {i: {k: v * (1 + eps * torch.randn(v.shape, generator=g)) for k, v in d.items()}
+                for i, d in snap.items()}
+        out, _ = oracle_step(world, pert, broadphase)
+        for i in band:
+            for k in band[i]:
+                band[i][k] = torch.maximum(band[i][k], (out[i][k] - expected[i][k]).abs().nan_to_num(0.0))
+    return band
+
+
+# Stated fp32 tolerance of one teacher-forced step (SURVEY.md §8c): |got - expected| <=
+#   atol (1e-5 on pos/rot, 1e-4 on vel/ang_vel/force/torque) + rtol 1e-4 * |expected|
+#   + 4 x the oracle's own 1-ulp sensitivity band (when provided)
+# and at most ``max_bad_frac`` of the environments may exceed it (contact cut-offs are
+# discontinuous: a 1-ulp distance difference at dist == dist_min switches a force on/off).
+def compare(a: Dict[int, dict], b: Dict[int, dict], world=None, atol_pos=1e-5, atol_vel=1e-4, rtol=1e-4,
+            band=None, band_factor=4.0, max_bad_frac=0.0):
     worst = {}
-    ok = True
+    bad_envs = None
     for i in a:
         for k, va in a[i].items():
             vb = b[i][k].to(va.device)
             diff = (va - vb).abs()
-            scale = vb.abs()
-            tol = (atol_pos if k in ("pos", "rot") else atol_vel) + rtol * scale
-            bad = diff > tol
-            m = float(diff.max()) if diff.numel() else 0.0
+            tol = (atol_pos if k in ("pos", "rot") else atol_vel) + rtol * vb.abs()
+            if band is not None:
+                tol = tol + band_factor * band[i][k]
+            bad = (diff > tol) | torch.isnan(va).ne(torch.isnan(vb))
+            bad = bad.reshape(bad.shape[0], -1).any(-1)
+            bad_envs = bad if bad_envs is None else (bad_envs | bad)
+            m = float(diff.nan_to_num(0.0).max()) if diff.numel() else 0.0
             name = world.entities[i].name if world is not None else str(i)
             if m > worst.get(k, (0.0, ""))[0]:
                 worst[k] = (m, name)
-            if bool(bad.any()) or bool(torch.isnan(va).ne(torch.isnan(vb)).any()):
-                ok = False
-    return {"ok": ok, "max_abs": {k: v[0] for k, v in worst.items()}, "where": {k: v[1] for k, v in worst.items()}}
+    n_bad = int(bad_envs.sum()) if bad_envs is not None else 0
+    n_env = int(bad_envs.numel()) if bad_envs is not None else 1
+    ok = n_bad <= max_bad_frac * n_env
+    return {"ok": ok, "bad_envs": n_bad, "n_envs": n_env, "max_abs": {k: v[0] for k, v in worst.items()},
+            "where": {k: v[1] for k, v in worst.items()}}
 
 
-def compare_one_step(world, broadphase: str = "batch", **tol):
+def compare_one_step(world, broadphase: str = "batch", with_band: bool = True, **tol):
     """Teacher-forced one-step parity: native engine vs this oracle from the same state."""
     snap = snapshot(world)
-    expected, _ = oracle_step(world, snap, broadphase)
+    expected, ow = oracle_step(world, snap, broadphase)
+    band = sensitivity_band(world, snap, expected, broadphase) if with_band else None
     world.broadphase = broadphase
     world.step()
     got = snapshot(world)
-    rep = compare(got, expected, world, **tol)
+    rep = compare(got, expected, world, band=band, **tol)
     rep["iterations"] = getattr(world.engine, "last_iterations", None)
+    rep["active_pairs_per_substep"] = [len(x) for x in ow.active_log]
     return rep
 
 

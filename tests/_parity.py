@@ -1,0 +1,75 @@
+"""Shared parity drivers: native engine (host backend or gfx950 kernels) vs the CPU oracle."""
+from __future__ import annotations
+
+import torch
+
+from oracle import vmas_oracle as O
+from vectorizedmultiagentsimulator_amd import make_env
+
+# (scenario, kwargs, substeps override) -- every narrowphase class, joints and LIDAR types occur
+SCENARIOS = [
+    ("balance", dict(n_agents=4), 10),       # S-S, L-S, B-S, B-L, world gravity, y semidim
+    ("transport", dict(n_agents=4), None),   # B-S, S-S, heavy box, semidims
+    ("discovery", dict(n_agents=4, use_agent_lidar=True), None),  # S-S, 2 LIDARs
+    ("flocking", dict(n_agents=4), None),    # S-S, scripted agent, LIDAR on obstacles
+    ("pollock", dict(n_agents=4, n_lines=3, n_boxes=3, lidar=True), None),  # all 6 classes + box/line rays
+    ("waterfall", dict(n_agents=5), None),   # joints (rotate / fixed rotation), L-L, B-L, B-B
+]
+
+
+def make(name, kw, substeps, device, num_envs, seed):
+    env = make_env(name, num_envs=num_envs, device=device, seed=seed, **kw)
+    if substeps is not None:
+        env.world._substeps = substeps
+        env.world._sub_dt = env.world._dt / substeps
+    return env
+
+
+def step_parity(env, n_steps, broadphase="batch", max_bad_frac=0.0):
+    """Free-run the engine on random actions; after each step compare one teacher-forced step."""
+    reports = []
+    for _ in range(n_steps):
+        env.step(env.get_random_actions())
+        rep = O.compare_one_step(env.world, broadphase=broadphase, max_bad_frac=max_bad_frac)
+        reports.append(rep)
+    return reports
+
+
+def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0):
+    """Every agent sensor: engine measure() vs the oracle's cast_rays on the same state/angles."""
+    w = env.world
+    snap = O.snapshot(w)
+    ow = O.OracleWorld(w, snap)
+    worst, n_bad, n_tot = 0.0, 0, 0
+    for agent in w.agents:
+        ai = w.entities.index(agent)
+        for sensor in agent.sensors:
+            got = sensor.measure().detach().cpu()
+            angles = sensor._angles.detach().cpu() + snap[ai]["rot"]
+            exp = ow.cast_rays(ai, angles, sensor._max_range, sensor.entity_filter)
+            diff = (got - exp).abs()
+            bad = diff > atol + rtol * exp.abs()
+            worst = max(worst, float(diff.max()))
+            n_bad += int(bad.any(-1).sum())
+            n_tot += got.shape[0]
+    return {"ok": n_bad <= max_bad_frac * max(n_tot, 1), "max_abs": worst, "bad_rows": n_bad, "rows": n_tot}
+
+
+def distance_parity(env, atol=2e-5):
+    """get_distance / is_overlapping for every entity pair: engine vs oracle."""
+    w = env.world
+    snap = O.snapshot(w)
+    ow = O.OracleWorld(w, snap)
+    worst, mism = 0.0, 0
+    ents = w.entities
+    for i, a in enumerate(ents):
+        for j, b in enumerate(ents):
+            if j <= i:
+                continue
+            got = w.get_distance(a, b).detach().cpu()
+            exp = ow.get_distance(ow.ents[i], ow.ents[j])
+            worst = max(worst, float((got - exp).abs().max()))
+            go = w.is_overlapping(a, b).detach().cpu()
+            eo = ow.is_overlapping(ow.ents[i], ow.ents[j])
+            mism += int((go != eo).sum())
+    return {"ok": worst <= atol and mism == 0, "max_abs": worst, "overlap_mismatch": mism}

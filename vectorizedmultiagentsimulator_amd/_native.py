@@ -54,6 +54,8 @@ EXPORTED_SYMBOLS = (
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
+    "vmas_world_set_timing",
+    "vmas_world_get_timing",
     "vmas_cast_rays",
     "vmas_distance",
 )
@@ -256,6 +258,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_world_destroy.argtypes = [_vp]
     lib.vmas_world_step.restype = _i32
     lib.vmas_world_step.argtypes = [_vp, _vp, _vp, _vp]
+    lib.vmas_world_set_timing.restype = _i32
+    lib.vmas_world_set_timing.argtypes = [_vp, _i32]
+    lib.vmas_world_get_timing.restype = _i32
+    lib.vmas_world_get_timing.argtypes = [_vp, _i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     lib.vmas_cast_rays.restype = _i32
     lib.vmas_cast_rays.argtypes = [
         _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,

@@ -218,6 +218,11 @@ struct VmasWorld {
     uint32_t* h_viol = nullptr;      // pinned
     float* d_scratch = nullptr;      // global-memory state rows when LDS is too small
     int W = 1, nblk = 0;
+    // optional kernel timing (HIP events around every k_step launch, on the launch stream)
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
+    double timed_ms = 0.0;
+    long timed_launches = 0;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1035,6 +1040,8 @@ int32_t vmas_world_destroy(VmasWorld* W) {
         if (W->d_viol) (void)hipFree(W->d_viol);
         if (W->h_viol) (void)hipHostFree(W->h_viol);
         if (W->d_scratch) (void)hipFree(W->d_scratch);
+        for (auto& ev : W->ev_pending) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+        for (auto& ev : W->ev_free) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     }
     delete W;
     return VMAS_OK;
@@ -1088,8 +1095,23 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     HIP_TRY(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
     const int max_it = batch_bp ? io->substeps + 2 : 1;
     for (int it = 0; it < max_it; ++it) {
+        std::pair<hipEvent_t, hipEvent_t> ev{};
+        if (W->timing) {
+            if (W->ev_free.empty()) {
+                HIP_TRY(hipEventCreate(&ev.first));
+                HIP_TRY(hipEventCreate(&ev.second));
+            } else {
+                ev = W->ev_free.back();
+                W->ev_free.pop_back();
+            }
+            HIP_TRY(hipEventRecord(ev.first, stream));
+        }
         hipLaunchKernelGGL(k_step, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
         HIP_TRY(hipGetLastError());
+        if (W->timing) {
+            HIP_TRY(hipEventRecord(ev.second, stream));
+            W->ev_pending.push_back(ev);
+        }
         if (iterations) *iterations = it + 1;
         if (!batch_bp) return VMAS_OK;
         hipLaunchKernelGGL(k_flags_reduce, dim3(1), dim3(256), 0, stream, (const uint32_t*)W->d_blk,
@@ -1100,6 +1122,35 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
         if (*W->h_viol == 0u) return VMAS_OK;
     }
     return fail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
+}
+
+int32_t vmas_world_set_timing(VmasWorld* W, int32_t enable) {
+    if (!W) return fail(VMAS_E_INVALID, "null world");
+    W->timing = enable != 0 && W->cfg.device >= 0;
+    return VMAS_OK;
+}
+
+int32_t vmas_world_get_timing(VmasWorld* W, int32_t reset, double* total_ms, int64_t* launches) {
+    if (!W) return fail(VMAS_E_INVALID, "null world");
+    if (W->cfg.device >= 0) {
+        if (int32_t rc = use_device(W->cfg.device)) return rc;
+        for (auto& ev : W->ev_pending) {
+            float ms = 0.f;
+            HIP_TRY(hipEventSynchronize(ev.second));
+            HIP_TRY(hipEventElapsedTime(&ms, ev.first, ev.second));
+            W->timed_ms += ms;
+            W->timed_launches += 1;
+            W->ev_free.push_back(ev);
+        }
+        W->ev_pending.clear();
+    }
+    if (total_ms) *total_ms = W->timed_ms;
+    if (launches) *launches = W->timed_launches;
+    if (reset) {
+        W->timed_ms = 0.0;
+        W->timed_launches = 0;
+    }
+    return VMAS_OK;
 }
 
 int32_t vmas_cast_rays(int32_t device, int32_t batch, int32_t n_rays, const float* origin,

@@ -315,11 +315,26 @@ class PhysicsEngine:
         self._io = N.VmasStepIO()
         self._sig = sig
 
+    # ---- kernel timing (bench.py roofline) --------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        self._ensure()
+        self._timing = bool(enable)
+        N.check(self.lib.vmas_world_set_timing(self._handle, int(enable)), "vmas_world_set_timing")
+
+    def get_timing(self, reset: bool = True):
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        N.check(self.lib.vmas_world_get_timing(self._handle, int(reset), ctypes.byref(ms), ctypes.byref(n)),
+                "vmas_world_get_timing")
+        return ms.value, n.value
+
     def _ensure(self):
         sub = int(self.world._substeps)
         sig = self._signature()
         if sig != self._sig or self._handle is None or sub > self._max_substeps:
             self._build(sig, max(sub, 16))
+            if getattr(self, "_timing", False):
+                N.check(self.lib.vmas_world_set_timing(self._handle, 1), "vmas_world_set_timing")
 
     # ---- the step ---------------------------------------------------------------------------------
     def step(self):
