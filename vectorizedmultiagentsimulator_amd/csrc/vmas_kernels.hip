@@ -201,6 +201,8 @@ struct VmasWorld {
     int nw = 8, chunk = 0, n_chunks = 1;
     std::vector<int32_t> contrib;      // flattened items
     std::vector<int32_t> contrib_off;  // [n_dyn][n_chunks + 1]
+    std::vector<int32_t> sched;        // pair indices, LPT-balanced per (chunk, wave)
+    std::vector<int32_t> sched_off;    // [n_chunks][nw + 1]
     size_t lds_state_floats = 0;       // per block, in floats (state/trig/results/acc/agent rows)
     bool global_scratch = false;
     // device allocations
@@ -212,6 +214,8 @@ struct VmasWorld {
     const int32_t* d_trig = nullptr;
     const int32_t* d_contrib = nullptr;
     const int32_t* d_contrib_off = nullptr;
+    const int32_t* d_sched = nullptr;
+    const int32_t* d_sched_off = nullptr;
     uint32_t* d_mask = nullptr;      // [max_substeps][W]
     uint32_t* d_blk = nullptr;       // [nblk][2][max_substeps][W]
     uint32_t* d_viol = nullptr;      // 1 word
@@ -235,6 +239,8 @@ struct StepK {
     const int32_t* trig;
     const int32_t* contrib;
     const int32_t* contrib_off;
+    const int32_t* sched;
+    const int32_t* sched_off;
     const VmasEntityIO* eio;
     const VmasAgentIO* aio;
     const VmasJointIO* jio;
@@ -423,7 +429,7 @@ __global__ void __launch_bounds__(512) k_step(StepK k) {
         s[0] = p.x; s[64] = p.y; s[128] = v.x; s[192] = v.y; s[256] = r; s[320] = w;
         const int ts = k.trig[e];
         if (ts >= 0) {
-            const Trig t = make_trig(r);
+            const Trig t = make_trig_for(r, k.ed[e].shape == VMAS_BOX);
             float* tt = TR + ts * 4 * 64 + lane;
             tt[0] = t.c0; tt[64] = t.s0; tt[128] = t.c1; tt[192] = t.s1;
         }
@@ -439,9 +445,10 @@ __global__ void __launch_bounds__(512) k_step(StepK k) {
     for (int s = 0; s < k.S; ++s) {
         for (int c = 0; c < k.n_chunks; ++c) {
             const int p0 = c * k.chunk;
-            const int p1 = min(k.P, p0 + k.chunk);
-            // ---- pair phase
-            for (int p = p0 + wave; p < p1; p += nw) {
+            // ---- pair phase: this wave's LPT-balanced share of the chunk's pairs
+            const int t0 = k.sched_off[c * (nw + 1) + wave], t1 = k.sched_off[c * (nw + 1) + wave + 1];
+            for (int t = t0; t < t1; ++t) {
+                const int p = k.sched[t];
                 const VmasPairDesc pd = k.pd[p];
                 bool inr = true;
                 if (pd.cls != VMAS_PAIR_JOINT) inr = norm(g.pos(pd.ea) - g.pos(pd.eb)) <= pd.bp_radius;
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(512) k_step(StepK k) {
                     sb[0] = p.x; sb[64] = p.y; sb[128] = v.x; sb[192] = v.y; sb[256] = rot; sb[320] = w;
                     const int ts = k.trig[e];
                     if (ts >= 0 && (d.flags & VMAS_F_ROTATABLE)) {
-                        const Trig t = make_trig(rot);
+                        const Trig t = make_trig_for(rot, d.shape == VMAS_BOX);
                         float* tt = TR + ts * 4 * 64 + lane;
                         tt[0] = t.c0; tt[64] = t.s0; tt[128] = t.c1; tt[192] = t.s1;
                     }
@@ -562,17 +569,21 @@ __global__ void __launch_bounds__(512) k_step(StepK k) {
 
 // OR the per-block activity words, decide whether the mask was a fixed point, update it if not.
 // blk: [nblk][2][S][W]  (R words then Z words).  One workgroup.
-__global__ void __launch_bounds__(256) k_flags_reduce(const uint32_t* blk, int nblk, int S, int W,
-                                                      uint32_t* mask, uint32_t* viol_out) {
+__global__ void __launch_bounds__(1024) k_flags_reduce(const uint32_t* blk, int nblk, int S, int W,
+                                                       uint32_t* mask, uint32_t* viol_out) {
     __shared__ uint32_t R[1024], Z[1024];
     __shared__ uint32_t viol;
     const int nwords = S * W;
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) { R[w] = 0u; Z[w] = 0u; }
     if (threadIdx.x == 0) viol = 0u;
     __syncthreads();
-    for (int w = 0; w < nwords; ++w) {
+    // thread -> (word, block group): every thread issues independent loads for one word
+    // (nwords <= 1024 = blockDim is enforced by vmas_world_create)
+    const int groups = max(1, (int)blockDim.x / nwords);
+    if ((int)threadIdx.x < groups * nwords) {
+        const int w = threadIdx.x % nwords, g0 = threadIdx.x / nwords;
         uint32_t r = 0u, z = 0u;
-        for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+        for (int i = g0; i < nblk; i += groups) {
             r |= blk[(size_t)i * 2 * nwords + w];
             z |= blk[(size_t)i * 2 * nwords + nwords + w];
         }
@@ -625,7 +636,7 @@ static void host_step_env(const VmasWorld& W, const VmasStepIO& io, const uint32
         vel[e] = hload2(x.vel, x.vel_s0, x.vel_s1, b);
         rot[e] = x.rot[(long)b * x.rot_s0];
         ang[e] = x.ang_vel[(long)b * x.ang_s0];
-        if (W.trig_slot[e] >= 0) tr[e] = make_trig(rot[e]);
+        if (W.trig_slot[e] >= 0) tr[e] = make_trig_for(rot[e], W.ed[e].shape == VMAS_BOX);
     }
     for (int a = 0; a < A; ++a) {
         const VmasAgentIO& x = io.agents[a];
@@ -700,7 +711,7 @@ static void host_step_env(const VmasWorld& W, const VmasStepIO& io, const uint32
             vel[e] = v2;
             rot[e] = r2;
             ang[e] = w2;
-            if (W.trig_slot[e] >= 0 && (d.flags & VMAS_F_ROTATABLE)) tr[e] = make_trig(r2);
+            if (W.trig_slot[e] >= 0 && (d.flags & VMAS_F_ROTATABLE)) tr[e] = make_trig_for(r2, d.shape == VMAS_BOX);
         }
     }
     const int B = W.cfg.batch;
@@ -982,6 +993,28 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
             }
             W->contrib.insert(W->contrib.end(), it.begin(), it.end());
         }
+        // longest-processing-time assignment of each chunk's pairs to the block's waves, with a
+        // static instruction-cost model per narrowphase class (box pairs are 3-35x a sphere pair)
+        static const float kCost[7] = {2.5f, 1.0f, 1.4f, 3.0f, 3.0f, 9.0f, 36.0f};
+        W->sched_off.assign((size_t)W->n_chunks * (W->nw + 1), 0);
+        for (int c = 0; c < W->n_chunks; ++c) {
+            const int p0 = c * chunk, p1 = std::min(P, p0 + chunk);
+            std::vector<int> order;
+            for (int p = p0; p < p1; ++p) order.push_back(p);
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return kCost[W->pd[a].cls] > kCost[W->pd[b].cls]; });
+            std::vector<std::vector<int>> per(W->nw);
+            std::vector<float> load(W->nw, 0.f);
+            for (int p : order) {
+                const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                per[w].push_back(p);
+                load[w] += kCost[W->pd[p].cls];
+            }
+            for (int w = 0; w < W->nw; ++w) {
+                W->sched_off[(size_t)c * (W->nw + 1) + w] = (int32_t)W->sched.size();
+                W->sched.insert(W->sched.end(), per[w].begin(), per[w].end());
+            }
+            W->sched_off[(size_t)c * (W->nw + 1) + W->nw] = (int32_t)W->sched.size();
+        }
         // one allocation for all tables
         size_t off = 0;
         const size_t o_ed = off; off = align_up(off + sizeof(VmasEntityDesc) * std::max(E, 1), 64);
@@ -991,6 +1024,8 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         const size_t o_trig = off; off = align_up(off + 4 * std::max(E, 1), 64);
         const size_t o_c = off; off = align_up(off + 4 * std::max<size_t>(W->contrib.size(), 1), 64);
         const size_t o_co = off; off = align_up(off + 4 * std::max<size_t>(W->contrib_off.size(), 1), 64);
+        const size_t o_s = off; off = align_up(off + 4 * std::max<size_t>(W->sched.size(), 1), 64);
+        const size_t o_so = off; off = align_up(off + 4 * std::max<size_t>(W->sched_off.size(), 1), 64);
         std::vector<char> h(off, 0);
         memcpy(h.data() + o_ed, W->ed.data(), sizeof(VmasEntityDesc) * E);
         memcpy(h.data() + o_pd, W->pd.data(), sizeof(VmasPairDesc) * P);
@@ -999,6 +1034,8 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         memcpy(h.data() + o_trig, W->trig_slot.data(), 4 * E);
         memcpy(h.data() + o_c, W->contrib.data(), 4 * W->contrib.size());
         memcpy(h.data() + o_co, W->contrib_off.data(), 4 * W->contrib_off.size());
+        memcpy(h.data() + o_s, W->sched.data(), 4 * W->sched.size());
+        memcpy(h.data() + o_so, W->sched_off.data(), 4 * W->sched_off.size());
         auto cleanup = [&](int32_t rc) { vmas_world_destroy(W); return rc; };
         if (hipMalloc((void**)&W->d_tables, off) != hipSuccess) return cleanup(fail(VMAS_E_NOMEM, "hipMalloc tables"));
         if (hipMemcpy(W->d_tables, h.data(), off, hipMemcpyHostToDevice) != hipSuccess)
@@ -1010,6 +1047,8 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         W->d_trig = (const int32_t*)(W->d_tables + o_trig);
         W->d_contrib = (const int32_t*)(W->d_tables + o_c);
         W->d_contrib_off = (const int32_t*)(W->d_tables + o_co);
+        W->d_sched = (const int32_t*)(W->d_tables + o_s);
+        W->d_sched_off = (const int32_t*)(W->d_tables + o_so);
         W->nblk = (B + 63) / 64;
         const size_t nwords = (size_t)cfg->max_substeps * W->W;
         if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
@@ -1072,6 +1111,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     StepK k{};
     k.ed = W->d_ed; k.pd = W->d_pd; k.jd = W->d_jd; k.dyn = W->d_dyn; k.trig = W->d_trig;
     k.contrib = W->d_contrib; k.contrib_off = W->d_contrib_off;
+    k.sched = W->d_sched; k.sched_off = W->d_sched_off;
     k.eio = (const VmasEntityIO*)dtab;
     k.aio = (const VmasAgentIO*)((const char*)dtab + oa);
     k.jio = (const VmasJointIO*)((const char*)dtab + oj);
@@ -1114,7 +1154,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
         }
         if (iterations) *iterations = it + 1;
         if (!batch_bp) return VMAS_OK;
-        hipLaunchKernelGGL(k_flags_reduce, dim3(1), dim3(256), 0, stream, (const uint32_t*)W->d_blk,
+        hipLaunchKernelGGL(k_flags_reduce, dim3(1), dim3(1024), 0, stream, (const uint32_t*)W->d_blk,
                            W->nblk, io->substeps, W->W, W->d_mask, W->d_viol);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(W->h_viol, W->d_viol, 4, hipMemcpyDeviceToHost, stream));

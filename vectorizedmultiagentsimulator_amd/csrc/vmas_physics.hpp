@@ -53,6 +53,17 @@ VHD Trig make_trig(float rot) {
     const float r2 = rot + kHalfPi;
     return Trig{cosf(rot), sinf(rot), cosf(r2), sinf(r2)};
 }
+// Lines and joint anchors only use cos/sin(rot); boxes also use the side normal rot + pi/2.
+VHD Trig make_trig_for(float rot, bool box) {
+    if (box) return make_trig(rot);
+    return Trig{cosf(rot), sinf(rot), 0.f, 0.f};
+}
+
+// Wave-uniform vote used for exact early-outs: on gfx950 true iff the predicate holds in every
+// active lane of the wave (so a skipped computation is skipped for all of them); on the host
+// backend (one environment at a time) it is the predicate itself.
+__device__ __forceinline__ bool vote_all(bool b) { return __all(b); }
+__host__ __forceinline__ bool vote_all(bool b) { return b; }
 
 // TorchUtils.clamp_with_norm (utils.py:168-173)
 VHD V2 clamp_with_norm(V2 t, float max_norm) {
@@ -77,6 +88,10 @@ VHD float logaddexp0(float x) {
 VHD V2 constraint_force(V2 pa, V2 pb, float dmin, float sc, float k, bool attractive) {
     const V2 delta = pa - pb;
     const float dist = norm(delta);
+    // The reference zeroes the force where dist < 1e-6 or (repulsive) dist > dmin /
+    // (attractive) dist < dmin; when that holds in every lane the softplus is not needed.
+    const bool zero = (dist < 1e-6f) || (attractive ? (dist < dmin) : (dist > dmin));
+    if (vote_all(zero)) return mk(0.f, 0.f);
     const float x = attractive ? (-(dmin - dist)) / k : (dmin - dist) / k;  // (dmin-dist)*sign/k
     const float pen = logaddexp0(x) * k;
     const float dsafe = (dist > 0.f) ? dist : 1e-8f;
