@@ -228,6 +228,23 @@ int32_t vmas_cast_rays(int32_t device, int32_t batch, int32_t n_rays, const floa
                        const VmasRayTarget* targets, int32_t n_targets, float max_range,
                        float* out, void* stream);
 
+/* Action validation of Environment.step (environment.py:621-623 and 653-655) for all agents in
+ * one pass: flags[2*i] = any NaN in agent i's action, flags[2*i+1] = any |u| > u_range in its
+ * physical columns (after the optional clamp, i.e. never when clamp != 0).  `flags` is a HOST
+ * array; the call returns after the flags are known (one device->host handshake). */
+typedef struct VmasActionRef {
+    const float* u;       /* [B, n_cols] action tensor (any strides) */
+    const float* u_range; /* [n_phys] u_range_tensor on the same device */
+    int32_t s0, s1;
+    int32_t n_cols;       /* columns checked for NaN */
+    int32_t n_phys;       /* leading columns range-checked */
+    int32_t clamp;        /* clamp_actions: the range check cannot fail */
+    int32_t pad;
+} VmasActionRef;
+
+int32_t vmas_check_actions(int32_t device, int32_t batch, const VmasActionRef* refs,
+                           int32_t n_refs, uint8_t* flags, void* stream);
+
 /* Distance queries; out has B floats, or B bytes of 0/1 (torch.bool) for VMAS_OVERLAP_PAIR. */
 int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
                       const VmasShapeRef* b, const float* test_point, int32_t tp_s0,

@@ -1,0 +1,176 @@
+"""Environment / make_env surface (restates the reference's tests/test_vmas.py behaviours on CPU)."""
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from vectorizedmultiagentsimulator_amd import debug_scenarios, make_env, scenarios
+
+ALL = scenarios + debug_scenarios
+
+
+@pytest.mark.parametrize("scenario", ALL)
+@pytest.mark.parametrize("continuous_actions", [True, False])
+def test_random_rollout(scenario, continuous_actions):
+    # test_vmas.py:42-62 (use_vmas_env random loop), dict spaces
+    env = make_env(scenario, num_envs=6, seed=0, continuous_actions=continuous_actions, dict_spaces=True)
+    obs = env.reset()
+    assert set(obs.keys()) == {a.name for a in env.agents}
+    for _ in range(5):
+        obs, rews, dones, info = env.step(env.get_random_actions())
+        assert dones.shape == (6,)
+        for a in env.agents:
+            assert rews[a.name].shape == (6,)
+            o = obs[a.name]
+            assert o.shape[0] == 6 and torch.isfinite(o).all()
+
+
+@pytest.mark.parametrize("scenario", ALL)
+def test_multi_discrete_and_non_dict(scenario):
+    env = make_env(scenario, num_envs=5, seed=0, multidiscrete_actions=True, continuous_actions=False)
+    for _ in range(3):
+        env.step(env.get_random_actions())
+    env = make_env(scenario, num_envs=5, seed=0, continuous_actions=True, dict_spaces=False)
+    for _ in range(3):
+        obs, rews, dones, info = env.step(env.get_random_actions())
+        assert isinstance(obs, list) and len(obs) == env.n_agents
+
+
+@pytest.mark.parametrize("scenario", ALL)
+def test_partial_and_global_reset(scenario):
+    # test_vmas.py:248-274
+    env = make_env(scenario, num_envs=4, seed=0)
+    for i in range(6):
+        env.step(env.get_random_actions())
+        env.reset_at(i % 4)
+        if i == 3:
+            env.reset()
+
+
+@pytest.mark.parametrize("multidiscrete", [True, False])
+def test_discrete_action_mapping(multidiscrete):
+    # test_vmas.py:78-154: odd n maps action 0 to u = 0, the rest evenly in [-U, U]
+    env = make_env("transport", num_envs=7, seed=0, multidiscrete_actions=multidiscrete, continuous_actions=False)
+    random.seed(0)
+    for agent in env.world.agents:
+        agent.discrete_action_nvec = [random.randint(2, 6) for _ in range(agent.action_size)]
+    env.action_space = env.get_action_space()
+    for _ in range(4):
+        actions = env.get_random_actions()
+        for a_batch, s in zip(actions, env.action_space.spaces):
+            for a in a_batch:
+                assert a.numpy() in s
+        env.step(actions)
+        if not multidiscrete:
+            conv = []
+            for a, agent in zip(actions, env.agents):
+                nvec = list(agent.discrete_action_nvec)
+                multi = []
+                flat = a.squeeze(-1)
+                for i in range(len(nvec)):
+                    n = math.prod(nvec[i + 1:])
+                    multi.append(flat // n)
+                    flat = flat % n
+                conv.append(torch.stack(multi, -1))
+            actions = conv
+        for i_a, agent in enumerate(env.agents):
+            for i, n in enumerate(agent.discrete_action_nvec):
+                a = actions[i_a][:, i]
+                u = agent.action.u[:, i]
+                U = agent.action.u_range_tensor[i]
+                k = agent.action.u_multiplier_tensor[i]
+                for aj, uj in zip(a, u):
+                    if n % 2 != 0:
+                        if aj == 0:
+                            assert uj == 0
+                        elif aj <= n // 2:
+                            assert torch.isclose(uj / k, (2 * U * (aj - 1)) / (n - 1) - U)
+                        else:
+                            assert torch.isclose(uj / k, 2 * U * (aj / (n - 1)) - U)
+                    else:
+                        assert torch.isclose(uj / k, 2 * U * (aj / (n - 1)) - U)
+
+
+def test_seeding():
+    # test_vmas.py:307-322: env.seed isolates the env RNG from the user's global RNG
+    env = make_env("balance", num_envs=2, seed=0)
+    env.seed(0)
+    random_obs = env.reset()[0][0, 0]
+    env.seed(0)
+    assert random_obs == env.reset()[0][0, 0]
+    env.seed(0)
+    torch.manual_seed(1)
+    assert random_obs == env.reset()[0][0, 0]
+    torch.manual_seed(0)
+    random_obs = torch.randn(1)
+    torch.manual_seed(0)
+    env.seed(1)
+    env.reset()
+    assert random_obs == torch.randn(1)
+
+
+def test_random_actions_match_per_agent_draws():
+    """get_random_actions (one RNG swap) draws exactly what per-agent get_random_action does."""
+    # the simulator RNG state is class-level (shared by every Environment, environment.py:58-62)
+    e1 = make_env("balance", num_envs=16, seed=3, n_agents=4)
+    e1.seed(5)
+    a1 = e1.get_random_actions()
+    e1.seed(5)
+    a2 = [e1.get_random_action(a) for a in e1.agents]
+    for x, y in zip(a1, a2):
+        assert torch.equal(x, y)
+    np_state = np.random.get_state()[1].copy()
+    e1.get_random_actions()
+    assert np.array_equal(np_state, np.random.get_state()[1])  # global numpy RNG untouched
+
+
+def test_action_validation_errors():
+    env = make_env("balance", num_envs=8, seed=0, n_agents=3)
+    acts = env.get_random_actions()
+    bad = [a.clone() for a in acts]
+    bad[1][3, 0] = float("nan")
+    with pytest.raises(AssertionError):
+        env.step(bad)
+    bad = [a.clone() for a in acts]
+    bad[2][5, 1] = 1.5
+    with pytest.raises(AssertionError, match="out of its range"):
+        env.step(bad)
+    env_c = make_env("balance", num_envs=8, seed=0, n_agents=3, clamp_actions=True)
+    env_c.step(bad)  # clamped: accepted
+    assert float(env_c.agents[2].action.u.abs().max()) <= 0.7 + 1e-6
+
+
+def test_terminated_truncated_and_max_steps():
+    env = make_env("transport", num_envs=3, seed=0, max_steps=2, terminated_truncated=True)
+    out = env.step(env.get_random_actions())
+    assert len(out) == 5
+    _, _, term, trunc, _ = env.step(env.get_random_actions())
+    assert trunc.all()
+
+
+def test_grad_enabled_is_refused_loudly():
+    env = make_env("balance", num_envs=4, seed=0, grad_enabled=True)
+    acts = [a.requires_grad_(True) for a in env.get_random_actions()]
+    with pytest.raises(NotImplementedError):
+        env.step(acts)
+
+
+def test_state_replacement_semantics():
+    """Integrated fields become NEW tensors each step (core.py:2866-2907); old aliases keep
+    their values; static entities keep their tensor objects; user-replaced tensors are read."""
+    env = make_env("balance", num_envs=4, seed=0, n_agents=2)
+    w = env.world
+    line, floor = w.landmarks[2], w.landmarks[3]
+    old_pos = line.state.pos
+    old_vals = old_pos.clone()
+    floor_pos = floor.state.pos
+    env.step(env.get_random_actions())
+    assert line.state.pos is not old_pos and torch.equal(old_pos, old_vals)
+    assert floor.state.pos is floor_pos
+    # user replaces a state tensor between steps: the engine reads the new one
+    line.set_pos(torch.tensor([[0.0, 0.5]]).repeat(4, 1), batch_index=None)
+    line.set_vel(torch.zeros(4, 2), batch_index=None)
+    env.step([torch.zeros(4, 2) for _ in env.agents])
+    assert float(line.state.pos[0, 1]) < 0.5  # fell under gravity from the new position

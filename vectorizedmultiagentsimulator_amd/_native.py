@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "vmas_world_get_timing",
     "vmas_cast_rays",
     "vmas_distance",
+    "vmas_check_actions",
 )
 
 _i32 = ctypes.c_int32
@@ -222,6 +223,19 @@ RAY_TARGET_DTYPE = np.dtype(
         ("pad", "<i4"),
     ]
 )
+ACTION_REF_DTYPE = np.dtype(
+    [
+        ("u", "<u8"),
+        ("u_range", "<u8"),
+        ("s0", "<i4"),
+        ("s1", "<i4"),
+        ("n_cols", "<i4"),
+        ("n_phys", "<i4"),
+        ("clamp", "<i4"),
+        ("pad", "<i4"),
+    ]
+)
+assert ACTION_REF_DTYPE.itemsize == 40
 assert ENTITY_IO_DTYPE.itemsize == 72
 assert AGENT_IO_DTYPE.itemsize == 32
 assert JOINT_IO_DTYPE.itemsize == 16
@@ -266,6 +280,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_cast_rays.argtypes = [
         _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp,
     ]
+    lib.vmas_check_actions.restype = _i32
+    lib.vmas_check_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp]
     lib.vmas_distance.restype = _i32
     lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
     ver = lib.vmas_abi_version()

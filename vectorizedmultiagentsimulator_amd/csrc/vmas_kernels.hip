@@ -396,8 +396,11 @@ __device__ __forceinline__ bool mask_bit(const uint32_t* m, int W, int s, int p)
 }
 
 // ------------------------------------------------------------------------------------------------
-// The fused step kernel.
-__global__ void __launch_bounds__(512) k_step(StepK k) {
+// The fused step kernel.  kGlobalRows = false keeps every row in LDS (the pointers are then
+// provably LDS and compile to ds_read/ds_write); true places the rows of big worlds in a per-block
+// global scratch slab (same layout) when they exceed the LDS budget.
+template <bool kGlobalRows>
+__global__ void __launch_bounds__(512, 4) k_step(StepK k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -408,8 +411,9 @@ __global__ void __launch_bounds__(512) k_step(StepK k) {
 
     uint32_t* FL = reinterpret_cast<uint32_t*>(lds);
     const int nfl = 2 * k.S * k.W;
-    float* base = k.scratch ? (k.scratch + (size_t)blockIdx.x * k.scratch_floats)
-                            : (lds + ((nfl + 3) & ~3));
+    float* base;
+    if constexpr (kGlobalRows) base = k.scratch + (size_t)blockIdx.x * k.scratch_floats;
+    else base = lds + ((nfl + 3) & ~3);
     float* SB = base;
     float* TR = SB + k.E * 6 * 64;
     float* RS = TR + k.n_trig * 4 * 64;
@@ -897,6 +901,32 @@ __global__ void __launch_bounds__(256) k_distance(int B, int kind, VmasShapeRef 
     store_query(out, kind, b, distance_query(kind, a, bref, tp, tp_s0, tp_s1, b));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Action validation: grid (agent, slice of envs); per-block OR then one atomicOr per flag word.
+__global__ void __launch_bounds__(256) k_check_actions(const VmasActionRef* refs, int B, uint32_t* flags) {
+    const VmasActionRef r = refs[blockIdx.y];
+    uint32_t nan_seen = 0u, out_of_range = 0u;
+    const long n = (long)B * r.n_cols;
+    for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
+        const int b = (int)(idx / r.n_cols), c = (int)(idx - (long)b * r.n_cols);
+        const float x = r.u[(long)b * r.s0 + (long)c * r.s1];
+        nan_seen |= (x != x);
+        if (c < r.n_phys && !r.clamp) out_of_range |= (fabsf(x) > r.u_range[c]);
+    }
+    if (__any(nan_seen) && (threadIdx.x & 63) == 0) atomicOr(&flags[2 * blockIdx.y], 1u);
+    if (__any(out_of_range) && (threadIdx.x & 63) == 0) atomicOr(&flags[2 * blockIdx.y + 1], 1u);
+}
+
+namespace {
+struct CheckScratch {
+    int device = -1;
+    uint32_t* d_flags = nullptr;
+    uint32_t* h_flags = nullptr;
+};
+std::mutex g_check_mu;
+std::vector<CheckScratch*> g_checks;
+}  // namespace
+
 // ================================================================================================
 // C ABI
 extern "C" {
@@ -1061,7 +1091,7 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
                 return cleanup(fail(VMAS_E_NOMEM, "hipMalloc state scratch"));
         }
         // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); harmless if refused
-        (void)hipFuncSetAttribute((const void*)k_step, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_step<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         (void)hipGetLastError();
     }
@@ -1146,7 +1176,10 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
             }
             HIP_TRY(hipEventRecord(ev.first, stream));
         }
-        hipLaunchKernelGGL(k_step, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
+        if (W->global_scratch)
+            hipLaunchKernelGGL(k_step<true>, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
+        else
+            hipLaunchKernelGGL(k_step<false>, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
         HIP_TRY(hipGetLastError());
         if (W->timing) {
             HIP_TRY(hipEventRecord(ev.second, stream));
@@ -1230,6 +1263,54 @@ int32_t vmas_cast_rays(int32_t device, int32_t batch, int32_t n_rays, const floa
     const long n = (long)batch * n_rays;
     hipLaunchKernelGGL(k_cast_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, k);
     HIP_TRY(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_check_actions(int32_t device, int32_t batch, const VmasActionRef* refs, int32_t n_refs,
+                           uint8_t* flags, void* stream_) {
+    if (n_refs <= 0) return VMAS_OK;
+    if (!refs || !flags || n_refs > 1024) return fail(VMAS_E_INVALID, "bad action refs");
+    if (device < 0) {
+        for (int i = 0; i < n_refs; ++i) {
+            const VmasActionRef& r = refs[i];
+            bool nan_seen = false, oor = false;
+            for (int b = 0; b < batch; ++b)
+                for (int c = 0; c < r.n_cols; ++c) {
+                    const float x = r.u[(long)b * r.s0 + (long)c * r.s1];
+                    nan_seen |= (x != x);
+                    if (c < r.n_phys && !r.clamp) oor |= (fabsf(x) > r.u_range[c]);
+                }
+            flags[2 * i] = nan_seen;
+            flags[2 * i + 1] = oor;
+        }
+        return VMAS_OK;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    if (int32_t rc = use_device(device)) return rc;
+    CheckScratch* cs = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_check_mu);
+        for (CheckScratch* x : g_checks)
+            if (x->device == device) cs = x;
+        if (!cs) {
+            cs = new CheckScratch();
+            cs->device = device;
+            HIP_TRY(hipMalloc((void**)&cs->d_flags, 2048 * 4));
+            HIP_TRY(hipHostMalloc((void**)&cs->h_flags, 2048 * 4, hipHostMallocDefault));
+            g_checks.push_back(cs);
+        }
+    }
+    const void* dref = nullptr;
+    if (int32_t rc = ring_upload(device, refs, sizeof(VmasActionRef) * n_refs, stream, &dref)) return rc;
+    HIP_TRY(hipMemsetAsync(cs->d_flags, 0, 8 * n_refs, stream));
+    const long per = (long)batch * 2;
+    const unsigned gx = (unsigned)std::max(1L, std::min(64L, (per + 4095) / 4096));
+    hipLaunchKernelGGL(k_check_actions, dim3(gx, n_refs), dim3(256), 0, stream, (const VmasActionRef*)dref,
+                       batch, cs->d_flags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(cs->h_flags, cs->d_flags, 8 * n_refs, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (int i = 0; i < 2 * n_refs; ++i) flags[i] = cs->h_flags[i] != 0u;
     return VMAS_OK;
 }
 

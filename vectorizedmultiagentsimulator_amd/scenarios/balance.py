@@ -108,7 +108,7 @@ class Scenario(BaseScenario):
             self.ground_rew[:] = 0
             self.compute_on_the_ground()
             self.package_dist = torch.linalg.vector_norm(self.package.state.pos - self.package.goal.state.pos, dim=1)
-            self.ground_rew[self.on_the_ground] = self.fall_reward
+            self.ground_rew.masked_fill_(self.on_the_ground, self.fall_reward)  # no host sync
             global_shaping = self.package_dist * self.shaping_factor
             self.pos_rew = self.global_shaping - global_shaping
             self.global_shaping = global_shaping

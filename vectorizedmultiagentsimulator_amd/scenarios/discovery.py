@@ -111,14 +111,15 @@ class Scenario(BaseScenario):
             self.shared_covering_rew[:] = 0
             for a in w.agents:
                 self.shared_covering_rew += self.agent_reward(a)
-            self.shared_covering_rew[self.shared_covering_rew != 0] /= 2
+            scr = self.shared_covering_rew
+            scr.copy_(torch.where(scr != 0, scr / 2, scr))
 
         agent.collision_rew[:] = 0
-        for a in w.agents:
-            if a != agent:
-                agent.collision_rew[w.get_distance(a, agent) < self.min_collision_distance] += (
-                    self.agent_collision_penalty
-                )
+        if self.agent_collision_penalty != 0:  # adding a zero penalty has no effect
+            for a in w.agents:
+                if a != agent:
+                    hit = w.get_distance(a, agent) < self.min_collision_distance
+                    agent.collision_rew += torch.where(hit, float(self.agent_collision_penalty), 0.0)
 
         if is_last:
             if self.targets_respawn:
@@ -132,13 +133,13 @@ class Scenario(BaseScenario):
                         x_bounds=(-w.x_semidim, w.x_semidim), y_bounds=(-w.y_semidim, w.y_semidim),
                     )
                     # in-place update of the target's state (read by the next LIDAR scans)
-                    target.state.pos[self.covered_targets[:, i]] = pos[self.covered_targets[:, i]].squeeze(1)
+                    covered = self.covered_targets[:, i].unsqueeze(-1)
+                    target.state.pos.copy_(torch.where(covered, pos.squeeze(1), target.state.pos))
             else:
                 self.all_time_covered_targets += self.covered_targets
                 for i, target in enumerate(self._targets):
-                    target.state.pos[self.covered_targets[:, i]] = self.get_outside_pos(None)[
-                        self.covered_targets[:, i]
-                    ]
+                    covered = self.covered_targets[:, i].unsqueeze(-1)
+                    target.state.pos.copy_(torch.where(covered, self.get_outside_pos(None), target.state.pos))
         covering_rew = agent.covering_reward if not self.shared_reward else self.shared_covering_rew
         return agent.collision_rew + covering_rew + self.time_rew
 

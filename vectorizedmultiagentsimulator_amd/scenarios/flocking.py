@@ -106,10 +106,11 @@ class Scenario(BaseScenario):
                         if j <= i:
                             continue
                         collision = w.get_distance(a, b) <= self.min_collision_distance
+                        add = torch.where(collision, float(self.collision_reward), 0.0)
                         if a.action_script is None:
-                            a.collision_rew[collision] += self.collision_reward
+                            a.collision_rew += add
                         if b.action_script is None:
-                            b.collision_rew[collision] += self.collision_reward
+                            b.collision_rew += add
         agents_dist_shaping = self._mean_sq_dist_error(agent)
         agent.dist_rew = agent.distance_shaping - agents_dist_shaping
         agent.distance_shaping = agents_dist_shaping

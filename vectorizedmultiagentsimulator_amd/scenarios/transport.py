@@ -74,13 +74,12 @@ class Scenario(BaseScenario):
             for package in self.packages:
                 package.dist_to_goal = torch.linalg.vector_norm(package.state.pos - package.goal.state.pos, dim=1)
                 package.on_goal = w.is_overlapping(package, package.goal)
-                package.color = torch.tensor(Color.RED.value, device=w.device, dtype=torch.float32).repeat(
-                    w.batch_dim, 1
-                )
-                package.color[package.on_goal] = torch.tensor(Color.GREEN.value, device=w.device, dtype=torch.float32)
+                red = torch.tensor(Color.RED.value, device=w.device, dtype=torch.float32)
+                green = torch.tensor(Color.GREEN.value, device=w.device, dtype=torch.float32)
+                package.color = torch.where(package.on_goal.unsqueeze(-1), green, red.expand(w.batch_dim, 3))
                 package_shaping = package.dist_to_goal * self.shaping_factor
-                off = ~package.on_goal
-                self.rew[off] += package.global_shaping[off] - package_shaping[off]
+                # rew[~on_goal] += shaping delta, without a boolean-mask host sync
+                self.rew += torch.where(package.on_goal, 0.0, package.global_shaping - package_shaping)
                 package.global_shaping = package_shaping
         return self.rew
 

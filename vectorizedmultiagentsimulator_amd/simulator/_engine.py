@@ -310,6 +310,14 @@ class PhysicsEngine:
         self.agents = agents
         self.n_out = (n_lin, n_rot, n_force, n_torque)
         self._eio = np.zeros(E, dtype=N.ENTITY_IO_DTYPE)
+        self._ent_cache = None
+        self._agent_cache = None
+        B = w.batch_dim
+        self._lin_rows = np.array([index[id(e)] for e in self.lin_slots], dtype=np.int64)
+        self._rot_rows = np.array([index[id(e)] for e in self.rot_slots], dtype=np.int64)
+        self._lin_slot_bytes = np.arange(len(self.lin_slots), dtype=np.uint64) * np.uint64(8 * B)
+        self._rot_slot_bytes = np.arange(len(self.rot_slots), dtype=np.uint64) * np.uint64(4 * B)
+        self._is_dyn = [bool(e.movable or e.rotatable) for e in ents]
         self._aio = np.zeros(max(len(agents), 1), dtype=N.AGENT_IO_DTYPE)
         self._jio = np.zeros(max(len(joints), 1), dtype=N.JOINT_IO_DTYPE)
         self._io = N.VmasStepIO()
@@ -337,46 +345,60 @@ class PhysicsEngine:
                 N.check(self.lib.vmas_world_set_timing(self._handle, 1), "vmas_world_set_timing")
 
     # ---- the step ---------------------------------------------------------------------------------
+    def _fill_entity_row(self, i, e, dev, B):
+        """(Re)read entity i's state tensors into its pointer-table row; cache them by identity."""
+        st = e._state
+        orig = (st._pos, st._vel, st._rot, st._ang_vel, e._gravity)
+        _check_grad(orig[:4])
+        pos, vel, rot, ang = (self._prep(t, dev) for t in orig[:4])
+        row = self._eio[i]
+        ps, vs = pos.stride(), vel.stride()
+        row["pos"], row["vel"], row["rot"], row["ang"] = pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr()
+        row["pos_s0"], row["pos_s1"], row["vel_s0"], row["vel_s1"] = ps[0], ps[1], vs[0], vs[1]
+        row["rot_s0"], row["ang_s0"] = rot.stride(0), ang.stride(0)
+        g = orig[4]
+        if g is not None:
+            g = self._prep(g, dev).expand(B, 2)
+            row["grav"] = g.data_ptr()
+            row["grav_s0"], row["grav_s1"] = g.stride(0), g.stride(1)
+        else:
+            row["grav"] = 0
+        # keep the converted tensors alive as long as the row points at them
+        self._ent_cache[i] = (orig, (pos, vel, rot, ang, g))
+
+    def _fill_agent_row(self, i, a, dev):
+        st = a._state
+        orig = (st._force, st._torque)
+        _check_grad(orig)
+        f, t = self._prep(orig[0], dev), self._prep(orig[1], dev)
+        row = self._aio[i]
+        fs = f.stride()
+        row["force"], row["torque"] = f.data_ptr(), t.data_ptr()
+        row["force_s0"], row["force_s1"], row["torque_s0"] = fs[0], fs[1], t.stride(0)
+        self._agent_cache[i] = (orig, (f, t))
+
     def step(self):
         self._ensure()
         w = self.world
         dev = self._dev
         B = w.batch_dim
-        ents, agents = self.entities, self.agents
-        keep = []  # tensors converted for the call, kept alive until it returns
-        eio = self._eio
-        for i, e in enumerate(ents):
+        if self._ent_cache is None:
+            self._ent_cache = [None] * len(self.entities)
+            self._agent_cache = [None] * len(self.agents)
+        # pointer tables: only tensors that are not the objects seen last step are re-read
+        for i, e in enumerate(self.entities):
+            c = self._ent_cache[i]
             st = e._state
-            pos, vel, rot, ang = st._pos, st._vel, st._rot, st._ang_vel
-            _check_grad((pos, vel, rot, ang))
-            pos, vel, rot, ang = (self._prep(pos, dev), self._prep(vel, dev), self._prep(rot, dev),
-                                  self._prep(ang, dev))
-            keep += [pos, vel, rot, ang]
-            ps, vs = pos.stride(), vel.stride()
-            row = eio[i]
-            row["pos"], row["vel"], row["rot"], row["ang"] = (
-                pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr())
-            row["pos_s0"], row["pos_s1"], row["vel_s0"], row["vel_s1"] = ps[0], ps[1], vs[0], vs[1]
-            row["rot_s0"], row["ang_s0"] = rot.stride(0), ang.stride(0)
-            g = e._gravity
-            if g is not None:
-                g = self._prep(g, dev).expand(B, 2)
-                keep.append(g)
-                row["grav"] = g.data_ptr()
-                row["grav_s0"], row["grav_s1"] = g.stride(0), g.stride(1)
-            else:
-                row["grav"] = 0
-        aio = self._aio
-        for i, a in enumerate(agents):
+            if (c is None or st._pos is not c[0][0] or st._vel is not c[0][1] or st._rot is not c[0][2]
+                    or st._ang_vel is not c[0][3] or e._gravity is not c[0][4]):
+                self._fill_entity_row(i, e, dev, B)
+        for i, a in enumerate(self.agents):
+            c = self._agent_cache[i]
             st = a._state
-            f, t = st._force, st._torque
-            _check_grad((f, t))
-            f, t = self._prep(f, dev), self._prep(t, dev)
-            keep += [f, t]
-            fs = f.stride()
-            aio[i]["force"], aio[i]["torque"] = f.data_ptr(), t.data_ptr()
-            aio[i]["force_s0"], aio[i]["force_s1"], aio[i]["torque_s0"] = fs[0], fs[1], t.stride(0)
+            if c is None or st._force is not c[0][0] or st._torque is not c[0][1]:
+                self._fill_agent_row(i, a, dev)
         jio = self._jio
+        keep = []
         for i, jc in enumerate(self.joint_list):
             fr = jc.fixed_rotation
             if isinstance(fr, torch.Tensor):
@@ -389,25 +411,17 @@ class PhysicsEngine:
             else:
                 jio[i]["fixed_rotation"] = 0
 
+        # one fresh output buffer: [pos | vel] x n_lin, [rot | ang_vel] x n_rot, force, torque
         n_lin, n_rot, n_force, n_torque = self.n_out
-        total = B * (4 * n_lin + 2 * n_rot + 2 * n_force + n_torque)
-        out = torch.empty(max(total, 1), device=dev, dtype=torch.float32)
-        o = 0
-        views = []
-        for n, width in ((n_lin, 2), (n_lin, 2), (n_rot, 1), (n_rot, 1), (n_force, 2), (n_torque, 1)):
-            views.append(out.narrow(0, o, n * B * width).view(n, B, width) if n else None)
-            o += n * B * width
+        sizes = (n_lin * B * 2, n_lin * B * 2, n_rot * B, n_rot * B, n_force * B * 2, n_torque * B)
+        out = torch.empty(max(sum(sizes), 1), device=dev, dtype=torch.float32)
         base = out.data_ptr()
+        offs = np.cumsum((0,) + sizes[:-1])
         io = self._io
-        io.entities, io.agents, io.joints = eio.ctypes.data, aio.ctypes.data, jio.ctypes.data
-        off = 0
-        ptrs = []
-        for n, width in ((n_lin, 2), (n_lin, 2), (n_rot, 1), (n_rot, 1), (n_force, 2), (n_torque, 1)):
-            ptrs.append(base + 4 * off)
-            off += n * B * width
-        io.out_pos, io.out_vel, io.out_rot, io.out_ang_vel, io.out_force, io.out_torque = ptrs
-        sub = int(w._substeps)
-        io.substeps = sub
+        io.entities, io.agents, io.joints = self._eio.ctypes.data, self._aio.ctypes.data, jio.ctypes.data
+        io.out_pos, io.out_vel, io.out_rot, io.out_ang_vel, io.out_force, io.out_torque = (
+            int(base + 4 * o) for o in offs)
+        io.substeps = int(w._substeps)
         io.sub_dt = _f32(w._dt / w._substeps)
         io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
         iters = ctypes.c_int32(0)
@@ -416,23 +430,45 @@ class PhysicsEngine:
         self.last_iterations = iters.value
         self.steps += 1
         del keep
-        # re-point the integrated fields at the fresh buffer (new tensor objects, as the reference)
+
+        # re-point the integrated fields at views of the fresh buffer (new tensor objects, as the
+        # reference) and update their pointer-table rows in bulk
+        eio = self._eio
         if n_lin:
-            pv, vv = views[0].unbind(0), views[1].unbind(0)
+            pv = out.narrow(0, int(offs[0]), sizes[0]).view(n_lin, B, 2).unbind(0)
+            vv = out.narrow(0, int(offs[1]), sizes[1]).view(n_lin, B, 2).unbind(0)
+            rows = self._lin_rows
+            eio["pos"][rows] = np.uint64(base + 4 * int(offs[0])) + self._lin_slot_bytes
+            eio["vel"][rows] = np.uint64(base + 4 * int(offs[1])) + self._lin_slot_bytes
+            eio["pos_s0"][rows], eio["pos_s1"][rows] = 2, 1
+            eio["vel_s0"][rows], eio["vel_s1"][rows] = 2, 1
             for k, e in enumerate(self.lin_slots):
-                e._state._pos = pv[k]
-                e._state._vel = vv[k]
+                st = e._state
+                st._pos, st._vel = pv[k], vv[k]
         if n_rot:
-            rv, av = views[2].unbind(0), views[3].unbind(0)
+            rv = out.narrow(0, int(offs[2]), sizes[2]).view(n_rot, B, 1).unbind(0)
+            av = out.narrow(0, int(offs[3]), sizes[3]).view(n_rot, B, 1).unbind(0)
+            rows = self._rot_rows
+            eio["rot"][rows] = np.uint64(base + 4 * int(offs[2])) + self._rot_slot_bytes
+            eio["ang"][rows] = np.uint64(base + 4 * int(offs[3])) + self._rot_slot_bytes
+            eio["rot_s0"][rows], eio["ang_s0"][rows] = 1, 1
             for k, e in enumerate(self.rot_slots):
-                e._state._rot = rv[k]
-                e._state._ang_vel = av[k]
+                st = e._state
+                st._rot, st._ang_vel = rv[k], av[k]
+        for i, e in enumerate(self.entities):
+            if self._is_dyn[i]:
+                st = e._state
+                _, conv = self._ent_cache[i]
+                c = (st._pos, st._vel, st._rot, st._ang_vel, e._gravity)
+                lin, rot = e.movable, e.rotatable
+                self._ent_cache[i] = (c, (c[0] if lin else conv[0], c[1] if lin else conv[1],
+                                          c[2] if rot else conv[2], c[3] if rot else conv[3], conv[4]))
         if n_force:
-            fv = views[4].unbind(0)
+            fv = out.narrow(0, int(offs[4]), sizes[4]).view(n_force, B, 2).unbind(0)
             for k, a in enumerate(self.force_slots):
                 a._state._force = fv[k]
         if n_torque:
-            tv = views[5].unbind(0)
+            tv = out.narrow(0, int(offs[5]), sizes[5]).view(n_torque, B, 1).unbind(0)
             for k, a in enumerate(self.torque_slots):
                 a._state._torque = tv[k]
 

@@ -11,6 +11,7 @@ Rendering is outside the scope of the MI355X engine.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import math
 import random
 from typing import Dict, List, Optional, Sequence, Union
@@ -309,6 +310,9 @@ class Environment(TorchVectorizedObject):
     @local_seed(vmas_random_state)
     def get_random_action(self, agent: Agent) -> torch.Tensor:
         """Random action with shape ``(agent.batch_dim, agent.action_size)`` (environment.py:524-582)."""
+        return self._random_action(agent)
+
+    def _random_action(self, agent: Agent) -> torch.Tensor:
         if self.continuous_actions:
             actions = []
             for action_index in range(agent.action_size):
@@ -331,8 +335,11 @@ class Environment(TorchVectorizedObject):
             return torch.stack(actions, dim=-1)
         return torch.randint(low=0, high=action_space.n, size=(agent.batch_dim,), device=agent.device)
 
+    @local_seed(vmas_random_state)
     def get_random_actions(self) -> Sequence[torch.Tensor]:
-        return [self.get_random_action(agent) for agent in self.agents]
+        """Random actions for all agents.  The reference swaps the RNG states once per agent
+        (environment.py:584-606); swapping once around the loop draws the identical streams."""
+        return [self._random_action(agent) for agent in self.agents]
 
     def _check_discrete_action(self, action: Tensor, low: int, high: int, type: str):
         assert torch.all(
@@ -340,17 +347,45 @@ class Environment(TorchVectorizedObject):
         ), f"Discrete {type} actions are out of bounds, allowed int range [{low},{high})"
 
     def _validate_continuous_actions(self, actions):
-        """NaN + range checks of every agent with one host sync (environment.py:621-623, 653-655)."""
-        checks = []
-        for action, agent in zip(actions, self.agents):
-            action = action.detach()
-            physical = action[..., : agent.action_size]
-            if self.clamp_action:
-                r = agent.action.u_range_tensor.unsqueeze(0).expand(physical.shape)
-                physical = physical.clamp(-r, r)
-            checks.append(action.isnan().any())
-            checks.append(torch.any(torch.abs(physical) > agent.action.u_range_tensor))
-        flags = torch.stack(checks).tolist()
+        """NaN + range checks of every agent with one host sync (environment.py:621-623, 653-655).
+
+        fp32 actions (the normal case) are checked by one native kernel (vmas_check_actions);
+        other dtypes keep the reference's torch comparisons in their own dtype."""
+        if all(a.dtype == torch.float32 for a in actions):
+            from ... import _native as N
+
+            n = len(actions)
+            refs = np.zeros(n, dtype=N.ACTION_REF_DTYPE)
+            keep = []
+            for i, (action, agent) in enumerate(zip(actions, self.agents)):
+                a = action.detach()
+                if a.device != self.device:
+                    a = a.to(self.device)
+                r = agent.action.u_range_tensor
+                keep += [a, r]
+                refs[i] = (a.data_ptr(), r.data_ptr(), a.stride(0), a.stride(1), a.shape[1],
+                           agent.action_size, int(bool(self.clamp_action)), 0)
+            flags = np.zeros(2 * max(n, 1), dtype=np.uint8)
+            dev = self.device
+            if dev.type == "cuda":
+                idx = dev.index if dev.index is not None else torch.cuda.current_device()
+                stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
+            else:
+                idx, stream = -1, None
+            N.check(N.load_library().vmas_check_actions(idx, self.num_envs, refs.ctypes.data, n,
+                                                        flags.ctypes.data, stream), "vmas_check_actions")
+            del keep
+        else:
+            checks = []
+            for action, agent in zip(actions, self.agents):
+                action = action.detach()
+                physical = action[..., : agent.action_size]
+                if self.clamp_action:
+                    r = agent.action.u_range_tensor.unsqueeze(0).expand(physical.shape)
+                    physical = physical.clamp(-r, r)
+                checks.append(action.isnan().any())
+                checks.append(torch.any(torch.abs(physical) > agent.action.u_range_tensor))
+            flags = torch.stack(checks).tolist()
         for i, agent in enumerate(self.agents):
             assert not flags[2 * i]
             assert not flags[2 * i + 1], (
