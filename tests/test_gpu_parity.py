@@ -68,3 +68,15 @@ def test_batch_broadphase_fixed_point_gpu(gpu_device):
     rep = O.compare_one_step(w)
     assert rep["ok"], rep
     assert rep["iterations"] >= 1
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("name,kw,substeps", [s for s in SCENARIOS if s[0] in ("balance", "pollock", "waterfall")],
+                         ids=["balance", "pollock", "waterfall"])
+def test_split_box_pairs_gpu(gpu_device, monkeypatch, split, name, kw, substeps):
+    """Box-line / box-box pairs evaluated whole by one wave (split=0) or as per-side parts on
+    several waves plus a finish phase (split=1) give the oracle's result either way."""
+    monkeypatch.setenv("VMAS_SPLIT_PAIRS", split)
+    env = make(name, kw, substeps, gpu_device, num_envs=300, seed=1)
+    for rep in step_parity(env, n_steps=3):
+        assert rep["ok"], rep

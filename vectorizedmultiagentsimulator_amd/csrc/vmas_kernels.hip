@@ -198,10 +198,14 @@ struct VmasWorld {
     // per-dynamic-entity contribution items ((pair << 2) | (side << 1) | torque), reference order
     std::vector<std::vector<int32_t>> items;
     // GPU launch geometry
-    int nw = 8, chunk = 0, n_chunks = 1;
+    int nw = 8, n_chunks = 1, rs_rows = 0;
+    std::vector<int32_t> chunk_p;      // [n_chunks + 1] first pair of each chunk
+    std::vector<int32_t> prow;         // [P] first result row of each pair within its chunk
+    std::vector<int32_t> fin;          // split pairs to finish, per (chunk, wave)
+    std::vector<int32_t> fin_off;      // [n_chunks][nw + 1]
     std::vector<int32_t> contrib;      // flattened items
     std::vector<int32_t> contrib_off;  // [n_dyn][n_chunks + 1]
-    std::vector<int32_t> sched;        // pair indices, LPT-balanced per (chunk, wave)
+    std::vector<int32_t> sched;        // tasks (pair << 4) | part, LPT-balanced per (chunk, wave)
     std::vector<int32_t> sched_off;    // [n_chunks][nw + 1]
     size_t lds_state_floats = 0;       // per block, in floats (state/trig/results/acc/agent rows)
     bool global_scratch = false;
@@ -216,7 +220,10 @@ struct VmasWorld {
     const int32_t* d_contrib_off = nullptr;
     const int32_t* d_sched = nullptr;
     const int32_t* d_sched_off = nullptr;
-    uint32_t* d_mask = nullptr;      // [max_substeps][W]
+    const int32_t* d_prow = nullptr;
+    const int32_t* d_fin = nullptr;
+    const int32_t* d_fin_off = nullptr;
+    uint32_t* d_mask = nullptr;     // [max_substeps][W]
     uint32_t* d_blk = nullptr;       // [nblk][2][max_substeps][W]
     uint32_t* d_viol = nullptr;      // 1 word
     uint32_t* h_viol = nullptr;      // pinned
@@ -241,6 +248,9 @@ struct StepK {
     const int32_t* contrib_off;
     const int32_t* sched;
     const int32_t* sched_off;
+    const int32_t* prow;
+    const int32_t* fin;
+    const int32_t* fin_off;
     const VmasEntityIO* eio;
     const VmasAgentIO* aio;
     const VmasJointIO* jio;
@@ -253,7 +263,7 @@ struct StepK {
     const uint32_t* mask;
     uint32_t* blk;
     float* scratch;
-    int B, E, A, P, W, S, n_dyn, n_trig, chunk, n_chunks;
+    int B, E, A, P, W, S, n_dyn, n_trig, rs_rows, n_chunks;
     size_t scratch_floats;
     float sdt;
     WorldK wk;
@@ -395,6 +405,38 @@ __device__ __forceinline__ bool mask_bit(const uint32_t* m, int W, int s, int p)
     return (m[s * W + (p >> 5)] >> (p & 31)) & 1u;
 }
 
+// Pair-phase task = (pair << 4) | part; part kWholePair evaluates the whole narrowphase, parts
+// 0..split_parts-1 one box side (box-line) or one side-vs-box test (box-box) of a split pair.
+// A split pair's result rows: split_parts x (p1.x, p1.y, p2.x, p2.y), then (pa.x, pa.y, pb.x, pb.y).
+constexpr int kWholePair = 15;
+__host__ __device__ __forceinline__ int split_parts(int cls) { return cls == VMAS_PAIR_BL ? 4 : 8; }
+
+// Finish step of split pair p from its rows r (this lane's column): overwrites the first four rows
+// with the whole-pair result (fa.x, fa.y, ta, tb) and raises the pair's Z bit in zwords
+// (out-of-range pair with a nonzero result) like the pair phase does for whole pairs.
+__device__ __forceinline__ void finish_split(const StepK& k, float* r, int p, bool valid,
+                                             int lane, uint32_t* zwords) {
+    const VmasPairDesc pd = k.pd[p];
+    const int n = split_parts(pd.cls);
+    const float* ctr = r + n * 4 * 64;
+    const V2 pa = mk(ctr[0], ctr[64]), pb = mk(ctr[128], ctr[192]);
+    const Pts q = select_min(n, [&](int i) {
+        const float* x = r + i * 4 * 64;
+        return Pts{mk(x[0], x[64]), mk(x[128], x[192])};
+    });
+    const bool ha = (k.ed[pd.ea].flags & VMAS_F_HOLLOW) != 0;
+    const bool hb = (k.ed[pd.eb].flags & VMAS_F_HOLLOW) != 0;
+    const PairOut o = pd.cls == VMAS_PAIR_BL ? bl_finish(pa, ha, pb, q, pd.dmin, k.wk)
+                                             : bb_finish(pa, ha, pb, hb, q, pd.dmin, k.wk);
+    if (k.blk) {
+        const bool nz = valid && !(norm(pa - pb) <= pd.bp_radius) &&
+                        (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || o.tb != 0.f);
+        const unsigned long long bal = __ballot(nz);
+        if (lane == 0 && bal) atomicOr(&zwords[p >> 5], 1u << (p & 31));
+    }
+    r[0] = o.fa.x; r[64] = o.fa.y; r[128] = o.ta; r[192] = o.tb;
+}
+
 // ------------------------------------------------------------------------------------------------
 // The fused step kernel.  kGlobalRows = false keeps every row in LDS (the pointers are then
 // provably LDS and compile to ds_read/ds_write); true places the rows of big worlds in a per-block
@@ -417,7 +459,7 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
     float* SB = base;
     float* TR = SB + k.E * 6 * 64;
     float* RS = TR + k.n_trig * 4 * 64;
-    float* AC = RS + k.chunk * 4 * 64;
+    float* AC = RS + k.rs_rows * 64;
     float* AF = AC + k.n_dyn * 3 * 64;
     const RowsK g{SB, TR, k.trig, lane};
 
@@ -448,19 +490,38 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
 
     for (int s = 0; s < k.S; ++s) {
         for (int c = 0; c < k.n_chunks; ++c) {
-            const int p0 = c * k.chunk;
-            // ---- pair phase: this wave's LPT-balanced share of the chunk's pairs
+            // ---- pair phase: this wave's LPT-balanced share of the chunk's tasks (a whole pair,
+            // or one part of a split box-line / box-box pair)
             const int t0 = k.sched_off[c * (nw + 1) + wave], t1 = k.sched_off[c * (nw + 1) + wave + 1];
             for (int t = t0; t < t1; ++t) {
-                const int p = k.sched[t];
+                const int task = k.sched[t];
+                const int p = task >> 4, part = task & 15;
                 const VmasPairDesc pd = k.pd[p];
+                float* r = RS + k.prow[p] * 64 + lane;
+                const bool head = part == kWholePair || part == 0;
                 bool inr = true;
-                if (pd.cls != VMAS_PAIR_JOINT) inr = norm(g.pos(pd.ea) - g.pos(pd.eb)) <= pd.bp_radius;
-                if (k.blk) {
+                if (head && pd.cls != VMAS_PAIR_JOINT) inr = norm(g.pos(pd.ea) - g.pos(pd.eb)) <= pd.bp_radius;
+                if (k.blk && head) {
                     const unsigned long long bal = __ballot(inr && valid);
                     if (lane == 0 && bal) atomicOr(&FL[s * k.W + (p >> 5)], 1u << (p & 31));
                 }
                 if (!mask_bit(k.mask, k.W, s, p)) continue;
+                if (part != kWholePair) {
+                    const VmasEntityDesc& da = k.ed[pd.ea];
+                    const VmasEntityDesc& db = k.ed[pd.eb];
+                    const V2 pa = g.pos(pd.ea), pb = g.pos(pd.eb);
+                    const Pts q = pd.cls == VMAS_PAIR_BL
+                        ? bl_part(pa, g.tr(pd.ea), da.half_length, da.half_width, pb, g.tr(pd.eb), db.half_length, part)
+                        : bb_part(pa, g.tr(pd.ea), da.half_length, da.half_width, pb, g.tr(pd.eb),
+                                  db.half_length, db.half_width, part);
+                    float* x = r + part * 4 * 64;
+                    x[0] = q.p1.x; x[64] = q.p1.y; x[128] = q.p2.x; x[192] = q.p2.y;
+                    if (part == 0) {  // the finish step needs the pre-integration centres
+                        float* ctr = r + split_parts(pd.cls) * 4 * 64;
+                        ctr[0] = pa.x; ctr[64] = pa.y; ctr[128] = pb.x; ctr[192] = pb.y;
+                    }
+                    continue;
+                }
                 float fixed_rot = 0.f;
                 if (pd.cls == VMAS_PAIR_JOINT) {
                     const VmasJointIO jio = k.jio[pd.joint];
@@ -468,7 +529,6 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
                                                    : k.jd[pd.joint].fixed_rotation;
                 }
                 const PairOut o = eval_pair(pd, k.ed, k.jd, g, k.wk, fixed_rot);
-                float* r = RS + (p - p0) * 4 * 64 + lane;
                 r[0] = o.fa.x; r[64] = o.fa.y; r[128] = o.ta; r[192] = o.tb;
                 if (k.blk && pd.cls != VMAS_PAIR_JOINT) {
                     const bool nz = valid && !inr &&
@@ -479,6 +539,16 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
                 }
             }
             __syncthreads();
+            // ---- finish phase of the chunk's split pairs (if any)
+            if (k.fin_off[c * (nw + 1) + nw] > k.fin_off[c * (nw + 1)]) {
+                const int f0 = k.fin_off[c * (nw + 1) + wave], f1 = k.fin_off[c * (nw + 1) + wave + 1];
+                for (int t = f0; t < f1; ++t) {
+                    const int p = k.fin[t];
+                    if (!mask_bit(k.mask, k.W, s, p)) continue;
+                    finish_split(k, RS + k.prow[p] * 64 + lane, p, valid, lane, FL + (k.S + s) * k.W);
+                }
+                __syncthreads();
+            }
             // ---- entity phase
             for (int i = wave; i < k.n_dyn; i += nw) {
                 const int e = k.dyn[i];
@@ -514,7 +584,7 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
                     const int it = k.contrib[j];
                     const int p = it >> 2;
                     if (!mask_bit(k.mask, k.W, s, p)) continue;
-                    const float* r = RS + (p - p0) * 4 * 64 + lane;
+                    const float* r = RS + k.prow[p] * 64 + lane;
                     const bool side = (it >> 1) & 1;
                     if (mov) {
                         const float rx = r[0], ry = r[64];
@@ -1005,11 +1075,46 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
                                   (size_t)cfg->n_agents * 3;
         const size_t flags_bytes = align_up((size_t)2 * cfg->max_substeps * W->W * 4, 16);
         const size_t budget = 96 * 1024;
-        int chunk = std::max(1, P);
-        while (chunk > 8 && (fixed_rows + (size_t)chunk * 4) * 256 + flags_bytes > budget) chunk = (chunk + 1) / 2;
-        W->chunk = chunk;
-        W->n_chunks = std::max(1, (P + chunk - 1) / chunk);
-        W->lds_state_floats = (fixed_rows + (size_t)chunk * 4) * 64;
+        // static instruction-cost model per narrowphase class (box pairs are 3-35x a sphere
+        // pair) and per part of a split pair
+        static const float kCost[7] = {2.5f, 1.0f, 1.4f, 3.0f, 3.0f, 9.0f, 36.0f};
+        auto part_cost = [](int cls) { return cls == VMAS_PAIR_BL ? 2.5f : 5.0f; };
+        // Split the box-line / box-box pairs across waves when one of them alone would set the
+        // pair phase's makespan (e.g. balance: one box-line pair = 9 of 41 cost units on 8
+        // waves).  VMAS_SPLIT_PAIRS=0/1 forces the choice (tests run both layouts).
+        float total = 0.f, heaviest = 0.f;
+        for (int p = 0; p < P; ++p) {
+            total += kCost[W->pd[p].cls];
+            heaviest = std::max(heaviest, kCost[W->pd[p].cls]);
+        }
+        bool split = heaviest > total / W->nw;
+        if (const char* env = getenv("VMAS_SPLIT_PAIRS")) {
+            if (env[0] == '0') split = false;
+            if (env[0] == '1') split = true;
+        }
+        auto is_split = [&](int p) {
+            return split && (W->pd[p].cls == VMAS_PAIR_BL || W->pd[p].cls == VMAS_PAIR_BB);
+        };
+        auto rows_of = [&](int p) { return is_split(p) ? 4 * split_parts(W->pd[p].cls) + 4 : 4; };
+        // chunks: consecutive pair ranges whose result rows fit the LDS budget
+        const long room = ((long)budget - (long)flags_bytes) / 256 - (long)fixed_rows;
+        const int row_budget = (int)std::max<long>(32, room);
+        W->prow.assign(P, 0);
+        W->chunk_p.assign(1, 0);
+        W->rs_rows = 0;
+        int rows = 0;
+        for (int p = 0; p < P; ++p) {
+            if (rows > 0 && rows + rows_of(p) > row_budget) {
+                W->chunk_p.push_back(p);
+                rows = 0;
+            }
+            W->prow[p] = rows;
+            rows += rows_of(p);
+            W->rs_rows = std::max(W->rs_rows, rows);
+        }
+        W->chunk_p.push_back(P);
+        W->n_chunks = (int)W->chunk_p.size() - 1;
+        W->lds_state_floats = (fixed_rows + (size_t)W->rs_rows) * 64;
         W->global_scratch = W->lds_state_floats * 4 + flags_bytes > 160 * 1024 - 1024;
         // per-(dyn entity, chunk) item ranges
         W->contrib_off.assign((size_t)n_dyn * (W->n_chunks + 1), 0);
@@ -1017,33 +1122,53 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
             const auto& it = W->items[i];
             size_t j = 0;
             for (int c = 0; c <= W->n_chunks; ++c) {
-                const int plim = std::min(P, c * chunk);
+                const int plim = W->chunk_p[c];
                 while (j < it.size() && (it[j] >> 2) < plim) ++j;
                 W->contrib_off[(size_t)i * (W->n_chunks + 1) + c] = (int32_t)(W->contrib.size() + j);
             }
             W->contrib.insert(W->contrib.end(), it.begin(), it.end());
         }
-        // longest-processing-time assignment of each chunk's pairs to the block's waves, with a
-        // static instruction-cost model per narrowphase class (box pairs are 3-35x a sphere pair)
-        static const float kCost[7] = {2.5f, 1.0f, 1.4f, 3.0f, 3.0f, 9.0f, 36.0f};
+        // longest-processing-time assignment of each chunk's tasks to the block's waves
         W->sched_off.assign((size_t)W->n_chunks * (W->nw + 1), 0);
         for (int c = 0; c < W->n_chunks; ++c) {
-            const int p0 = c * chunk, p1 = std::min(P, p0 + chunk);
-            std::vector<int> order;
-            for (int p = p0; p < p1; ++p) order.push_back(p);
-            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return kCost[W->pd[a].cls] > kCost[W->pd[b].cls]; });
+            std::vector<std::pair<int, float>> tasks;  // (task, cost)
+            for (int p = W->chunk_p[c]; p < W->chunk_p[c + 1]; ++p) {
+                if (is_split(p)) {
+                    for (int i = 0; i < split_parts(W->pd[p].cls); ++i)
+                        tasks.push_back({(p << 4) | i, part_cost(W->pd[p].cls)});
+                } else {
+                    tasks.push_back({(p << 4) | kWholePair, kCost[W->pd[p].cls]});
+                }
+            }
+            std::stable_sort(tasks.begin(), tasks.end(),
+                             [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second > b.second; });
             std::vector<std::vector<int>> per(W->nw);
             std::vector<float> load(W->nw, 0.f);
-            for (int p : order) {
+            for (const auto& t : tasks) {
                 const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-                per[w].push_back(p);
-                load[w] += kCost[W->pd[p].cls];
+                per[w].push_back(t.first);
+                load[w] += t.second;
             }
             for (int w = 0; w < W->nw; ++w) {
                 W->sched_off[(size_t)c * (W->nw + 1) + w] = (int32_t)W->sched.size();
                 W->sched.insert(W->sched.end(), per[w].begin(), per[w].end());
             }
             W->sched_off[(size_t)c * (W->nw + 1) + W->nw] = (int32_t)W->sched.size();
+        }
+        // finish tasks of split pairs: round-robin over the waves, box-box (2 inner points) first
+        W->fin_off.assign((size_t)W->n_chunks * (W->nw + 1), 0);
+        for (int c = 0; c < W->n_chunks; ++c) {
+            std::vector<int> order;
+            for (int p = W->chunk_p[c]; p < W->chunk_p[c + 1]; ++p)
+                if (is_split(p)) order.push_back(p);
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return W->pd[a].cls > W->pd[b].cls; });
+            std::vector<std::vector<int>> per(W->nw);
+            for (size_t i = 0; i < order.size(); ++i) per[i % W->nw].push_back(order[i]);
+            for (int w = 0; w < W->nw; ++w) {
+                W->fin_off[(size_t)c * (W->nw + 1) + w] = (int32_t)W->fin.size();
+                W->fin.insert(W->fin.end(), per[w].begin(), per[w].end());
+            }
+            W->fin_off[(size_t)c * (W->nw + 1) + W->nw] = (int32_t)W->fin.size();
         }
         // one allocation for all tables
         size_t off = 0;
@@ -1056,7 +1181,13 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         const size_t o_co = off; off = align_up(off + 4 * std::max<size_t>(W->contrib_off.size(), 1), 64);
         const size_t o_s = off; off = align_up(off + 4 * std::max<size_t>(W->sched.size(), 1), 64);
         const size_t o_so = off; off = align_up(off + 4 * std::max<size_t>(W->sched_off.size(), 1), 64);
+        const size_t o_pr = off; off = align_up(off + 4 * std::max(P, 1), 64);
+        const size_t o_f = off; off = align_up(off + 4 * std::max<size_t>(W->fin.size(), 1), 64);
+        const size_t o_fo = off; off = align_up(off + 4 * W->fin_off.size(), 64);
         std::vector<char> h(off, 0);
+        memcpy(h.data() + o_pr, W->prow.data(), 4 * P);
+        memcpy(h.data() + o_f, W->fin.data(), 4 * W->fin.size());
+        memcpy(h.data() + o_fo, W->fin_off.data(), 4 * W->fin_off.size());
         memcpy(h.data() + o_ed, W->ed.data(), sizeof(VmasEntityDesc) * E);
         memcpy(h.data() + o_pd, W->pd.data(), sizeof(VmasPairDesc) * P);
         if (cfg->n_joints) memcpy(h.data() + o_jd, W->jd.data(), sizeof(VmasJointDesc) * cfg->n_joints);
@@ -1079,6 +1210,9 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         W->d_contrib_off = (const int32_t*)(W->d_tables + o_co);
         W->d_sched = (const int32_t*)(W->d_tables + o_s);
         W->d_sched_off = (const int32_t*)(W->d_tables + o_so);
+        W->d_prow = (const int32_t*)(W->d_tables + o_pr);
+        W->d_fin = (const int32_t*)(W->d_tables + o_f);
+        W->d_fin_off = (const int32_t*)(W->d_tables + o_fo);
         W->nblk = (B + 63) / 64;
         const size_t nwords = (size_t)cfg->max_substeps * W->W;
         if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
@@ -1142,6 +1276,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     k.ed = W->d_ed; k.pd = W->d_pd; k.jd = W->d_jd; k.dyn = W->d_dyn; k.trig = W->d_trig;
     k.contrib = W->d_contrib; k.contrib_off = W->d_contrib_off;
     k.sched = W->d_sched; k.sched_off = W->d_sched_off;
+    k.prow = W->d_prow; k.fin = W->d_fin; k.fin_off = W->d_fin_off;
     k.eio = (const VmasEntityIO*)dtab;
     k.aio = (const VmasAgentIO*)((const char*)dtab + oa);
     k.jio = (const VmasJointIO*)((const char*)dtab + oj);
@@ -1153,7 +1288,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     k.scratch = W->global_scratch ? W->d_scratch : nullptr;
     k.scratch_floats = W->lds_state_floats;
     k.B = cfg.batch; k.E = E; k.A = A; k.P = cfg.n_pairs; k.W = W->W; k.S = io->substeps;
-    k.n_dyn = (int)W->dyn.size(); k.n_trig = W->n_trig; k.chunk = W->chunk; k.n_chunks = W->n_chunks;
+    k.n_dyn = (int)W->dyn.size(); k.n_trig = W->n_trig; k.rs_rows = W->rs_rows; k.n_chunks = W->n_chunks;
     k.sdt = io->sub_dt;
     k.wk = WorldK{cfg.contact_margin, cfg.collision_force, cfg.joint_force, cfg.torque_constraint_force};
     k.gx = cfg.gravity_x; k.gy = cfg.gravity_y; k.has_g = cfg.has_world_gravity;

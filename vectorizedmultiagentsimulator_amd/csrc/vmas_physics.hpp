@@ -300,11 +300,41 @@ VHD PairOut pair_bs(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 ps, fl
     return PairOut{fb, cross(cpb - pbx, fb), 0.f};
 }
 
-// _box_line_vectorized_collision (core.py:2553-2652); a = box, b = line
-VHD PairOut pair_bl(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 pl, Trig tl, float hll,
-                    float dmin, const WorldK& w) {
-    V2 pb, plp;
-    closest_line_box(pbx, tbx, hl, hw, Seg{pl, mk(tl.c0, tl.s0), hll}, &pb, &plp);
+// Box-line / box-box narrowphases split into independent parts (one box side / one
+// side-vs-box test each) plus a finish step, so that several waves can evaluate one pair.  The
+// finish step replays the reference's "first strict minimum" selection over the parts in order,
+// hence split and fused evaluation are bit-identical.
+struct Pts {
+    V2 p1, p2;
+};
+VHD Pts bl_part(V2 pbx, Trig tbx, float hl, float hw, V2 pl, Trig tl, float hll, int side) {
+    Pts r;
+    closest_points_line_line(box_side(pbx, tbx, hl, hw, side), Seg{pl, mk(tl.c0, tl.s0), hll}, &r.p1, &r.p2);
+    return r;
+}
+VHD Pts bb_part(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, float hlb, float hwb, int i) {
+    Pts r;
+    if (i < 4) closest_line_box(pb, tb, hlb, hwb, box_side(pa, ta, hla, hwa, i), &r.p2, &r.p1);
+    else closest_line_box(pa, ta, hla, hwa, box_side(pb, tb, hlb, hwb, i - 4), &r.p1, &r.p2);
+    return r;
+}
+template <class PartFn>
+VHD Pts select_min(int n, PartFn part) {
+    Pts best{mk(INFINITY, INFINITY), mk(INFINITY, INFINITY)};
+    float bd = INFINITY;
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) {
+        const Pts q = part(i);
+        const float d = norm(q.p1 - q.p2);
+        if (d < bd) {
+            bd = d;
+            best = q;
+        }
+    }
+    return best;
+}
+VHD PairOut bl_finish(V2 pbx, bool hollow, V2 pl, Pts q, float dmin, const WorldK& w) {
+    const V2 pb = q.p1, plp = q.p2;
     V2 inner = pb;
     float d = 0.f;
     if (!hollow) inner = inner_point_box(plp, pb, pbx, &d);
@@ -312,12 +342,8 @@ VHD PairOut pair_bl(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 pl, Tr
     const V2 fline = -fbox;
     return PairOut{fbox, cross(pb - pbx, fbox), cross(plp - pl, fline)};
 }
-
-// _box_box_vectorized_collision (core.py:2654-2785)
-VHD PairOut pair_bb(V2 pa, Trig ta, float hla, float hwa, bool hol_a, V2 pb, Trig tb, float hlb,
-                    float hwb, bool hol_b, float dmin, const WorldK& w) {
-    V2 qa, qb;
-    closest_box_box(pa, ta, hla, hwa, pb, tb, hlb, hwb, &qa, &qb);
+VHD PairOut bb_finish(V2 pa, bool hol_a, V2 pb, bool hol_b, Pts q, float dmin, const WorldK& w) {
+    const V2 qa = q.p1, qb = q.p2;
     V2 ia = qa, ib = qb;
     float da = 0.f, db = 0.f;
     if (!hol_a) ia = inner_point_box(qb, qa, pa, &da);
@@ -325,6 +351,20 @@ VHD PairOut pair_bb(V2 pa, Trig ta, float hla, float hwa, bool hol_a, V2 pb, Tri
     const V2 fa = constraint_force(ia, ib, (da + db) + dmin, w.c, w.k, false);
     const V2 fb = -fa;
     return PairOut{fa, cross(qa - pa, fa), cross(qb - pb, fb)};
+}
+
+// _box_line_vectorized_collision (core.py:2553-2652); a = box, b = line
+VHD PairOut pair_bl(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 pl, Trig tl, float hll,
+                    float dmin, const WorldK& w) {
+    const Pts q = select_min(4, [&](int i) { return bl_part(pbx, tbx, hl, hw, pl, tl, hll, i); });
+    return bl_finish(pbx, hollow, pl, q, dmin, w);
+}
+
+// _box_box_vectorized_collision (core.py:2654-2785)
+VHD PairOut pair_bb(V2 pa, Trig ta, float hla, float hwa, bool hol_a, V2 pb, Trig tb, float hlb,
+                    float hwb, bool hol_b, float dmin, const WorldK& w) {
+    const Pts q = select_min(8, [&](int i) { return bb_part(pa, ta, hla, hwa, pb, tb, hlb, hwb, i); });
+    return bb_finish(pa, hol_a, pb, hol_b, q, dmin, w);
 }
 
 // TorchUtils.rotate_vector (utils.py:176-191) with precomputed cos/sin of the angle

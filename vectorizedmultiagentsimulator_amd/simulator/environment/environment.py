@@ -315,15 +315,16 @@ class Environment(TorchVectorizedObject):
     def _random_action(self, agent: Agent) -> torch.Tensor:
         if self.continuous_actions:
             actions = []
+            # (uniform_ overwrites every element: empty() draws the same numbers as zeros())
             for action_index in range(agent.action_size):
                 r = self._u_range_value(agent, action_index)
                 actions.append(
-                    torch.zeros(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(-r, r)
+                    torch.empty(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(-r, r)
                 )
             if self.world.dim_c != 0 and not agent.silent:
                 for _ in range(self.world.dim_c):
                     actions.append(
-                        torch.zeros(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(0, 1)
+                        torch.empty(agent.batch_dim, device=agent.device, dtype=torch.float32).uniform_(0, 1)
                     )
             return torch.stack(actions, dim=-1)
         action_space = self.get_agent_action_space(agent)
@@ -400,7 +401,8 @@ class Environment(TorchVectorizedObject):
         action = action.to(self.device)
         if not validated:
             assert not action.isnan().any()
-        agent.action.u = torch.zeros(self.batch_dim, agent.action_size, device=self.device, dtype=torch.float32)
+        if not self.continuous_actions:  # (the continuous branch below replaces u outright)
+            agent.action.u = torch.zeros(self.batch_dim, agent.action_size, device=self.device, dtype=torch.float32)
         assert action.shape[1] == self.get_agent_action_size(agent), (
             f"Agent {agent.name} has wrong action size, got {action.shape[1]}, "
             f"expected {self.get_agent_action_size(agent)}"
