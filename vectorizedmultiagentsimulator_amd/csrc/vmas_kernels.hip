@@ -1079,19 +1079,12 @@ int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* enti
         // pair) and per part of a split pair
         static const float kCost[7] = {2.5f, 1.0f, 1.4f, 3.0f, 3.0f, 9.0f, 36.0f};
         auto part_cost = [](int cls) { return cls == VMAS_PAIR_BL ? 2.5f : 5.0f; };
-        // Split the box-line / box-box pairs across waves when one of them alone would set the
-        // pair phase's makespan (e.g. balance: one box-line pair = 9 of 41 cost units on 8
-        // waves).  VMAS_SPLIT_PAIRS=0/1 forces the choice (tests run both layouts).
-        float total = 0.f, heaviest = 0.f;
-        for (int p = 0; p < P; ++p) {
-            total += kCost[W->pd[p].cls];
-            heaviest = std::max(heaviest, kCost[W->pd[p].cls]);
-        }
-        bool split = heaviest > total / W->nw;
-        if (const char* env = getenv("VMAS_SPLIT_PAIRS")) {
-            if (env[0] == '0') split = false;
-            if (env[0] == '1') split = true;
-        }
+        // Optionally split the box-line / box-box pairs across waves (VMAS_SPLIT_PAIRS=1; the
+        // tests run both layouts).  Off by default: on balance (one box-line pair = 9 of 41 cost
+        // units on 8 waves) the extra finish barrier cost more than the shorter pair phase saved
+        // (k_step 112 -> 128 us, SQ_WAIT_ANY +16 %; profiles/r01/run4).
+        bool split = false;
+        if (const char* env = getenv("VMAS_SPLIT_PAIRS")) split = env[0] == '1';
         auto is_split = [&](int p) {
             return split && (W->pd[p].cls == VMAS_PAIR_BL || W->pd[p].cls == VMAS_PAIR_BB);
         };
