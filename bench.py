@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=6, help="timed CPU-oracle steps (0 = skip)")
     p.add_argument("--cpu-envs", type=int, default=32768)
     p.add_argument("--device", default=None, help="override device (e.g. cpu for plumbing tests)")
+    p.add_argument("--kw", default="{}", help='extra scenario kwargs as JSON, e.g. \'{"use_agent_lidar": true}\'')
     return p.parse_args()
 
 
@@ -51,6 +52,7 @@ def make_world_env(args, device, seed):
     from vectorizedmultiagentsimulator_amd import make_env
 
     kw = {"n_agents": args.n_agents} if args.scenario in ("balance", "transport", "discovery", "flocking") else {}
+    kw.update(json.loads(args.kw))
     env = make_env(args.scenario, num_envs=args.envs if device != "cpu-baseline" else args.cpu_envs,
                    device=device if device != "cpu-baseline" else "cpu", seed=seed, **kw)
     if args.substeps:
@@ -164,8 +166,10 @@ def main():
 
     total_envs = args.envs * world_size
     value = total_envs * args.steps / elapsed
-    workload = (f"{args.scenario} {args.envs} envs/GPU, n_agents={args.n_agents}, substeps={args.substeps}, "
+    workload = (f"{args.scenario} {args.envs} envs/GPU, n_agents={args.n_agents}, substeps={world._substeps}, "
                 f"broadphase={args.broadphase}")
+    if json.loads(args.kw):
+        workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)
     roofline = None
     if on_gpu and launches:
@@ -203,7 +207,7 @@ def main():
             "num_envs_per_gpu": args.envs,
             "global_envs": total_envs,
             "n_agents": args.n_agents,
-            "substeps": args.substeps,
+            "substeps": world._substeps,
             "parallelism": f"replicas x{world_size} (one process per GPU, no collective in the step)",
         },
         "roofline": roofline,

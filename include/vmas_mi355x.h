@@ -250,6 +250,27 @@ int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasSha
                       const VmasShapeRef* b, const float* test_point, int32_t tp_s0,
                       int32_t tp_s1, void* out, void* stream);
 
+/* Spawn sampler: one batch of tries of ScenarioUtils.find_random_pos_for_entity
+ * (vmas/simulator/utils.py:272-319; rows "next" #3 of SURVEY.md §8f).  Implemented in
+ * csrc/vmas_spawn.hip.
+ *   occupied    [B, n_occ, 2] (element strides occ_s0/s1/s2); n_occ may be 0
+ *   candidates  [n_tries][2][B]: try k of env b = (x, y) = (c[k*2B + b], c[k*2B + B + b]), drawn by
+ *               the caller with the reference's torch uniform_ calls
+ *   resolved    [B] int32, -1 for envs still searching; set to the global try index (first_try + k)
+ *               of the first candidate whose torch.cdist distance to every occupied position is
+ *               >= min_dist (fp32), whose (x, y) is then written to pos [B][2]
+ *   max_accepted / n_unresolved: host int32 outputs (max accepted index, envs still searching);
+ *               the call synchronises `stream` to return them.
+ * The reference loop consumes 1 try if every env accepts try 0, else max_accepted + 2 tries. */
+int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied, int32_t n_occ,
+                           int32_t occ_s0, int32_t occ_s1, int32_t occ_s2, const float* candidates,
+                           int32_t first_try, int32_t n_tries, float min_dist, float* pos,
+                           int32_t* resolved, int32_t* max_accepted, int32_t* n_unresolved,
+                           void* stream);
+
+/* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
+const char* vmas_aux_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -965,3 +965,29 @@ def install(world) -> None:
                 setattr(s, "_" + k, v)
 
     world.step = step
+
+
+# ------------------------------------------------------------------------------------------------
+# ScenarioUtils.find_random_pos_for_entity (reference vmas/simulator/utils.py:272-319), the
+# reference's per-try loop (torch.cdist + torch.any host sync), for the spawn-sampler parity tests.
+def find_random_pos_for_entity(occupied_positions, batch_size, device, min_dist_between_entities, x_bounds, y_bounds):
+    pos = None
+    while True:
+        proposed_pos = torch.cat(
+            [
+                torch.empty((batch_size, 1, 1), device=device, dtype=torch.float32).uniform_(*x_bounds),
+                torch.empty((batch_size, 1, 1), device=device, dtype=torch.float32).uniform_(*y_bounds),
+            ],
+            dim=2,
+        )
+        if pos is None:
+            pos = proposed_pos
+        if occupied_positions.shape[1] == 0:
+            break
+        dist = torch.cdist(occupied_positions, pos)
+        overlaps = torch.any((dist < min_dist_between_entities).squeeze(2), dim=1)
+        if torch.any(overlaps, dim=0):
+            pos[overlaps] = proposed_pos[overlaps]
+        else:
+            break
+    return pos

@@ -59,6 +59,8 @@ EXPORTED_SYMBOLS = (
     "vmas_cast_rays",
     "vmas_distance",
     "vmas_check_actions",
+    "vmas_spawn_resolve",
+    "vmas_aux_last_error",
 )
 
 _i32 = ctypes.c_int32
@@ -284,6 +286,12 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_check_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp]
     lib.vmas_distance.restype = _i32
     lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
+    lib.vmas_spawn_resolve.restype = _i32
+    lib.vmas_spawn_resolve.argtypes = [
+        _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _f32, _vp, _vp,
+        ctypes.POINTER(_i32), ctypes.POINTER(_i32), _vp,
+    ]
+    lib.vmas_aux_last_error.restype = ctypes.c_char_p
     ver = lib.vmas_abi_version()
     if ver != VMAS_ABI_VERSION:
         raise NativeLibraryError(f"ABI version mismatch: library {ver}, python {VMAS_ABI_VERSION}")
@@ -295,4 +303,11 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load_library().vmas_last_error().decode(errors="replace")
+        raise NativeLibraryError(f"{what} failed ({rc}): {msg}")
+
+
+def check_aux(rc: int, what: str) -> None:
+    """Error check of the auxiliary entry points (csrc/vmas_spawn.hip)."""
+    if rc != 0:
+        msg = load_library().vmas_aux_last_error().decode(errors="replace")
         raise NativeLibraryError(f"{what} failed ({rc}): {msg}")

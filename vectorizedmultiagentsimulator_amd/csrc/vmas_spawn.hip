@@ -1,0 +1,158 @@
+// vmas_spawn.hip -- rejection-sampling resolver for ScenarioUtils.find_random_pos_for_entity
+// (reference vmas/simulator/utils.py:272-319), gfx950 kernel + host backend + C ABI.
+//
+// The reference loop draws a full [B,1,2] proposal per try (x then y, torch uniform_), checks
+// every env's current position against the occupied positions with torch.cdist, replaces the
+// overlapping envs' positions with the new proposal, and stops at the first try where no env
+// overlaps -- one host sync and ~10 kernels per try.  Per env, the accepted position is therefore
+// the FIRST candidate that overlaps nothing (a non-overlapping position never changes again), and
+// the number of tries the loop consumes is 1 if every env accepts candidate 0, else
+// max_env(first accepted index) + 2.  The host side draws the candidates with the same torch
+// calls (so the random numbers are the reference's), this kernel resolves a whole batch of tries
+// at once, and the host rewinds the generator to exactly the reference's consumption.
+//
+// Distance: torch.cdist (p = 2) computes sqrt(fl(fl(d0^2) + fl(d1^2))) with d = a - b on both the
+// CUDA/HIP kernel (per-dim squares, then a shuffle-reduction add) and the CPU kernel; the
+// comparison `dist < min_dist` runs in fp32.  Compiled with -ffp-contract=off like the engine.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <mutex>
+#include <string>
+
+#include "vmas_mi355x.h"
+
+namespace {
+
+std::string g_aux_err;
+std::mutex g_aux_mu;
+
+int32_t aux_fail(int32_t code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_aux_err = buf;
+    return code;
+}
+
+#define AUX_HIP(x)                                                                            \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) return aux_fail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+struct SpawnArgs {
+    int B, n_occ, occ_s0, occ_s1, occ_s2;
+    const float* occ;
+    const float* cand;  // [n_tries][2][B]: candidate k of env b = (cand[k*2B + b], cand[k*2B + B + b])
+    int first_try, n_tries;
+    float min_dist;
+    float* pos;         // [B][2]
+    int32_t* resolved;  // [B], -1 = not yet
+};
+
+__host__ __device__ inline bool overlaps(const SpawnArgs& a, int b, float x, float y) {
+    bool hit = false;
+    for (int j = 0; j < a.n_occ; ++j) {
+        const float* o = a.occ + (long)b * a.occ_s0 + (long)j * a.occ_s1;
+        const float d0 = o[0] - x, d1 = o[a.occ_s2] - y;
+        const float dist = sqrtf(d0 * d0 + d1 * d1);
+        hit = hit || (dist < a.min_dist);
+    }
+    return hit;
+}
+
+// resolve env b over this batch's candidates; returns its accepted index or -1
+__host__ __device__ inline int resolve_env(const SpawnArgs& a, int b) {
+    int r = a.resolved[b];
+    if (r >= 0) return r;
+    for (int k = 0; k < a.n_tries; ++k) {
+        const float x = a.cand[(long)k * 2 * a.B + b], y = a.cand[(long)k * 2 * a.B + a.B + b];
+        if (!overlaps(a, b, x, y)) {
+            a.pos[2 * (long)b] = x;
+            a.pos[2 * (long)b + 1] = y;
+            a.resolved[b] = a.first_try + k;
+            return a.first_try + k;
+        }
+    }
+    return -1;
+}
+
+// out[0] = max accepted index over envs, out[1] = number of unresolved envs
+__global__ void __launch_bounds__(256) k_spawn_resolve(SpawnArgs a, int32_t* out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    int r = 0, unresolved = 0;
+    if (b < a.B) {
+        r = resolve_env(a, b);
+        unresolved = r < 0;
+    }
+    // wave-level max / count, then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        r = max(r, __shfl_xor(r, off));
+        unresolved += __shfl_xor(unresolved, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&out[0], r);
+        if (unresolved) atomicAdd(&out[1], unresolved);
+    }
+}
+
+struct DevScratch {
+    int32_t* d_out = nullptr;
+    int32_t* h_out = nullptr;
+};
+DevScratch g_scratch[64];
+
+}  // namespace
+
+extern "C" {
+
+const char* vmas_aux_last_error(void) { return g_aux_err.c_str(); }
+
+int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied, int32_t n_occ,
+                           int32_t occ_s0, int32_t occ_s1, int32_t occ_s2, const float* candidates,
+                           int32_t first_try, int32_t n_tries, float min_dist, float* pos,
+                           int32_t* resolved, int32_t* max_accepted, int32_t* n_unresolved,
+                           void* stream) {
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    if (batch <= 0 || n_occ < 0 || n_tries <= 0 || first_try < 0 || !candidates || !pos || !resolved ||
+        !max_accepted || !n_unresolved || (n_occ > 0 && !occupied))
+        return aux_fail(VMAS_E_INVALID, "vmas_spawn_resolve: bad argument");
+    SpawnArgs a{batch, n_occ, occ_s0, occ_s1, occ_s2, occupied, candidates, first_try, n_tries, min_dist,
+                pos, resolved};
+    if (device < 0) {
+        int mx = 0, un = 0;
+        for (int b = 0; b < batch; ++b) {
+            const int r = resolve_env(a, b);
+            if (r < 0) ++un;
+            else mx = r > mx ? r : mx;
+        }
+        *max_accepted = mx;
+        *n_unresolved = un;
+        return VMAS_OK;
+    }
+    if (device >= 64) return aux_fail(VMAS_E_INVALID, "vmas_spawn_resolve: device %d", device);
+    int cur = -1;
+    AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) AUX_HIP(hipSetDevice(device));
+    DevScratch& s = g_scratch[device];
+    if (!s.d_out) {
+        AUX_HIP(hipMalloc((void**)&s.d_out, 2 * sizeof(int32_t)));
+        AUX_HIP(hipHostMalloc((void**)&s.h_out, 2 * sizeof(int32_t), hipHostMallocDefault));
+    }
+    hipStream_t st = (hipStream_t)stream;
+    AUX_HIP(hipMemsetAsync(s.d_out, 0, 2 * sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_spawn_resolve, dim3((batch + 255) / 256), dim3(256), 0, st, a, s.d_out);
+    AUX_HIP(hipGetLastError());
+    AUX_HIP(hipMemcpyAsync(s.h_out, s.d_out, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    AUX_HIP(hipStreamSynchronize(st));
+    *max_accepted = s.h_out[0];
+    *n_unresolved = s.h_out[1];
+    return VMAS_OK;
+}
+
+}  // extern "C"

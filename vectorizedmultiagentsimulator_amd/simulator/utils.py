@@ -6,6 +6,7 @@ native engine, see ``_engine.py``).
 """
 from __future__ import annotations
 
+import ctypes
 import typing
 import warnings
 from abc import ABC, abstractmethod
@@ -196,34 +197,71 @@ class ScenarioUtils:
         y_bounds: Tuple[int, int],
         disable_warn: bool = False,
     ):
+        """Rejection sampling of utils.py:272-319 with the same random numbers and the same
+        generator consumption, resolved natively (``vmas_spawn_resolve``).
+
+        The reference draws a [B,1,2] proposal per try (x then y), replaces the positions of the
+        envs that overlap an occupied position (torch.cdist < min_dist), and stops at the first
+        try where no env overlaps; each env thus keeps its first non-overlapping candidate and the
+        loop consumes 1 try (all envs accept try 0) or max accepted index + 2 tries.  Here the
+        tries are drawn with the reference's uniform_ calls in batches, one native call per batch
+        finds every env's first non-overlapping candidate (one sync per batch instead of one per
+        try), and the generator is rewound to the state after exactly the reference's tries.
+        """
         batch_size = world.batch_dim if env_index is None else 1
-        pos = None
-        tries = 0
+        dev = torch.device(world.device)
+
+        def draw(shape_x, out_x=None, out_y=None):
+            x = torch.empty(shape_x, device=dev, dtype=torch.float32) if out_x is None else out_x
+            y = torch.empty(shape_x, device=dev, dtype=torch.float32) if out_y is None else out_y
+            return x.uniform_(*x_bounds), y.uniform_(*y_bounds)
+
+        if occupied_positions.shape[1] == 0:
+            x, y = draw((batch_size, 1, 1))
+            return torch.cat([x, y], dim=2)
+
+        from .. import _native as N
+
+        lib = N.load_library()
+        if dev.type == "cuda":
+            dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+            gen = torch.cuda.default_generators[dev_index]
+            stream = torch.cuda.current_stream(dev_index).cuda_stream
+        else:
+            dev_index, gen, stream = -1, torch.default_generator, None
+        occ = occupied_positions.detach()
+        if occ.dtype != torch.float32:
+            occ = occ.float()
+        pos = torch.empty((batch_size, 1, 2), device=dev, dtype=torch.float32)
+        resolved = torch.full((batch_size,), -1, device=dev, dtype=torch.int32)
+        states = []  # generator state after each try, to rewind to the reference's consumption
+        first, n = 0, 8
+        mx, un = N._i32(0), N._i32(0)
         while True:
-            proposed_pos = torch.cat(
-                [
-                    torch.empty((batch_size, 1, 1), device=world.device, dtype=torch.float32).uniform_(*x_bounds),
-                    torch.empty((batch_size, 1, 1), device=world.device, dtype=torch.float32).uniform_(*y_bounds),
-                ],
-                dim=2,
-            )
-            if pos is None:
-                pos = proposed_pos
-            if occupied_positions.shape[1] == 0:
+            cand = torch.empty((n, 2, batch_size), device=dev, dtype=torch.float32)
+            for k in range(n):
+                draw(None, cand[k, 0], cand[k, 1])
+                states.append(gen.get_state())
+            N.check_aux(lib.vmas_spawn_resolve(
+                dev_index, batch_size, occ.data_ptr(), occ.shape[1], occ.stride(0), occ.stride(1), occ.stride(2),
+                cand.data_ptr(), first, n, float(torch.tensor(min_dist_between_entities, dtype=torch.float32)),
+                pos.data_ptr(), resolved.data_ptr(), ctypes.byref(mx), ctypes.byref(un), stream),
+                "vmas_spawn_resolve")
+            if un.value == 0:
                 break
-            dist = torch.cdist(occupied_positions, pos)
-            overlaps = torch.any((dist < min_dist_between_entities).squeeze(2), dim=1)
-            if torch.any(overlaps, dim=0):
-                pos[overlaps] = proposed_pos[overlaps]
-            else:
-                break
-            tries += 1
-            if tries > 50_000 and not disable_warn:
+            first += n
+            n = min(2 * n, 64)
+            if first > 50_000 and not disable_warn:
                 warnings.warn(
                     "It is taking many iterations to spawn the entity, make sure the bounds or "
                     "the min_dist_between_entities are not too tight to fit all entities."
                     "You can disable this warning by setting disable_warn=True"
                 )
+        consumed = 1 if mx.value == 0 else mx.value + 2
+        if consumed <= len(states):
+            gen.set_state(states[consumed - 1])
+        else:  # the reference's final (unused) proposal lies just past the last batch
+            draw((batch_size, 1, 1))
         return pos
 
     @staticmethod
