@@ -71,14 +71,15 @@ def alg_bytes_per_env_step(world) -> int:
     return 24 * len(ents) + 24 * e_dyn + 12 * n_agents
 
 
-def load_traffic(workload: str):
-    """HBM bytes per k_step launch from a committed rocprofv3 PMC summary (profiles/), if any."""
+def load_traffic(workload: str, kernel: str):
+    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC summary (profiles/), if it
+    was measured on this workload and this kernel."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
     try:
         d = json.loads(f.read_text())
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel") == kernel:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -175,7 +176,7 @@ def main():
     if on_gpu and launches:
         per_launch_ms = kernel_ms / launches
         achieved = b_env * args.envs / (per_launch_ms * 1e-3) / 1e9
-        traffic = load_traffic(workload)
+        traffic = load_traffic(workload, world.engine.kernel_name)
         roofline = {
             "bound": "hbm",
             "achieved": round(achieved, 2),
@@ -183,7 +184,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
-            "kernel": "k_step",
+            "kernel": world.engine.kernel_name,
             "kernel_us_per_launch": round(per_launch_ms * 1e3, 3),
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,

@@ -31,7 +31,9 @@
 #ifndef VMAS_MI355X_H
 #define VMAS_MI355X_H
 
+#ifndef __HIPCC_RTC__ /* under hipRTC the types come from csrc/vmas_physics.hpp */
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -270,6 +272,33 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);
+
+/* World-specialised step (csrc/vmas_jit.hip): same seam and semantics as vmas_world_create /
+ * vmas_world_step (World.step, core.py:1971-2014), GPU only.  vmas_jit_world_create generates a
+ * gfx950 kernel for this exact world (constants folded, per-wave straight-line pair/entity code)
+ * and compiles it with hipRTC; it returns VMAS_E_INVALID for worlds beyond its argument-block or
+ * LDS budget, in which case the caller uses vmas_world_step.  Results are bit-identical to
+ * vmas_world_step. */
+typedef struct VmasJitWorld VmasJitWorld;
+int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                              const VmasPairDesc* pairs, const VmasJointDesc* joints,
+                              VmasJitWorld** out_world);
+int32_t vmas_jit_world_destroy(VmasJitWorld* world);
+int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
+                            int32_t* iterations);
+int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
+int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
+                                  int64_t* launches);
+/* Generated source of a world (length returned; copied into buf when buf != NULL). */
+int32_t vmas_jit_world_source(const VmasJitWorld* world, char* buf, int64_t cap);
+/* Generate + compile a world's kernel without a device (build checks); returns the source length. */
+int32_t vmas_jit_compile_check(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                               const VmasPairDesc* pairs, const VmasJointDesc* joints, char* buf,
+                               int64_t cap);
+/* Phase timestamps (s_memtime) of one workgroup from the last launch when the world was created
+ * with VMAS_JIT_PROFILE=<workgroup> set: [max_substeps*4 + 2][8 waves]; returns the count. */
+int32_t vmas_jit_world_profile(VmasJitWorld* world, uint64_t* out, int64_t cap);
+const char* vmas_jit_last_error(void);
 
 #ifdef __cplusplus
 }

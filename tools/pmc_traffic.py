@@ -4,7 +4,7 @@ roofline.traffic.
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports 1/2 of the bytes of
 wide coalesced reads -> doubled; WRITE_SIZE is taken as reported.  Both counters are KiB.
-usage: python tools/pmc_traffic.py <pmc dir with p1 (FETCH_SIZE) and p2 (WRITE_SIZE)> <workload>
+usage: python tools/pmc_traffic.py <pmc dir with p1 (FETCH_SIZE) and p2 (WRITE_SIZE)> <workload> [kernel]
        <alg bytes per launch>
 """
 import csv
@@ -18,7 +18,7 @@ def per_launch(d, counter):
     vals = {}
     for f in glob.glob(f"{d}/**/pmc_counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if "k_step" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+            if ("k_step" in row["Kernel_Name"] or "k_world" in row["Kernel_Name"]) and row["Counter_Name"] == counter:
                 vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for k_step under {d}")
@@ -32,7 +32,7 @@ def main():
     hbm = 2 * fetch_kib * 1024 + write_kib * 1024
     out = {
         "workload": workload,
-        "kernel": "k_step",
+        "kernel": sys.argv[4] if len(sys.argv) > 4 else "k_world",
         "launches_sampled": [n1, n2],
         "fetch_size_kib_per_launch": round(fetch_kib, 1),
         "write_size_kib_per_launch": round(write_kib, 1),

@@ -13,7 +13,10 @@ from vectorizedmultiagentsimulator_amd import make_env  # noqa: E402
 
 scenario = sys.argv[1] if len(sys.argv) > 1 else "balance"
 n_envs = int(sys.argv[2]) if len(sys.argv) > 2 else 32768
-kw = {"n_agents": 4} if scenario != "discovery" else {"n_agents": 8, "use_agent_lidar": True}
+n_agents = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if scenario in ("discovery", "flocking") else 4)
+kw = {"n_agents": n_agents}
+if scenario == "discovery":
+    kw["use_agent_lidar"] = True
 env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, **kw)
 if scenario == "balance":
     env.world._substeps = 10

@@ -61,6 +61,15 @@ EXPORTED_SYMBOLS = (
     "vmas_check_actions",
     "vmas_spawn_resolve",
     "vmas_aux_last_error",
+    "vmas_jit_world_create",
+    "vmas_jit_world_destroy",
+    "vmas_jit_world_step",
+    "vmas_jit_world_set_timing",
+    "vmas_jit_world_get_timing",
+    "vmas_jit_world_source",
+    "vmas_jit_compile_check",
+    "vmas_jit_world_profile",
+    "vmas_jit_last_error",
 )
 
 _i32 = ctypes.c_int32
@@ -292,6 +301,24 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
         ctypes.POINTER(_i32), ctypes.POINTER(_i32), _vp,
     ]
     lib.vmas_aux_last_error.restype = ctypes.c_char_p
+    lib.vmas_jit_world_create.restype = _i32
+    lib.vmas_jit_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
+    lib.vmas_jit_world_destroy.restype = _i32
+    lib.vmas_jit_world_destroy.argtypes = [_vp]
+    lib.vmas_jit_world_step.restype = _i32
+    lib.vmas_jit_world_step.argtypes = [_vp, _vp, _vp, _vp]
+    lib.vmas_jit_world_set_timing.restype = _i32
+    lib.vmas_jit_world_set_timing.argtypes = [_vp, _i32]
+    lib.vmas_jit_world_get_timing.restype = _i32
+    lib.vmas_jit_world_get_timing.argtypes = [_vp, _i32, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_int64)]
+    lib.vmas_jit_world_source.restype = _i32
+    lib.vmas_jit_world_source.argtypes = [_vp, _vp, ctypes.c_int64]
+    lib.vmas_jit_compile_check.restype = _i32
+    lib.vmas_jit_compile_check.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.c_int64]
+    lib.vmas_jit_world_profile.restype = _i32
+    lib.vmas_jit_world_profile.argtypes = [_vp, _vp, ctypes.c_int64]
+    lib.vmas_jit_last_error.restype = ctypes.c_char_p
     ver = lib.vmas_abi_version()
     if ver != VMAS_ABI_VERSION:
         raise NativeLibraryError(f"ABI version mismatch: library {ver}, python {VMAS_ABI_VERSION}")
@@ -303,6 +330,13 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load_library().vmas_last_error().decode(errors="replace")
+        raise NativeLibraryError(f"{what} failed ({rc}): {msg}")
+
+
+def check_jit(rc: int, what: str) -> None:
+    """Error check of the world-specialised step entry points (csrc/vmas_jit.hip)."""
+    if rc < 0:
+        msg = load_library().vmas_jit_last_error().decode(errors="replace")
         raise NativeLibraryError(f"{what} failed ({rc}): {msg}")
 
 

@@ -1,0 +1,1016 @@
+// vmas_jit.hip -- world-specialised step kernels (hipRTC) for the VMAS physics step.
+//
+// vmas_world_step's k_step is generic: every pair and entity is a table row, dispatched at run
+// time.  For a fixed world (VMAS worlds are fixed after make_env), this module generates one HIP
+// kernel for that world and compiles it with hipRTC for gfx950.  It keeps k_step's decomposition
+// and arithmetic:
+//   * one workgroup = 64 envs (lane = env) x 8 waves; per substep a pair phase (each wave its
+//     statically scheduled pair tasks), a barrier, an entity phase (each wave its dynamic
+//     entities: action clamps / friction / gravity, then the pair results in the reference's
+//     summation order, then semi-implicit Euler), a barrier;
+//   * the same vmas_physics.hpp functions with the same fp32 operation order, so results are
+//     bit-identical to k_step and the host backend (tests/test_jit.py);
+// and specialises what k_step looks up at run time:
+//   * per-wave straight-line code for exactly its pair tasks and entities (no descriptor loads,
+//     no class switch); entity/pair/joint/world constants are constexpr, so flag tests fold;
+//   * a dynamic entity's state, velocity and agent force/torque live in its owner wave's
+//     registers for the whole launch; positions, rotations and trig rows are published to LDS;
+//   * box-line / box-box pairs are split into their per-side parts (4 / 8 tasks) on several
+//     waves; a finish task (last in its wave's list) waits for the parts on an LDS counter,
+//     replays the reference's first-strict-minimum selection and finishes the contact.  Every
+//     wave runs all its parts before any finish, so the waits cannot deadlock;
+//   * tasks are placed by longest-processing-time with class costs measured with
+//     tools/jit_phase_profile.py (a contact pair costs several times an out-of-contact one; the
+//     costs are for the contact case);
+//   * the per-call tensor pointers and strides are kernel arguments (no staging upload); static
+//     entities are loaded once; entities in no pair and not dynamic are never read.
+// A single work queue shared by the waves was measured slower (one switch over every pair in the
+// substep loop: the hoisted constants spilled 114 SGPRs, +37 % pair-phase work).
+// Worlds beyond the kernel-argument or LDS budget return VMAS_E_INVALID from
+// vmas_jit_world_create and the caller uses vmas_world_step.
+//
+// Batch-global broadphase (core.py:2796): identical fixed-point scheme to vmas_world_step (R/Z
+// flags per block, a reduction that checks the mask, host re-run on violation).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "vmas_mi355x.h"
+
+namespace {
+
+thread_local std::string g_jit_err;
+
+int32_t jfail(int32_t code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_jit_err = buf;
+    return code;
+}
+
+#define JHIP(x)                                                                                 \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) return jfail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_));    \
+    } while (0)
+
+// exact fp32 literal
+std::string fl(float v) {
+    if (v != v) return "__builtin_nanf(\"\")";
+    if (v == __builtin_huge_valf()) return "__builtin_huge_valf()";
+    if (v == -__builtin_huge_valf()) return "(-__builtin_huge_valf())";
+    char b[64];
+    snprintf(b, sizeof b, "%af", (double)v);
+    return b;
+}
+std::string it(long v) { return std::to_string(v); }
+std::string bl(bool v) { return v ? "true" : "false"; }
+
+constexpr int kNW = 8;
+constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
+constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
+constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
+
+// pointer-table sources of the kernel argument block
+enum Src { S_POS, S_VEL, S_ROT, S_ANG, S_GRAV, S_FORCE, S_TORQUE, S_JFIX };
+
+struct Item {
+    int pair, side, torque;
+};
+constexpr int kWhole = -1, kFinish = -2;
+struct Task {
+    int pair, part;  // kWhole, 0..n-1 (one part of a split pair) or kFinish
+    float cost;
+};
+
+struct Gen {
+    const VmasWorldConfig& cfg;
+    const std::vector<VmasEntityDesc>& ed;
+    const std::vector<VmasPairDesc>& pd;
+    const std::vector<VmasJointDesc>& jd;
+    int E, P, A, J, W, nfl;
+    bool split_boxes = true;
+    long lds_budget = kLdsTwoPerCu;
+    int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
+    std::vector<char> dyn, in_pair, need_trig, need_rot, split;
+    std::vector<int> owner;  // wave owning a dynamic entity / loading a static pair entity
+    std::vector<std::vector<int>> wave_ents, wave_static;
+    std::vector<std::vector<Task>> wave_tasks;
+    std::vector<std::vector<Item>> items;  // per entity, reference order
+    std::vector<int> split_idx;            // per split pair: its LDS completion counter
+    int n_split = 0;
+    // LDS rows (64 floats each)
+    std::vector<int> r_p, r_rot, r_trig, r_res;
+    int n_rows = 0;
+    // argument block
+    std::vector<std::pair<int, int>> ptr_src, str_src;  // (Src, index); strides: (Src*4 + k, index)
+    std::vector<int> ptr_of[8], str_of[8][2];
+    std::string src;
+
+    Gen(const VmasWorldConfig& c, const std::vector<VmasEntityDesc>& e, const std::vector<VmasPairDesc>& p,
+        const std::vector<VmasJointDesc>& j)
+        : cfg(c), ed(e), pd(p), jd(j) {
+        E = c.n_entities;
+        P = c.n_pairs;
+        A = c.n_agents;
+        J = c.n_joints;
+        W = std::max(1, (P + 31) / 32);
+        nfl = 2 * c.max_substeps * W;
+    }
+
+    static int parts(int cls) { return cls == VMAS_PAIR_BL ? 4 : 8; }
+
+    int ptr(Src s, int idx) {
+        int& slot = ptr_of[s][idx];
+        if (slot < 0) {
+            slot = (int)ptr_src.size();
+            ptr_src.push_back({s, idx});
+        }
+        return slot;
+    }
+    int str(Src s, int k, int idx) {
+        int& slot = str_of[s][k][idx];
+        if (slot < 0) {
+            slot = (int)str_src.size();
+            str_src.push_back({s * 4 + k, idx});
+        }
+        return slot;
+    }
+    int rows(int n) {
+        const int r = n_rows;
+        n_rows += n;
+        return r;
+    }
+
+    bool plan(std::string* why) {
+        dyn.assign(E, 0);
+        in_pair.assign(E, 0);
+        need_trig.assign(E, 0);
+        need_rot.assign(E, 0);
+        split.assign(P, 0);
+        split_idx.assign(P, -1);
+        for (int e = 0; e < E; ++e) dyn[e] = (ed[e].flags & (VMAS_F_MOVABLE | VMAS_F_ROTATABLE)) != 0;
+        for (const auto& q : pd) {
+            in_pair[q.ea] = in_pair[q.eb] = 1;
+            if (q.cls == VMAS_PAIR_JOINT) need_trig[q.ea] = need_trig[q.eb] = need_rot[q.ea] = need_rot[q.eb] = 1;
+        }
+        for (int e = 0; e < E; ++e) {
+            if (in_pair[e] && ed[e].shape != VMAS_SPHERE) need_trig[e] = 1;
+            if (need_trig[e]) need_rot[e] = 1;
+        }
+        for (int p = 0; p < P; ++p) {
+            split[p] = split_boxes && (pd[p].cls == VMAS_PAIR_BL || pd[p].cls == VMAS_PAIR_BB);
+            if (split[p]) split_idx[p] = n_split++;
+        }
+        items.assign(E, {});
+        for (int p = 0; p < P; ++p) {
+            for (int side = 0; side < 2; ++side) {
+                const int e = side ? pd[p].eb : pd[p].ea;
+                if (!dyn[e]) continue;
+                int tq = 1;  // spheres in SS/LS/BS receive no torque (core.py:2330-2338, 2383-2391, 2543-2551)
+                if (pd[p].cls == VMAS_PAIR_SS) tq = 0;
+                if ((pd[p].cls == VMAS_PAIR_LS || pd[p].cls == VMAS_PAIR_BS) && side == 1) tq = 0;
+                items[e].push_back({p, side, tq});
+            }
+        }
+        // pair tasks: longest-processing-time over the waves.  Contact-case costs in units of a
+        // sphere-sphere contact, measured per wave with tools/jit_phase_profile.py.
+        static const float kCost[7] = {1.5f, 1.0f, 2.0f, 1.8f, 2.2f, 7.4f, 30.f};
+        std::vector<Task> all, finishes;
+        for (int p = 0; p < P; ++p) {
+            if (split[p]) {
+                for (int k = 0; k < parts(pd[p].cls); ++k)
+                    all.push_back({p, k, pd[p].cls == VMAS_PAIR_BL ? 1.8f : 3.8f});
+                finishes.push_back({p, kFinish, 1.5f});
+            } else {
+                all.push_back({p, kWhole, kCost[pd[p].cls]});
+            }
+        }
+        std::stable_sort(all.begin(), all.end(), [](const Task& a, const Task& b) { return a.cost > b.cost; });
+        wave_tasks.assign(kNW, {});
+        std::vector<float> load(kNW, 0.f);
+        auto place = [&](const Task& t) {
+            const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            wave_tasks[w].push_back(t);
+            load[w] += t.cost;
+        };
+        for (const Task& t : all) place(t);
+        // parts first in their waves (a finish waits for them), finishes last: a wave waiting in
+        // a finish has run all of its parts
+        for (auto& v : wave_tasks)
+            std::stable_sort(v.begin(), v.end(), [](const Task& a, const Task& b) {
+                const bool pa = a.part >= 0, pb = b.part >= 0;
+                return pa != pb ? pa : a.pair < b.pair;
+            });
+        for (const Task& t : finishes) place(t);
+        // entity phase: dynamic entities over the waves by contribution count (LPT)
+        owner.assign(E, -1);
+        wave_ents.assign(kNW, {});
+        wave_static.assign(kNW, {});
+        {
+            std::vector<int> order;
+            for (int e = 0; e < E; ++e)
+                if (dyn[e]) order.push_back(e);
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return items[a].size() > items[b].size(); });
+            std::vector<float> eload(kNW, 0.f);
+            for (int e : order) {
+                const int w = (int)(std::min_element(eload.begin(), eload.end()) - eload.begin());
+                owner[e] = w;
+                wave_ents[w].push_back(e);
+                eload[w] += 4.f + items[e].size();
+            }
+            int rr = 0;
+            for (int e = 0; e < E; ++e)
+                if (!dyn[e] && in_pair[e]) {
+                    owner[e] = rr % kNW;
+                    wave_static[rr % kNW].push_back(e);
+                    ++rr;
+                }
+        }
+        // LDS rows: published entity state, then per pair 4 result rows (a split pair first holds
+        // its parts' (p1, p2) and the pre-integration centres)
+        r_p.assign(E, -1);
+        r_rot.assign(E, -1);
+        r_trig.assign(E, -1);
+        r_res.assign(P, -1);
+        for (int e = 0; e < E; ++e) {
+            if (!in_pair[e]) continue;
+            r_p[e] = rows(2);
+            if (need_rot[e]) r_rot[e] = rows(1);
+            if (need_trig[e]) r_trig[e] = rows(4);
+        }
+        for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : 4);
+        const long lds = (long)n_rows * 256 + (long)nfl * 4 + 4 * (n_split + 1);
+        if (lds > lds_budget) {
+            *why = "LDS budget exceeded (" + it(lds) + " B)";
+            return false;
+        }
+        // argument block slots
+        for (auto& v : ptr_of) v.assign(std::max(E, std::max(A, J)) + 1, -1);
+        for (auto& a : str_of)
+            for (auto& v : a) v.assign(std::max(E, std::max(A, J)) + 1, -1);
+        for (int e = 0; e < E; ++e) {
+            if (!(dyn[e] || in_pair[e])) continue;
+            ptr(S_POS, e), str(S_POS, 0, e), str(S_POS, 1, e);
+            if (need_rot[e] || dyn[e]) ptr(S_ROT, e), str(S_ROT, 0, e);
+            if (dyn[e]) {
+                ptr(S_VEL, e), str(S_VEL, 0, e), str(S_VEL, 1, e);
+                ptr(S_ANG, e), str(S_ANG, 0, e);
+                if (ed[e].flags & VMAS_F_GRAVITY) ptr(S_GRAV, e), str(S_GRAV, 0, e), str(S_GRAV, 1, e);
+                if (ed[e].agent_index >= 0) {
+                    const int a = ed[e].agent_index;
+                    ptr(S_FORCE, a), str(S_FORCE, 0, a), str(S_FORCE, 1, a);
+                    ptr(S_TORQUE, a), str(S_TORQUE, 0, a);
+                }
+            }
+        }
+        for (int p = 0; p < P; ++p)
+            if (pd[p].cls == VMAS_PAIR_JOINT) ptr(S_JFIX, pd[p].joint), str(S_JFIX, 0, pd[p].joint);
+        if (str_src.size() % 2) str_src.push_back({-1, 0});  // keep the int block 8-byte aligned
+        if (arg_bytes() > kMaxArgBytes) {
+            *why = "kernel argument block too large (" + it(arg_bytes()) + " B)";
+            return false;
+        }
+        return true;
+    }
+
+    size_t arg_bytes() const {  // layout of the generated struct Args
+        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 3) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+    }
+
+    // expressions for entity e as seen by wave w (registers when w owns it)
+    static std::string row(int r, int k = 0) { return "L[" + it((long)(r + k) * 64) + " + lane]"; }
+    bool mine(int e, int w) const { return dyn[e] && owner[e] == w; }
+    std::string pos(int e, int w) const {
+        if (mine(e, w)) return "p" + it(e);
+        return "mk(" + row(r_p[e]) + ", " + row(r_p[e], 1) + ")";
+    }
+    std::string rot(int e, int w) const {
+        if (mine(e, w)) return "r" + it(e);
+        return row(r_rot[e]);
+    }
+    std::string trig(int e, int w) const {
+        if (mine(e, w)) return "t" + it(e);
+        return "Trig{" + row(r_trig[e]) + ", " + row(r_trig[e], 1) + ", " + row(r_trig[e], 2) + ", " +
+               row(r_trig[e], 3) + "}";
+    }
+    std::string P_(Src s, int i) const { return "a.ptr[" + it(ptr_of[s][i]) + "]"; }
+    std::string S_(Src s, int k, int i) const { return "a.str[" + it(str_of[s][k][i]) + "]"; }
+    std::string ld2(Src s, int i) const {
+        return "ld2(" + P_(s, i) + ", " + S_(s, 0, i) + ", " + S_(s, 1, i) + ", bb)";
+    }
+    std::string ld1(Src s, int i) const { return P_(s, i) + "[(long)bb * " + S_(s, 0, i) + "]"; }
+    std::string mbit(int p) const { return "(m" + it(p >> 5) + " & " + it(1u << (p & 31)) + "u)"; }
+    // first of the 4 result rows (fa.x, fa.y, ta, tb) of pair p
+    int res(int p) const { return split[p] ? r_res[p] + 4 * parts(pd[p].cls) + 4 : r_res[p]; }
+
+    // timestamp slot: per substep s, k = 0 pair phase done, 1 after its barrier, 2 entity phase
+    // done, 3 after its barrier; prologue: slots max_substeps*4 + {0, 1}
+    std::string stamp(int w, const std::string& slot) const {
+        if (prof_block < 0) return "";
+        return "if (blockIdx.x == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kNW) + " + " +
+               it(w) + "] = __builtin_amdgcn_s_memtime();\n";
+    }
+
+    std::string desc(int e) const {
+        const VmasEntityDesc& d = ed[e];
+        return "{" + it(d.shape) + ", " + it(d.flags) + "u, " + it(d.agent_index) + ", " + it(d.out_lin) + ", " +
+               it(d.out_rot) + ", " + it(d.out_force) + ", " + it(d.out_torque) + ", " + fl(d.radius) + ", " +
+               fl(d.half_length) + ", " + fl(d.half_width) + ", " + fl(d.mass) + ", " + fl(d.inertia) + ", " +
+               fl(d.one_minus_drag) + ", " + fl(d.lin_fric) + ", " + fl(d.ang_fric) + ", " + fl(d.max_speed) + ", " +
+               fl(d.v_range) + ", " + fl(d.max_f) + ", " + fl(d.f_range) + ", " + fl(d.max_t) + ", " +
+               fl(d.t_range) + "}";
+    }
+
+    void publish(std::string& o, int e, const std::string& ind, bool with_pos, bool with_rot) const {
+        if (!in_pair[e]) return;
+        if (with_pos) o += ind + row(r_p[e]) + " = p" + it(e) + ".x; " + row(r_p[e], 1) + " = p" + it(e) + ".y;\n";
+        if (with_rot && r_rot[e] >= 0) o += ind + row(r_rot[e]) + " = r" + it(e) + ";\n";
+        if (with_rot && r_trig[e] >= 0)
+            o += ind + row(r_trig[e]) + " = t" + it(e) + ".c0; " + row(r_trig[e], 1) + " = t" + it(e) + ".s0; " +
+                 row(r_trig[e], 2) + " = t" + it(e) + ".c1; " + row(r_trig[e], 3) + " = t" + it(e) + ".s1;\n";
+    }
+
+    std::string pair_call(int p, int w) const {
+        const VmasPairDesc& q = pd[p];
+        const int a = q.ea, b = q.eb;
+        const VmasEntityDesc &da = ed[a], &db = ed[b];
+        const std::string ha = bl(da.flags & VMAS_F_HOLLOW), hb = bl(db.flags & VMAS_F_HOLLOW);
+        const std::string dm = fl(q.dmin);
+        switch (q.cls) {
+            case VMAS_PAIR_SS: return "pair_ss(" + pos(a, w) + ", " + pos(b, w) + ", " + dm + ", WK)";
+            case VMAS_PAIR_LS:
+                return "pair_ls(" + pos(a, w) + ", " + trig(a, w) + ", " + fl(da.half_length) + ", " + pos(b, w) +
+                       ", " + dm + ", WK)";
+            case VMAS_PAIR_LL:
+                return "pair_ll(" + pos(a, w) + ", " + trig(a, w) + ", " + fl(da.half_length) + ", " + pos(b, w) +
+                       ", " + trig(b, w) + ", " + fl(db.half_length) + ", " + dm + ", WK)";
+            case VMAS_PAIR_BS:
+                return "pair_bs(" + pos(a, w) + ", " + trig(a, w) + ", " + fl(da.half_length) + ", " +
+                       fl(da.half_width) + ", " + ha + ", " + pos(b, w) + ", " + dm + ", WK)";
+            case VMAS_PAIR_BL:
+                return "pair_bl(" + pos(a, w) + ", " + trig(a, w) + ", " + fl(da.half_length) + ", " +
+                       fl(da.half_width) + ", " + ha + ", " + pos(b, w) + ", " + trig(b, w) + ", " +
+                       fl(db.half_length) + ", " + dm + ", WK)";
+            case VMAS_PAIR_BB:
+                return "pair_bb(" + pos(a, w) + ", " + trig(a, w) + ", " + fl(da.half_length) + ", " +
+                       fl(da.half_width) + ", " + ha + ", " + pos(b, w) + ", " + trig(b, w) + ", " +
+                       fl(db.half_length) + ", " + fl(db.half_width) + ", " + hb + ", " + dm + ", WK)";
+            default: {
+                const VmasJointDesc& j = jd[q.joint];
+                return "pair_joint(" + pos(a, w) + ", " + rot(a, w) + ", " + trig(a, w) + ", " + pos(b, w) + ", " +
+                       rot(b, w) + ", " + trig(b, w) + ", mk(" + fl(j.delta_a_x) + ", " + fl(j.delta_a_y) + "), mk(" +
+                       fl(j.delta_b_x) + ", " + fl(j.delta_b_y) + "), " + fl(j.dist) + ", " + bl(j.rotate) +
+                       ", fixed_rot, WK)";
+            }
+        }
+    }
+
+    std::string flag_r(int p, const std::string& ind) const {  // R: some env within the broadphase radius
+        return ind + "if (a.blk) {\n" + ind + "    const unsigned long long bal = __ballot(inr && valid);\n" + ind +
+               "    if (lane == 0 && bal) atomicOr(&FL[s * " + it(W) + " + " + it(p >> 5) + "], " +
+               it(1u << (p & 31)) + "u);\n" + ind + "}\n";
+    }
+    std::string flag_z(int p, const std::string& ind) const {  // Z: an out-of-range env got a force
+        return ind + "if (a.blk) {\n" + ind +
+               "    const bool nz = valid && !inr && (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || o.tb != 0.f);\n" +
+               ind + "    const unsigned long long bal = __ballot(nz);\n" + ind +
+               "    if (lane == 0 && bal) atomicOr(&FL[(a.S + s) * " + it(W) + " + " + it(p >> 5) + "], " +
+               it(1u << (p & 31)) + "u);\n" + ind + "}\n";
+    }
+    std::string store_res(int p, const std::string& ind) const {
+        const int r = res(p);
+        return ind + row(r) + " = o.fa.x; " + row(r, 1) + " = o.fa.y; " + row(r, 2) + " = o.ta; " + row(r, 3) +
+               " = o.tb;\n";
+    }
+
+    void task_code(std::string& o, const Task& k, int w) const {
+        const int p = k.pair;
+        const VmasPairDesc& q = pd[p];
+        const std::string I = "            ";
+        o += "        {  // pair " + it(p) + " class " + it(q.cls) + " (" + it(q.ea) + ", " + it(q.eb) + ")" +
+             (k.part >= 0 ? " part " + it(k.part) : k.part == kFinish ? std::string(" finish") : std::string()) +
+             "\n";
+        if (k.part == kFinish) {  // wait for the parts, select, finish the contact, store the result
+            const int n = parts(q.cls), base = r_res[p], c = base + 4 * n;
+            o += I + "if " + mbit(p) + " {\n";
+            o += I + "    if (lane == 0) {\n" + I + "        while (atomicAdd(&DONE[" + it(split_idx[p]) + "], 0u) < " +
+                 it(n) + "u) __builtin_amdgcn_s_sleep(1);\n" + I + "    }\n";
+            o += I + "    __builtin_amdgcn_wave_barrier();\n" + I + "    __threadfence_block();\n";
+            o += I + "    const V2 ca = mk(" + row(c) + ", " + row(c, 1) + "), cb = mk(" + row(c, 2) + ", " + row(c, 3) +
+                 ");\n";
+            o += I + "    const Pts q = select_min(" + it(n) + ", [&](int i) { const float* x = L + " +
+                 it((long)base * 64) + " + i * 256 + lane; return Pts{mk(x[0], x[64]), mk(x[128], x[192])}; });\n";
+            if (q.cls == VMAS_PAIR_BL)
+                o += I + "    const PairOut o = bl_finish(ca, " + bl(ed[q.ea].flags & VMAS_F_HOLLOW) + ", cb, q, " +
+                     fl(q.dmin) + ", WK);\n";
+            else
+                o += I + "    const PairOut o = bb_finish(ca, " + bl(ed[q.ea].flags & VMAS_F_HOLLOW) + ", cb, " +
+                     bl(ed[q.eb].flags & VMAS_F_HOLLOW) + ", q, " + fl(q.dmin) + ", WK);\n";
+            o += I + "    const bool inr = norm(ca - cb) <= " + fl(q.bp_radius) + ";\n";
+            o += flag_z(p, I + "    ");
+            o += store_res(p, I + "    ");
+            o += I + "}\n        }\n";
+            return;
+        }
+        if (k.part == kWhole || k.part == 0) {
+            if (q.cls != VMAS_PAIR_JOINT)
+                o += I + "const bool inr = norm(" + pos(q.ea, w) + " - " + pos(q.eb, w) + ") <= " + fl(q.bp_radius) +
+                     ";\n";
+            else
+                o += I + "const bool inr = true;\n";
+            o += flag_r(p, I);
+        }
+        o += I + "if " + mbit(p) + " {\n";
+        if (k.part == kWhole) {
+            if (q.cls == VMAS_PAIR_JOINT) {
+                const int j = q.joint;
+                o += I + "    const float* frp = " + P_(S_JFIX, j) + ";\n";
+                o += I + "    const float fixed_rot = frp ? frp[(long)bb * " + S_(S_JFIX, 0, j) + "] : " +
+                     fl(jd[j].fixed_rotation) + ";\n";
+            }
+            o += I + "    const PairOut o = " + pair_call(p, w) + ";\n";
+            o += store_res(p, I + "    ");
+            if (q.cls != VMAS_PAIR_JOINT) o += flag_z(p, I + "    ");
+            o += I + "}\n        }\n";
+            return;
+        }
+        const VmasEntityDesc &da = ed[q.ea], &db = ed[q.eb];
+        if (q.cls == VMAS_PAIR_BL)
+            o += I + "    const Pts q = bl_part(" + pos(q.ea, w) + ", " + trig(q.ea, w) + ", " + fl(da.half_length) + ", " +
+                 fl(da.half_width) + ", " + pos(q.eb, w) + ", " + trig(q.eb, w) + ", " + fl(db.half_length) + ", " +
+                 it(k.part) + ");\n";
+        else
+            o += I + "    const Pts q = bb_part(" + pos(q.ea, w) + ", " + trig(q.ea, w) + ", " + fl(da.half_length) + ", " +
+                 fl(da.half_width) + ", " + pos(q.eb, w) + ", " + trig(q.eb, w) + ", " + fl(db.half_length) + ", " +
+                 fl(db.half_width) + ", " + it(k.part) + ");\n";
+        const int r = r_res[p] + 4 * k.part;
+        o += I + "    " + row(r) + " = q.p1.x; " + row(r, 1) + " = q.p1.y; " + row(r, 2) + " = q.p2.x; " + row(r, 3) +
+             " = q.p2.y;\n";
+        if (k.part == 0) {  // the finish needs the pre-integration centres
+            const int c = r_res[p] + 4 * parts(q.cls);
+            const std::string pa = pos(q.ea, w), pb = pos(q.eb, w);
+            o += I + "    { const V2 ca = " + pa + ", cb = " + pb + "; " + row(c) + " = ca.x; " + row(c, 1) + " = ca.y; " +
+                 row(c, 2) + " = cb.x; " + row(c, 3) + " = cb.y; }\n";
+        }
+        o += I + "}\n";
+        o += I + "__threadfence_block();\n" + I + "if (lane == 0) atomicAdd(&DONE[" + it(split_idx[p]) + "], 1u);\n";
+        o += "        }\n";
+    }
+
+    void wave_body(std::string& o, int w) {
+        o += "template <> __device__ __forceinline__ void run<" + it(w) +
+             ">(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, int lane, int b, int bb, bool valid) {\n";
+        // prologue: static pair entities (loaded once), dynamic entities into registers
+        for (int e : wave_static[w]) {
+            o += "    {  // static entity " + it(e) + "\n";
+            o += "        const V2 p" + it(e) + " = " + ld2(S_POS, e) + ";\n";
+            if (need_rot[e]) o += "        const float r" + it(e) + " = " + ld1(S_ROT, e) + ";\n";
+            if (need_trig[e])
+                o += "        const Trig t" + it(e) + " = make_trig_for(r" + it(e) + ", " + bl(ed[e].shape == VMAS_BOX) +
+                     ");\n";
+            publish(o, e, "        ", true, true);
+            o += "    }\n";
+        }
+        for (int e : wave_ents[w]) {
+            const VmasEntityDesc& d = ed[e];
+            const std::string s = it(e);
+            o += "    V2 p" + s + " = " + ld2(S_POS, e) + ", v" + s + " = " + ld2(S_VEL, e) + ";\n";
+            o += "    float r" + s + " = " + ld1(S_ROT, e) + ", w" + s + " = " + ld1(S_ANG, e) + ";\n";
+            if (d.agent_index >= 0)
+                o += "    V2 af" + s + " = " + ld2(S_FORCE, d.agent_index) + "; float at" + s + " = " +
+                     ld1(S_TORQUE, d.agent_index) + ";\n";
+            else
+                o += "    V2 af" + s + " = mk(0.f, 0.f); float at" + s + " = 0.f;\n";
+            if (d.flags & VMAS_F_GRAVITY) o += "    const V2 eg" + s + " = " + ld2(S_GRAV, e) + ";\n";
+            else o += "    const V2 eg" + s + " = mk(0.f, 0.f);\n";
+            if (need_trig[e])
+                o += "    Trig t" + s + " = make_trig_for(r" + s + ", " + bl(d.shape == VMAS_BOX) + ");\n";
+            publish(o, e, "    ", true, true);
+        }
+        const std::string pro = it((long)cfg.max_substeps * 4);
+        o += "    " + stamp(w, pro);
+        o += "    __syncthreads();\n";
+        o += "    " + stamp(w, pro + " + 1");
+        o += "    for (int s = 0; s < a.S; ++s) {\n";
+        std::vector<char> word(W, 0);  // mask words this wave reads
+        for (const Task& t : wave_tasks[w]) word[t.pair >> 5] = 1;
+        for (int e : wave_ents[w])
+            for (const Item& x : items[e]) word[x.pair >> 5] = 1;
+        for (int k = 0; k < W; ++k)
+            if (word[k]) o += "        const uint32_t m" + it(k) + " = a.mask[s * " + it(W) + " + " + it(k) + "];\n";
+        for (const Task& t : wave_tasks[w]) task_code(o, t, w);
+        o += "        " + stamp(w, "s * 4");
+        o += "        __syncthreads();\n";
+        o += "        " + stamp(w, "s * 4 + 1");
+        if (w == 0 && n_split)  // no part signals before the next pair phase
+            o += "        for (int i = lane; i < " + it(n_split) + "; i += 64) DONE[i] = 0u;\n";
+        // entity phase
+        for (int e : wave_ents[w]) {
+            const VmasEntityDesc& d = ed[e];
+            const std::string s = it(e);
+            const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+            o += "        {  // entity " + s + "\n";
+            o += "            float fx, fy, tq;\n";
+            o += "            pre_forces(D" + s + ", " + bl(d.agent_index >= 0) + ", af" + s + ", at" + s + ", v" + s +
+                 ", w" + s + ", eg" + s + ", " + bl(d.flags & VMAS_F_GRAVITY) + ", GX, GY, HAS_G, a.sdt, fx, fy, tq);\n";
+            for (const Item& x : items[e]) {
+                const int r = res(x.pair);
+                std::string body;
+                if (mov)
+                    body += x.side ? "fx = fx + -" + row(r) + "; fy = fy + -" + row(r, 1) + "; "
+                                   : "fx = fx + " + row(r) + "; fy = fy + " + row(r, 1) + "; ";
+                if (rotb && x.torque) body += "tq = tq + " + row(r, x.side ? 3 : 2) + "; ";
+                if (!body.empty()) o += "            if " + mbit(x.pair) + " { " + body + "}\n";
+            }
+            o += "            integrate(D" + s + ", s, a.sdt, fx, fy, tq, HAS_XS, XS, HAS_YS, YS, p" + s + ", v" + s +
+                 ", r" + s + ", w" + s + ");\n";
+            if (need_trig[e] && rotb)
+                o += "            t" + s + " = make_trig_for(r" + s + ", " + bl(d.shape == VMAS_BOX) + ");\n";
+            publish(o, e, "            ", mov, rotb);
+            o += "        }\n";
+        }
+        o += "        " + stamp(w, "s * 4 + 2");
+        o += "        __syncthreads();\n";
+        o += "        " + stamp(w, "s * 4 + 3");
+        o += "    }\n";
+        // epilogue: the integrated fields into the fresh output tensors
+        if (!wave_ents[w].empty()) {
+            o += "    if (valid) {\n";
+            for (int e : wave_ents[w]) {
+                const VmasEntityDesc& d = ed[e];
+                const std::string s = it(e);
+                if (d.out_lin >= 0)
+                    o += "        reinterpret_cast<float2*>(a.out[0])[(size_t)" + it(d.out_lin) + " * a.B + b] = make_float2(p" +
+                         s + ".x, p" + s + ".y);\n        reinterpret_cast<float2*>(a.out[1])[(size_t)" + it(d.out_lin) +
+                         " * a.B + b] = make_float2(v" + s + ".x, v" + s + ".y);\n";
+                if (d.out_rot >= 0)
+                    o += "        a.out[2][(size_t)" + it(d.out_rot) + " * a.B + b] = r" + s + ";\n        a.out[3][(size_t)" +
+                         it(d.out_rot) + " * a.B + b] = w" + s + ";\n";
+                if (d.agent_index >= 0) {
+                    if (d.out_force >= 0)
+                        o += "        reinterpret_cast<float2*>(a.out[4])[(size_t)" + it(d.out_force) +
+                             " * a.B + b] = make_float2(af" + s + ".x, af" + s + ".y);\n";
+                    if (d.out_torque >= 0)
+                        o += "        a.out[5][(size_t)" + it(d.out_torque) + " * a.B + b] = at" + s + ";\n";
+                }
+            }
+            o += "    }\n";
+        }
+        o += "}\n\n";
+    }
+
+    void generate() {
+        std::string& o = src;
+        o += "// generated by vmas_jit.hip for one world\n#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
+        o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
+             "];\n    float* out[6];\n    const uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
+             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int pad;\n};\n\n";
+        o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
+             "    if (s0 == 2 && s1 == 1) {\n"
+             "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
+             "        return mk(v.x, v.y);\n    }\n"
+             "    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);\n}\n\n";
+        o += "constexpr WorldK WK{" + fl(cfg.contact_margin) + ", " + fl(cfg.collision_force) + ", " +
+             fl(cfg.joint_force) + ", " + fl(cfg.torque_constraint_force) + "};\n";
+        o += "constexpr float GX = " + fl(cfg.gravity_x) + ", GY = " + fl(cfg.gravity_y) + ";\n";
+        o += "constexpr bool HAS_G = " + bl(cfg.has_world_gravity) + ";\n";
+        o += "constexpr float XS = " + fl(cfg.x_semidim) + ", YS = " + fl(cfg.y_semidim) + ";\n";
+        o += "constexpr bool HAS_XS = " + bl(cfg.has_x_semidim) + ", HAS_YS = " + bl(cfg.has_y_semidim) + ";\n";
+        for (int e = 0; e < E; ++e)
+            if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + desc(e) + ";\n";
+        o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
+             "uint32_t* DONE, int lane, int b, int bb, bool valid);\n\n";
+        for (int w = 0; w < kNW; ++w) wave_body(o, w);
+        // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
+        const int waves_per_eu = lds_budget <= kLdsTwoPerCu ? 4 : 2;
+        o += "extern \"C\" __global__ void __launch_bounds__(" + it(kNW * 64) + ", " + it(waves_per_eu) +
+             ") k_world(Args a) {\n";
+        o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
+        o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
+        o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
+        o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n"
+             "    const int b = blockIdx.x * 64 + lane;\n"
+             "    const bool valid = b < a.B;\n"
+             "    const int bb = valid ? b : (a.B - 1);\n";
+        o += "    const int nfl = 2 * a.S * " + it(W) + ";\n"
+             "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+             "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
+        o += "    switch (wave) {\n";
+        for (int w = 0; w < kNW; ++w)
+            o += "        case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, lane, b, bb, valid); break;\n";
+        o += "        default: break;\n    }\n";
+        o += "    if (a.blk) {\n        __syncthreads();\n        uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
+             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) dst[i] = FL[i];\n    }\n}\n";
+    }
+};
+
+// Plan a world: box pairs split with two workgroups per CU, else unsplit, else unsplit with the
+// whole LDS (one workgroup per CU).  VMAS_JIT_SPLIT=0 disables splitting.
+std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<VmasEntityDesc>& ed,
+                               const std::vector<VmasPairDesc>& pd, const std::vector<VmasJointDesc>& jd,
+                               std::string* why) {
+    const char* sp = getenv("VMAS_JIT_SPLIT");
+    const bool allow_split = !(sp && sp[0] == '0');
+    const struct {
+        bool split;
+        long budget;
+    } tries[] = {{true, kLdsTwoPerCu}, {false, kLdsTwoPerCu}, {false, kLdsOnePerCu}};
+    for (const auto& t : tries) {
+        if (t.split && !allow_split) continue;
+        std::unique_ptr<Gen> g(new Gen(cfg, ed, pd, jd));
+        if ((size_t)cfg.max_substeps * g->W > 1024) {
+            *why = "too many substeps x pairs";
+            return nullptr;
+        }
+        g->split_boxes = t.split;
+        g->lds_budget = t.budget;
+        why->clear();
+        if (g->plan(why)) return g;
+    }
+    return nullptr;
+}
+
+// OR the per-block activity words, decide whether the mask was a fixed point, update it if not
+// (same scheme as vmas_world_step's reduction).  blk: [nblk][2][S][W]; one workgroup.
+__global__ void __launch_bounds__(1024) k_jit_flags_reduce(const uint32_t* blk, int nblk, int S, int W,
+                                                           uint32_t* mask, uint32_t* viol_out) {
+    __shared__ uint32_t R[1024], Z[1024];
+    __shared__ uint32_t viol;
+    const int nwords = S * W;
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        R[w] = 0u;
+        Z[w] = 0u;
+    }
+    if (threadIdx.x == 0) viol = 0u;
+    __syncthreads();
+    const int groups = max(1, (int)blockDim.x / nwords);
+    if ((int)threadIdx.x < groups * nwords) {
+        const int w = threadIdx.x % nwords, g0 = threadIdx.x / nwords;
+        uint32_t r = 0u, z = 0u;
+        for (int i = g0; i < nblk; i += groups) {
+            r |= blk[(size_t)i * 2 * nwords + w];
+            z |= blk[(size_t)i * 2 * nwords + nwords + w];
+        }
+        if (r) atomicOr(&R[w], r);
+        if (z) atomicOr(&Z[w], z);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        const uint32_t m = mask[w];
+        if ((m & ~R[w] & Z[w]) | (~m & R[w])) atomicOr(&viol, 1u);
+    }
+    __syncthreads();
+    if (viol)
+        for (int w = threadIdx.x; w < nwords; w += blockDim.x) mask[w] = R[w];
+    if (threadIdx.x == 0) *viol_out = viol;
+}
+
+// hipRTC compile with an in-process cache (identical worlds share one code object)
+std::mutex g_cache_mu;
+std::unordered_map<std::string, std::vector<char>> g_code_cache;
+
+std::string module_dir() {
+    Dl_info info{};
+    if (dladdr((const void*)&jfail, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        const size_t k = p.rfind('/');
+        return k == std::string::npos ? std::string(".") : p.substr(0, k);
+    }
+    return ".";
+}
+
+int32_t compile(const std::string& src, std::vector<char>* code) {
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto f = g_code_cache.find(src);
+        if (f != g_code_cache.end()) {
+            *code = f->second;
+            return VMAS_OK;
+        }
+    }
+    const std::string dir = module_dir();
+    const std::string inc1 = "-I" + dir + "/csrc", inc2 = "-I" + dir + "/../include";
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                          inc1.c_str(), inc2.c_str()};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "vmas_world.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        return jfail(VMAS_E_HIP, "hiprtcCreateProgram failed");
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        return jfail(VMAS_E_HIP, "hipRTC compile failed: %.900s", log.c_str());
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code->resize(n);
+    hiprtcGetCode(prog, code->data());
+    hiprtcDestroyProgram(&prog);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_code_cache[src] = *code;
+    return VMAS_OK;
+}
+
+}  // namespace
+
+struct VmasJitWorld {
+    VmasWorldConfig cfg{};
+    std::vector<VmasEntityDesc> ed;
+    std::vector<VmasPairDesc> pd;
+    std::vector<VmasJointDesc> jd;
+    std::string src;
+    std::vector<std::pair<int, int>> ptr_src, str_src;
+    size_t arg_bytes = 0;
+    int W = 1, nblk = 0;
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
+    unsigned long long* d_prof = nullptr;  // phase timestamps of one workgroup (VMAS_JIT_PROFILE)
+    size_t n_prof = 0;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
+    double timed_ms = 0.0;
+    long timed_launches = 0;
+};
+
+extern "C" {
+
+const char* vmas_jit_last_error(void) { return g_jit_err.c_str(); }
+
+int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
+    if (!W) return VMAS_OK;
+    if (W->cfg.device >= 0) {
+        (void)hipSetDevice(W->cfg.device);
+        if (W->mod) (void)hipModuleUnload(W->mod);
+        if (W->d_mask) (void)hipFree(W->d_mask);
+        if (W->d_blk) (void)hipFree(W->d_blk);
+        if (W->d_viol) (void)hipFree(W->d_viol);
+        if (W->h_viol) (void)hipHostFree(W->h_viol);
+        if (W->d_prof) (void)hipFree(W->d_prof);
+        for (auto& ev : W->ev_pending) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+        for (auto& ev : W->ev_free) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+    }
+    delete W;
+    return VMAS_OK;
+}
+
+int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities, const VmasPairDesc* pairs,
+                              const VmasJointDesc* joints, VmasJitWorld** out_world) {
+    if (!cfg || !out_world) return jfail(VMAS_E_INVALID, "null argument");
+    if (cfg->device < 0) return jfail(VMAS_E_INVALID, "the specialised step is a GPU path (device >= 0)");
+    if (cfg->batch <= 0 || cfg->n_entities <= 0 || cfg->n_pairs < 0 || cfg->max_substeps <= 0)
+        return jfail(VMAS_E_INVALID, "bad world config");
+    auto* W = new VmasJitWorld();
+    W->cfg = *cfg;
+    W->ed.assign(entities, entities + cfg->n_entities);
+    W->pd.assign(pairs, pairs + cfg->n_pairs);
+    if (cfg->n_joints) W->jd.assign(joints, joints + cfg->n_joints);
+    for (const auto& q : W->pd)
+        if (q.ea < 0 || q.ea >= cfg->n_entities || q.eb < 0 || q.eb >= cfg->n_entities || q.cls < 0 || q.cls > 6 ||
+            (q.cls == VMAS_PAIR_JOINT && (q.joint < 0 || q.joint >= cfg->n_joints))) {
+            delete W;
+            return jfail(VMAS_E_INVALID, "bad pair table");
+        }
+    std::string why;
+    std::unique_ptr<Gen> gp = make_plan(W->cfg, W->ed, W->pd, W->jd, &why);
+    if (!gp) {
+        delete W;
+        return jfail(VMAS_E_INVALID, "world not specialised: %s", why.c_str());
+    }
+    Gen& g = *gp;
+    if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
+    g.generate();
+    W->src = g.src;
+    W->ptr_src = g.ptr_src;
+    W->str_src = g.str_src;
+    W->arg_bytes = g.arg_bytes();
+    W->W = g.W;
+    W->nblk = (cfg->batch + 63) / 64;
+    auto cleanup = [&](int32_t rc) {
+        vmas_jit_world_destroy(W);
+        return rc;
+    };
+    std::vector<char> code;
+    if (int32_t rc = compile(W->src, &code)) return cleanup(rc);
+    JHIP(hipSetDevice(cfg->device));
+    if (hipModuleLoadData(&W->mod, code.data()) != hipSuccess) return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
+    if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
+        return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
+    const size_t nwords = (size_t)cfg->max_substeps * W->W;
+    if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
+        hipMalloc((void**)&W->d_blk, (size_t)W->nblk * 2 * nwords * 4) != hipSuccess ||
+        hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
+        hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
+        return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
+    if (g.prof_block >= 0) {
+        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kNW;
+        if (hipMalloc((void**)&W->d_prof, W->n_prof * 8) != hipSuccess ||
+            hipMemset(W->d_prof, 0, W->n_prof * 8) != hipSuccess)
+            return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc profile buffer"));
+    }
+    *out_world = W;
+    return VMAS_OK;
+}
+
+// Phase timestamps of the profiled workgroup from the last launch (VMAS_JIT_PROFILE=<block> at
+// create): [max_substeps*4 + 2][NW] s_memtime values (see Gen::stamp); returns the count.
+int32_t vmas_jit_world_profile(VmasJitWorld* W, uint64_t* out, int64_t cap) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    if (!W->d_prof) return 0;
+    JHIP(hipSetDevice(W->cfg.device));
+    JHIP(hipDeviceSynchronize());
+    const size_t n = std::min<size_t>(W->n_prof, cap > 0 ? (size_t)cap : 0);
+    if (out && n) JHIP(hipMemcpy(out, W->d_prof, n * 8, hipMemcpyDeviceToHost));
+    return (int32_t)W->n_prof;
+}
+
+// Generate and compile (hipRTC, gfx950) the specialised kernel of a world without a device:
+// returns the source length (copied into buf when given) or a negative VMAS_E_* code.
+int32_t vmas_jit_compile_check(const VmasWorldConfig* cfg, const VmasEntityDesc* entities, const VmasPairDesc* pairs,
+                               const VmasJointDesc* joints, char* buf, int64_t cap) {
+    if (!cfg || cfg->n_entities <= 0 || cfg->max_substeps <= 0) return jfail(VMAS_E_INVALID, "bad world config");
+    std::vector<VmasEntityDesc> ed(entities, entities + cfg->n_entities);
+    std::vector<VmasPairDesc> pd(pairs, pairs + cfg->n_pairs);
+    std::vector<VmasJointDesc> jd;
+    if (cfg->n_joints) jd.assign(joints, joints + cfg->n_joints);
+    std::string why;
+    std::unique_ptr<Gen> gp = make_plan(*cfg, ed, pd, jd, &why);
+    if (!gp) return jfail(VMAS_E_INVALID, "world not specialised: %s", why.c_str());
+    Gen& g = *gp;
+    g.generate();
+    std::vector<char> code;
+    if (int32_t rc = compile(g.src, &code)) return rc;
+    if (buf && cap > 0) {
+        const size_t k = std::min<size_t>(g.src.size(), (size_t)cap - 1);
+        memcpy(buf, g.src.data(), k);
+        buf[k] = '\0';
+    }
+    return (int32_t)g.src.size();
+}
+
+int32_t vmas_jit_world_source(const VmasJitWorld* W, char* buf, int64_t cap) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    const int64_t n = (int64_t)W->src.size();
+    if (buf && cap > 0) {
+        const int64_t k = std::min(n, cap - 1);
+        memcpy(buf, W->src.data(), (size_t)k);
+        buf[k] = '\0';
+    }
+    return (int32_t)std::min<int64_t>(n, INT32_MAX);
+}
+
+int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_, int32_t* iterations) {
+    if (!W || !io) return jfail(VMAS_E_INVALID, "null argument");
+    const VmasWorldConfig& cfg = W->cfg;
+    if (io->substeps <= 0 || io->substeps > cfg.max_substeps)
+        return jfail(VMAS_E_INVALID, "substeps %d outside [1, %d]", io->substeps, cfg.max_substeps);
+    int cur = -1;
+    JHIP(hipGetDevice(&cur));
+    if (cur != cfg.device) JHIP(hipSetDevice(cfg.device));
+    hipStream_t stream = (hipStream_t)stream_;
+    // kernel argument block (layout of the generated `struct Args`)
+    std::vector<char> buf(W->arg_bytes, 0);
+    char* p = buf.data();
+    auto put_ptr = [&](const void* v) {
+        memcpy(p, &v, 8);
+        p += 8;
+    };
+    auto put_i32 = [&](int32_t v) {
+        memcpy(p, &v, 4);
+        p += 4;
+    };
+    for (const auto& s : W->ptr_src) {
+        const int i = s.second;
+        const VmasEntityIO* e = io->entities + (s.first <= S_GRAV ? i : 0);
+        switch (s.first) {
+            case S_POS: put_ptr(e->pos); break;
+            case S_VEL: put_ptr(e->vel); break;
+            case S_ROT: put_ptr(e->rot); break;
+            case S_ANG: put_ptr(e->ang_vel); break;
+            case S_GRAV: put_ptr(e->gravity); break;
+            case S_FORCE: put_ptr(io->agents[i].force); break;
+            case S_TORQUE: put_ptr(io->agents[i].torque); break;
+            default: put_ptr(io->joints ? io->joints[i].fixed_rotation : nullptr); break;
+        }
+    }
+    if (W->ptr_src.empty()) put_ptr(nullptr);
+    put_ptr(io->out_pos);
+    put_ptr(io->out_vel);
+    put_ptr(io->out_rot);
+    put_ptr(io->out_ang_vel);
+    put_ptr(io->out_force);
+    put_ptr(io->out_torque);
+    put_ptr(W->d_mask);
+    const bool batch_bp = io->broadphase == VMAS_BROADPHASE_BATCH;
+    put_ptr(batch_bp ? W->d_blk : nullptr);
+    put_ptr(W->d_prof);
+    for (const auto& s : W->str_src) {
+        const int kind = s.first / 4, k = s.first % 4, i = s.second;
+        int32_t v = 0;
+        if (s.first >= 0) {
+            const VmasEntityIO* e = io->entities + (kind <= S_GRAV ? i : 0);
+            switch (kind) {
+                case S_POS: v = k ? e->pos_s1 : e->pos_s0; break;
+                case S_VEL: v = k ? e->vel_s1 : e->vel_s0; break;
+                case S_ROT: v = e->rot_s0; break;
+                case S_ANG: v = e->ang_s0; break;
+                case S_GRAV: v = k ? e->grav_s1 : e->grav_s0; break;
+                case S_FORCE: v = k ? io->agents[i].force_s1 : io->agents[i].force_s0; break;
+                case S_TORQUE: v = io->agents[i].torque_s0; break;
+                default: v = io->joints ? io->joints[i].s0 : 0; break;
+            }
+        }
+        put_i32(v);
+    }
+    if (W->str_src.empty()) {
+        put_i32(0);
+        put_i32(0);
+    }
+    put_i32(cfg.batch);
+    put_i32(io->substeps);
+    memcpy(p, &io->sub_dt, 4);
+    p += 4;
+    put_i32(0);
+    size_t size = (size_t)(p - buf.data());
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                     HIP_LAUNCH_PARAM_END};
+
+    const size_t nwords = (size_t)io->substeps * W->W;
+    JHIP(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
+    const int max_it = batch_bp ? io->substeps + 2 : 1;
+    for (int it = 0; it < max_it; ++it) {
+        std::pair<hipEvent_t, hipEvent_t> ev{};
+        if (W->timing) {
+            if (W->ev_free.empty()) {
+                JHIP(hipEventCreate(&ev.first));
+                JHIP(hipEventCreate(&ev.second));
+            } else {
+                ev = W->ev_free.back();
+                W->ev_free.pop_back();
+            }
+            JHIP(hipEventRecord(ev.first, stream));
+        }
+        JHIP(hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, kNW * 64, 1, 1, 0, stream, nullptr, extra));
+        if (W->timing) {
+            JHIP(hipEventRecord(ev.second, stream));
+            W->ev_pending.push_back(ev);
+        }
+        if (iterations) *iterations = it + 1;
+        if (!batch_bp) return VMAS_OK;
+        hipLaunchKernelGGL(k_jit_flags_reduce, dim3(1), dim3(1024), 0, stream, (const uint32_t*)W->d_blk, W->nblk,
+                           io->substeps, W->W, W->d_mask, W->d_viol);
+        JHIP(hipGetLastError());
+        JHIP(hipMemcpyAsync(W->h_viol, W->d_viol, 4, hipMemcpyDeviceToHost, stream));
+        JHIP(hipStreamSynchronize(stream));
+        if (*W->h_viol == 0u) return VMAS_OK;
+    }
+    return jfail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
+}
+
+int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    W->timing = enable != 0;
+    return VMAS_OK;
+}
+
+int32_t vmas_jit_world_get_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    JHIP(hipSetDevice(W->cfg.device));
+    for (auto& ev : W->ev_pending) {
+        float ms = 0.f;
+        JHIP(hipEventSynchronize(ev.second));
+        JHIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+        W->timed_ms += ms;
+        W->timed_launches += 1;
+        W->ev_free.push_back(ev);
+    }
+    W->ev_pending.clear();
+    if (total_ms) *total_ms = W->timed_ms;
+    if (launches) *launches = W->timed_launches;
+    if (reset) {
+        W->timed_ms = 0.0;
+        W->timed_launches = 0;
+    }
+    return VMAS_OK;
+}
+
+}  // extern "C"

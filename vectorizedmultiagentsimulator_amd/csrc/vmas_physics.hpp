@@ -8,9 +8,23 @@
 // Citations are file:line in the reference checkout.
 #pragma once
 
+// Under hipRTC (the world-specialised step kernels of csrc/vmas_jit.hip) the HIP runtime, device
+// math and fixed-width integer types are provided by the runtime compiler itself.
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#else
+typedef __hip_internal::int8_t int8_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+#ifndef INFINITY
+#define INFINITY __builtin_huge_valf()
+#endif
+#endif
 
 #include "../../include/vmas_mi355x.h"
 

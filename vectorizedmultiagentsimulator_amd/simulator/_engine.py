@@ -14,6 +14,7 @@ host backend of the same library (same arithmetic).  There is no PyTorch fallbac
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Callable, List
 
 import numpy as np
@@ -57,6 +58,9 @@ class PhysicsEngine:
         self.lib = N.load_library()
         self._sig = None
         self._handle = None
+        self._jit = None
+        self.jit_error = None
+        self.kernel_name = "k_step"
         self._dev_index = -1
         self.last_iterations = 0
         self.steps = 0
@@ -65,6 +69,8 @@ class PhysicsEngine:
         try:
             if self._handle is not None:
                 self.lib.vmas_world_destroy(self._handle)
+            if self._jit is not None:
+                self.lib.vmas_jit_world_destroy(self._jit)
         except Exception:
             pass
 
@@ -304,6 +310,21 @@ class PhysicsEngine:
         if self._handle is not None:
             self.lib.vmas_world_destroy(self._handle)
         self._handle = handle
+        # GPU worlds: the world-specialised kernel (csrc/vmas_jit.hip) when it applies, with the
+        # generic k_step as the fallback (both native; VMAS_JIT=0 forces the generic kernel)
+        if self._jit is not None:
+            self.lib.vmas_jit_world_destroy(self._jit)
+            self._jit = None
+        self.jit_error = None
+        if self._dev_index >= 0 and os.environ.get("VMAS_JIT", "1") != "0":
+            jh = ctypes.c_void_p()
+            rc = self.lib.vmas_jit_world_create(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(jh))
+            if rc == 0:
+                self._jit = jh
+            else:
+                self.jit_error = self.lib.vmas_jit_last_error().decode(errors="replace")
+        self.kernel_name = "k_world" if self._jit is not None else "k_step"
+        self._tables = (ed, pd, jd)
         self._cfg = cfg
         self._max_substeps = max_substeps
         self.entities = ents
@@ -327,14 +348,58 @@ class PhysicsEngine:
     def set_timing(self, enable: bool) -> None:
         self._ensure()
         self._timing = bool(enable)
-        N.check(self.lib.vmas_world_set_timing(self._handle, int(enable)), "vmas_world_set_timing")
+        self._apply_timing()
+
+    def _apply_timing(self):
+        on = int(getattr(self, "_timing", False))
+        N.check(self.lib.vmas_world_set_timing(self._handle, on), "vmas_world_set_timing")
+        if self._jit is not None:
+            N.check_jit(self.lib.vmas_jit_world_set_timing(self._jit, on), "vmas_jit_world_set_timing")
 
     def get_timing(self, reset: bool = True):
+        """(milliseconds, launches) of the step kernel (k_world or k_step) since the last reset."""
         ms = ctypes.c_double(0.0)
         n = ctypes.c_int64(0)
-        N.check(self.lib.vmas_world_get_timing(self._handle, int(reset), ctypes.byref(ms), ctypes.byref(n)),
-                "vmas_world_get_timing")
+        if self._jit is not None:
+            N.check_jit(self.lib.vmas_jit_world_get_timing(self._jit, int(reset), ctypes.byref(ms), ctypes.byref(n)),
+                        "vmas_jit_world_get_timing")
+        else:
+            N.check(self.lib.vmas_world_get_timing(self._handle, int(reset), ctypes.byref(ms), ctypes.byref(n)),
+                    "vmas_world_get_timing")
         return ms.value, n.value
+
+    def jit_source(self) -> str:
+        """Generated source of the world-specialised kernel ('' when the generic kernel runs)."""
+        self._ensure()
+        if self._jit is None:
+            return ""
+        n = self.lib.vmas_jit_world_source(self._jit, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        self.lib.vmas_jit_world_source(self._jit, buf, n + 1)
+        return buf.value.decode()
+
+    def jit_profile(self):
+        """Phase timestamps [max_substeps*4 + 2, 8] of the profiled workgroup (VMAS_JIT_PROFILE)."""
+        if self._jit is None:
+            return None
+        n = self.lib.vmas_jit_world_profile(self._jit, None, 0)
+        N.check_jit(n, "vmas_jit_world_profile")
+        if n == 0:
+            return None
+        out = np.zeros(n, dtype=np.uint64)
+        N.check_jit(self.lib.vmas_jit_world_profile(self._jit, out.ctypes.data, n), "vmas_jit_world_profile")
+        return out.reshape(-1, 8)
+
+    def jit_compile_check(self) -> str:
+        """Generate and hipRTC-compile this world's specialised kernel without a device (build
+        check on CPU machines); returns the generated source, raises on failure."""
+        self._ensure()
+        ed, pd, jd = self._tables
+        n = self.lib.vmas_jit_compile_check(ctypes.byref(self._cfg), ed, pd, jd, None, 0)
+        N.check_jit(n, "vmas_jit_compile_check")
+        buf = ctypes.create_string_buffer(n + 1)
+        self.lib.vmas_jit_compile_check(ctypes.byref(self._cfg), ed, pd, jd, buf, n + 1)
+        return buf.value.decode()
 
     def _ensure(self):
         sub = int(self.world._substeps)
@@ -342,7 +407,7 @@ class PhysicsEngine:
         if sig != self._sig or self._handle is None or sub > self._max_substeps:
             self._build(sig, max(sub, 16))
             if getattr(self, "_timing", False):
-                N.check(self.lib.vmas_world_set_timing(self._handle, 1), "vmas_world_set_timing")
+                self._apply_timing()
 
     # ---- the step ---------------------------------------------------------------------------------
     def _fill_entity_row(self, i, e, dev, B):
@@ -425,8 +490,12 @@ class PhysicsEngine:
         io.sub_dt = _f32(w._dt / w._substeps)
         io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
         iters = ctypes.c_int32(0)
-        N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
-                                         ctypes.byref(iters)), "vmas_world_step")
+        if self._jit is not None:
+            N.check_jit(self.lib.vmas_jit_world_step(self._jit, ctypes.byref(io), self._stream(dev),
+                                                     ctypes.byref(iters)), "vmas_jit_world_step")
+        else:
+            N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
+                                             ctypes.byref(iters)), "vmas_world_step")
         self.last_iterations = iters.value
         self.steps += 1
         del keep
