@@ -71,19 +71,25 @@ def alg_bytes_per_env_step(world) -> int:
     return 24 * len(ents) + 24 * e_dyn + 12 * n_agents
 
 
-def load_traffic(workload: str, kernel: str):
-    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC summary (profiles/), if it
-    was measured on this workload and this kernel."""
+def load_pmc(workload: str, kernel: str) -> dict:
+    """Per-launch PMC record of the step kernel (profiles/pmc_traffic.json, written by
+    tools/pmc_traffic.py), if it was measured on this workload and this kernel."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return {}
     try:
         d = json.loads(f.read_text())
         if d.get("workload") == workload and d.get("kernel") == kernel:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except Exception:
-        return None
-    return None
+        return {}
+    return {}
+
+
+# VALU issue peak of the MI355X (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU
+# instruction per 2 cycles per SIMD, 2.4 GHz -> 1.23e12 wave-instructions/s (= the 157.3 TF/s
+# fp32 vector peak / 128 flop per wave-FMA)
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
 
 
 def cpu_baseline(args):
@@ -176,7 +182,8 @@ def main():
     if on_gpu and launches:
         per_launch_ms = kernel_ms / launches
         achieved = b_env * args.envs / (per_launch_ms * 1e-3) / 1e9
-        traffic = load_traffic(workload, world.engine.kernel_name)
+        pmc = load_pmc(workload, world.engine.kernel_name)
+        traffic = pmc.get("hbm_bytes_per_launch")
         roofline = {
             "bound": "hbm",
             "achieved": round(achieved, 2),
@@ -189,6 +196,16 @@ def main():
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,
         }
+        if pmc.get("valu_insts_per_launch"):
+            # the bound the kernel actually meets: VALU issue, from PMC SQ_INSTS_VALU
+            rate = pmc["valu_insts_per_launch"] / (per_launch_ms * 1e-3)
+            roofline["valu_issue"] = {
+                "achieved": round(rate / 1e9, 1),
+                "peak": round(VALU_PEAK_WAVE_INSTS / 1e9, 1),
+                "unit": "G wave-instructions/s",
+                "frac": round(rate / VALU_PEAK_WAVE_INSTS, 4),
+                "valu_insts_per_launch": round(pmc["valu_insts_per_launch"]),
+            }
     out = {
         "metric": "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU",
         "value": round(value, 1),

@@ -29,6 +29,10 @@ def main():
     d, workload, alg = sys.argv[1], sys.argv[2], float(sys.argv[3])
     fetch_kib, n1 = per_launch(d, "FETCH_SIZE")
     write_kib, n2 = per_launch(d, "WRITE_SIZE")
+    try:  # wave-level VALU instructions per launch (VALU-issue roofline in bench.py)
+        valu, _ = per_launch(d, "SQ_INSTS_VALU")
+    except SystemExit:
+        valu = None
     hbm = 2 * fetch_kib * 1024 + write_kib * 1024
     out = {
         "workload": workload,
@@ -39,6 +43,7 @@ def main():
         "hbm_bytes_per_launch": round(hbm),
         "alg_bytes_per_launch": round(alg),
         "traffic_over_alg": round(hbm / alg, 3),
+        "valu_insts_per_launch": valu,
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads), WRITE_SIZE x1; KiB -> B",
         "source": d,
     }
