@@ -14,6 +14,7 @@ import contextlib
 import ctypes
 import math
 import random
+import sys
 from typing import Dict, List, Optional, Sequence, Union
 
 import numpy as np
@@ -46,6 +47,24 @@ def local_seed(vmas_random_state):
 
 def _f32(x) -> float:
     return float(np.float32(x))
+
+
+_storage_use_count = getattr(torch._C, "_storage_Use_Count", None)
+
+
+def _owned_or_clone(value):
+    """The reference clones every reward / observation / info it returns (environment.py:
+    149-196) so that callers never alias tensors the scenario keeps.  A tensor that nothing else
+    can reach -- the fresh result of torch.cat / an arithmetic op, referenced only by this call
+    (Python refcount) and sharing its storage with no other tensor (storage use count: the tensor
+    plus the temporary storage wrapper) -- is returned as is: identical values, no alias, one
+    kernel less.  Anything else (scenario attributes, views, dicts) is cloned as the reference
+    does."""
+    if (isinstance(value, Tensor) and _storage_use_count is not None
+            and sys.getrefcount(value) <= 3  # the caller's stack slot, this parameter, the argument
+            and _storage_use_count(value.untyped_storage()._cdata) <= 2):
+        return value
+    return TorchUtils.recursive_clone(value)
 
 
 class Environment(TorchVectorizedObject):
@@ -155,14 +174,14 @@ class Environment(TorchVectorizedObject):
         # order matters: rewards may mutate state that observations read (discovery.py:180-210)
         if get_rewards:
             for agent in self.agents:
-                reward = self.scenario.reward(agent).clone()
+                reward = _owned_or_clone(self.scenario.reward(agent))
                 if dict_agent_names:
                     rewards.update({agent.name: reward})
                 else:
                     rewards.append(reward)
         if get_observations:
             for agent in self.agents:
-                observation = TorchUtils.recursive_clone(self.scenario.observation(agent))
+                observation = _owned_or_clone(self.scenario.observation(agent))
                 if dict_agent_names:
                     obs.update({agent.name: observation})
                 else:
@@ -394,7 +413,13 @@ class Environment(TorchVectorizedObject):
             )
 
     def _set_action(self, action, agent, validated: bool = False):
-        action = action.clone()
+        # The reference clones the action so that its in-place ops never touch the caller's
+        # tensor.  The continuous path without communication has no in-place op on it: u is made
+        # out of place below (u = action * multiplier, the same values as clone + *=).
+        no_comm = not (self.world.dim_c > 0 and not agent.silent)
+        scaled = False
+        if not (self.continuous_actions and no_comm):
+            action = action.clone()
         comm_action = None
         if not self.grad_enabled:
             action = action.detach()
@@ -424,7 +449,11 @@ class Environment(TorchVectorizedObject):
                 assert not torch.any(torch.abs(physical_action) > agent.action.u_range_tensor), (
                     f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
                 )
-            agent.action.u = physical_action.to(torch.float32)
+            if no_comm:
+                agent.action.u = physical_action.to(torch.float32) * agent.action.u_multiplier_tensor
+                scaled = True
+            else:
+                agent.action.u = physical_action.to(torch.float32)
         else:
             if not self.multidiscrete_actions:
                 # flat index of the cartesian product of the discrete spaces -> multi-discrete
@@ -450,7 +479,8 @@ class Environment(TorchVectorizedObject):
                     physical_action[decrement] -= 1
                 agent.action.u[:, action_index] = (physical_action / (n - 1)) * (2 * u_max) - u_max
                 action_index += 1
-        agent.action.u *= agent.action.u_multiplier_tensor
+        if not scaled:
+            agent.action.u *= agent.action.u_multiplier_tensor
         if agent.action.u_noise > 0:
             noise = torch.randn(*agent.action.u.shape, device=self.device, dtype=torch.float32) * agent.u_noise
             agent.action.u += noise
