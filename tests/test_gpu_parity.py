@@ -80,3 +80,18 @@ def test_split_box_pairs_gpu(gpu_device, monkeypatch, split, name, kw, substeps)
     env = make(name, kw, substeps, gpu_device, num_envs=300, seed=1)
     for rep in step_parity(env, n_steps=3):
         assert rep["ok"], rep
+
+
+@pytest.mark.parametrize("name,kw,envs", [
+    ("transport", dict(n_agents=4), 32768),                         # C3
+    ("discovery", dict(n_agents=8, use_agent_lidar=True), 16384),   # C4
+    ("flocking", dict(n_agents=8), 32768),                          # C5 (per GPU)
+], ids=["C3_transport", "C4_discovery", "C5_flocking"])
+def test_baseline_configs_full_size_gpu(gpu_device, name, kw, envs):
+    """BASELINE.json configs C3-C5 at their full per-GPU sizes: teacher-forced step parity and
+    LIDAR parity against the oracle (0.1 % of envs may sit on a contact cut-off)."""
+    env = make(name, kw, None, gpu_device, num_envs=envs, seed=0)
+    for rep in step_parity(env, n_steps=2, max_bad_frac=1e-3):
+        assert rep["ok"], rep
+    rep = lidar_parity(env, max_bad_frac=1e-3)
+    assert rep["ok"], rep
