@@ -34,11 +34,13 @@ for _ in range(5):
 torch.cuda.synchronize()
 eng = env.world.engine
 print("kernel:", eng.kernel_name, eng.jit_error or "")
-t = eng.jit_profile().astype(np.int64)  # [max_substeps*4 + 2, 8]
+t = eng.jit_profile().astype(np.int64)  # [max_substeps*4 + 2, 16]
 S = env.world._substeps
 ms = eng._max_substeps
+nw = int((t[ms * 4 + 1] != 0).sum())  # waves that stamped the prologue release
+t = t[:, :nw]
 pro_done, pro_rel = t[ms * 4], t[ms * 4 + 1]
-st = t[: S * 4].reshape(S, 4, 8)
+st = t[: S * 4].reshape(S, 4, nw)
 start = np.concatenate([pro_rel[None], st[:-1, 3]], 0)  # each substep starts at the previous release
 pair = (st[:, 0] - start).mean(0)
 wait1 = (st[:, 1] - st[:, 0]).mean(0)
@@ -46,7 +48,7 @@ ent = (st[:, 2] - st[:, 1]).mean(0)
 wait2 = (st[:, 3] - st[:, 2]).mean(0)
 print(f"prologue: busy {(pro_done - pro_done.min()).tolist()} release at {int(pro_rel.max() - pro_done.min())}")
 print("wave | pair busy | wait | entity busy | wait   (cycles per substep, mean over substeps)")
-for w in range(8):
+for w in range(nw):
     print(f"{w:4d} | {pair[w]:9.0f} | {wait1[w]:6.0f} | {ent[w]:11.0f} | {wait2[w]:6.0f}")
 per_sub = (st[-1, 3].max() - pro_rel.min()) / S
 print(f"substep period {per_sub:.0f} cycles; pair makespan {pair.max():.0f}, entity makespan {ent.max():.0f}")

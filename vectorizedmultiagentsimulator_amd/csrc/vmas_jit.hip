@@ -39,6 +39,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -81,7 +82,21 @@ std::string fl(float v) {
 std::string it(long v) { return std::to_string(v); }
 std::string bl(bool v) { return v ? "true" : "false"; }
 
-constexpr int kNW = 8;
+// Largest float x with sqrtf(x) <= r (sqrtf correctly rounded on both the host and gfx950 with
+// -fno-fast-math, hence monotonic): for d2 = fl(fl(dx*dx) + fl(dy*dy)),
+// norm(d) <= r  <=>  d2 <= sq_limit(r), and norm(d) > r <=> d2 > sq_limit(r); NaN compares false
+// both ways, as in the reference.
+float sq_limit(float r) {
+    if (!(r >= 0.f)) return -1.f;  // no finite d2 qualifies (NaN / negative radius)
+    if (r == __builtin_huge_valf()) return __builtin_huge_valf();
+    float x = r * r;
+    while (x > 0.f && std::sqrt(x) > r) x = std::nextafter(x, 0.f);
+    while (std::sqrt(std::nextafter(x, __builtin_huge_valf())) <= r) x = std::nextafter(x, __builtin_huge_valf());
+    return x;
+}
+
+constexpr int kNW = 8;      // waves per workgroup (VMAS_JIT_WAVES overrides: 8 or 16)
+constexpr int kMaxNW = 16;  // column stride of the phase-profile buffer
 constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
 constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
 constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
@@ -106,6 +121,7 @@ struct Gen {
     int E, P, A, J, W, nfl;
     bool split_boxes = true;
     long lds_budget = kLdsTwoPerCu;
+    int nw = kNW;         // waves per workgroup
     int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
     std::vector<char> dyn, in_pair, need_trig, need_rot, split;
     std::vector<int> owner;  // wave owning a dynamic entity / loading a static pair entity
@@ -202,8 +218,8 @@ struct Gen {
             }
         }
         std::stable_sort(all.begin(), all.end(), [](const Task& a, const Task& b) { return a.cost > b.cost; });
-        wave_tasks.assign(kNW, {});
-        std::vector<float> load(kNW, 0.f);
+        wave_tasks.assign(nw, {});
+        std::vector<float> load(nw, 0.f);
         auto place = [&](const Task& t) {
             const int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
             wave_tasks[w].push_back(t);
@@ -220,14 +236,14 @@ struct Gen {
         for (const Task& t : finishes) place(t);
         // entity phase: dynamic entities over the waves by contribution count (LPT)
         owner.assign(E, -1);
-        wave_ents.assign(kNW, {});
-        wave_static.assign(kNW, {});
+        wave_ents.assign(nw, {});
+        wave_static.assign(nw, {});
         {
             std::vector<int> order;
             for (int e = 0; e < E; ++e)
                 if (dyn[e]) order.push_back(e);
             std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return items[a].size() > items[b].size(); });
-            std::vector<float> eload(kNW, 0.f);
+            std::vector<float> eload(nw, 0.f);
             for (int e : order) {
                 const int w = (int)(std::min_element(eload.begin(), eload.end()) - eload.begin());
                 owner[e] = w;
@@ -237,8 +253,8 @@ struct Gen {
             int rr = 0;
             for (int e = 0; e < E; ++e)
                 if (!dyn[e] && in_pair[e]) {
-                    owner[e] = rr % kNW;
-                    wave_static[rr % kNW].push_back(e);
+                    owner[e] = rr % nw;
+                    wave_static[rr % nw].push_back(e);
                     ++rr;
                 }
         }
@@ -254,7 +270,7 @@ struct Gen {
             if (need_rot[e]) r_rot[e] = rows(1);
             if (need_trig[e]) r_trig[e] = rows(4);
         }
-        for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : 4);
+        for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : res_rows(p));
         const long lds = (long)n_rows * 256 + (long)nfl * 4 + 4 * (n_split + 1);
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
@@ -323,7 +339,7 @@ struct Gen {
     // done, 3 after its barrier; prologue: slots max_substeps*4 + {0, 1}
     std::string stamp(int w, const std::string& slot) const {
         if (prof_block < 0) return "";
-        return "if (blockIdx.x == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kNW) + " + " +
+        return "if (blockIdx.x == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kMaxNW) + " + " +
                it(w) + "] = __builtin_amdgcn_s_memtime();\n";
     }
 
@@ -393,10 +409,18 @@ struct Gen {
                "    if (lane == 0 && bal) atomicOr(&FL[(a.S + s) * " + it(W) + " + " + it(p >> 5) + "], " +
                it(1u << (p & 31)) + "u);\n" + ind + "}\n";
     }
+    // result rows a whole pair needs: no torque is ever read from a sphere-sphere result, and
+    // none for the sphere side of a line/box-sphere result (the entity items' torque flags)
+    int res_rows(int p) const {
+        const int c = pd[p].cls;
+        return c == VMAS_PAIR_SS ? 2 : (c == VMAS_PAIR_LS || c == VMAS_PAIR_BS) ? 3 : 4;
+    }
     std::string store_res(int p, const std::string& ind) const {
-        const int r = res(p);
-        return ind + row(r) + " = o.fa.x; " + row(r, 1) + " = o.fa.y; " + row(r, 2) + " = o.ta; " + row(r, 3) +
-               " = o.tb;\n";
+        const int r = res(p), n = split[p] ? 4 : res_rows(p);
+        std::string o = ind + row(r) + " = o.fa.x; " + row(r, 1) + " = o.fa.y;";
+        if (n > 2) o += " " + row(r, 2) + " = o.ta;";
+        if (n > 3) o += " " + row(r, 3) + " = o.tb;";
+        return o + "\n";
     }
 
     void task_code(std::string& o, const Task& k, int w) const {
@@ -428,10 +452,13 @@ struct Gen {
             o += I + "}\n        }\n";
             return;
         }
+        const bool needs_d2 = q.cls != VMAS_PAIR_JOINT && (k.part == kWhole || k.part == 0);
+        if (needs_d2)  // squared centre distance, rounded as inside norm()
+            o += I + "const V2 dl = " + pos(q.ea, w) + " - " + pos(q.eb, w) + ";\n" + I +
+                 "const float d2 = dl.x * dl.x + dl.y * dl.y;\n";
         if (k.part == kWhole || k.part == 0) {
-            if (q.cls != VMAS_PAIR_JOINT)
-                o += I + "const bool inr = norm(" + pos(q.ea, w) + " - " + pos(q.eb, w) + ") <= " + fl(q.bp_radius) +
-                     ";\n";
+            if (q.cls != VMAS_PAIR_JOINT)  // norm(pa - pb) <= bp_radius, without the sqrt
+                o += I + "const bool inr = d2 <= " + fl(sq_limit(q.bp_radius)) + ";\n";
             else
                 o += I + "const bool inr = true;\n";
             o += flag_r(p, I);
@@ -444,7 +471,11 @@ struct Gen {
                 o += I + "    const float fixed_rot = frp ? frp[(long)bb * " + S_(S_JFIX, 0, j) + "] : " +
                      fl(jd[j].fixed_rotation) + ";\n";
             }
-            o += I + "    const PairOut o = " + pair_call(p, w) + ";\n";
+            if (q.cls == VMAS_PAIR_SS)  // every lane beyond d_min: the reference's force is 0
+                o += I + "    const PairOut o = vote_all(d2 > " + fl(sq_limit(q.dmin)) +
+                     ") ? PairOut{mk(0.f, 0.f), 0.f, 0.f} : " + pair_call(p, w) + ";\n";
+            else
+                o += I + "    const PairOut o = " + pair_call(p, w) + ";\n";
             o += store_res(p, I + "    ");
             if (q.cls != VMAS_PAIR_JOINT) o += flag_z(p, I + "    ");
             o += I + "}\n        }\n";
@@ -596,10 +627,10 @@ struct Gen {
             if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + desc(e) + ";\n";
         o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
              "uint32_t* DONE, int lane, int b, int bb, bool valid);\n\n";
-        for (int w = 0; w < kNW; ++w) wave_body(o, w);
+        for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
-        const int waves_per_eu = lds_budget <= kLdsTwoPerCu ? 4 : 2;
-        o += "extern \"C\" __global__ void __launch_bounds__(" + it(kNW * 64) + ", " + it(waves_per_eu) +
+        const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
+        o += "extern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) +
              ") k_world(Args a) {\n";
         o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
@@ -612,7 +643,7 @@ struct Gen {
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
         o += "    switch (wave) {\n";
-        for (int w = 0; w < kNW; ++w)
+        for (int w = 0; w < nw; ++w)
             o += "        case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, lane, b, bb, valid); break;\n";
         o += "        default: break;\n    }\n";
         o += "    if (a.blk) {\n        __syncthreads();\n        uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
@@ -624,7 +655,7 @@ struct Gen {
 // whole LDS (one workgroup per CU).  VMAS_JIT_SPLIT=0 disables splitting.
 std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<VmasEntityDesc>& ed,
                                const std::vector<VmasPairDesc>& pd, const std::vector<VmasJointDesc>& jd,
-                               std::string* why) {
+                               std::string* why, int force_nw = 0) {
     const char* sp = getenv("VMAS_JIT_SPLIT");
     const bool allow_split = !(sp && sp[0] == '0');
     const struct {
@@ -640,6 +671,14 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
         }
         g->split_boxes = t.split;
         g->lds_budget = t.budget;
+        // 16 waves per workgroup once there are enough pair tasks to spread (measured: flocking
+        // 81 pairs 72 -> 59 us, discovery 19.2 -> 16.3 us; balance's 24 tasks 67.7 -> 69.7 us)
+        int n_tasks = 0;
+        for (const auto& q : pd)
+            n_tasks += (t.split && (q.cls == VMAS_PAIR_BL || q.cls == VMAS_PAIR_BB)) ? Gen::parts(q.cls) + 1 : 1;
+        g->nw = n_tasks >= 32 ? 16 : kNW;
+        if (const char* nws = getenv("VMAS_JIT_WAVES")) g->nw = atoi(nws) == 16 ? 16 : kNW;
+        if (force_nw) g->nw = force_nw;
         why->clear();
         if (g->plan(why)) return g;
     }
@@ -740,7 +779,7 @@ struct VmasJitWorld {
     std::string src;
     std::vector<std::pair<int, int>> ptr_src, str_src;
     size_t arg_bytes = 0;
-    int W = 1, nblk = 0;
+    int W = 1, nblk = 0, nw = kNW;
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
@@ -790,31 +829,46 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             delete W;
             return jfail(VMAS_E_INVALID, "bad pair table");
         }
+    auto cleanup = [&](int32_t rc) {
+        vmas_jit_world_destroy(W);
+        return rc;
+    };
+    JHIP(hipSetDevice(cfg->device));
     std::string why;
-    std::unique_ptr<Gen> gp = make_plan(W->cfg, W->ed, W->pd, W->jd, &why);
-    if (!gp) {
-        delete W;
-        return jfail(VMAS_E_INVALID, "world not specialised: %s", why.c_str());
+    std::unique_ptr<Gen> gp;
+    // A 16-wave kernel whose register budget (8 waves/SIMD -> 64 VGPRs) makes it spill is
+    // regenerated with 8 waves (measured: pollock 154 spilled VGPRs at 16 waves).
+    for (int force_nw : {0, kNW}) {
+        gp = make_plan(W->cfg, W->ed, W->pd, W->jd, &why, force_nw);
+        if (!gp) {
+            delete W;
+            return jfail(VMAS_E_INVALID, "world not specialised: %s", why.c_str());
+        }
+        Gen& g = *gp;
+        if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
+        g.generate();
+        std::vector<char> code;
+        if (int32_t rc = compile(g.src, &code)) return cleanup(rc);
+        if (W->mod) {
+            (void)hipModuleUnload(W->mod);
+            W->mod = nullptr;
+        }
+        if (hipModuleLoadData(&W->mod, code.data()) != hipSuccess)
+            return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
+        if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
+            return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
+        int scratch = 0;
+        (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
+        if (scratch == 0 || g.nw == kNW) break;
     }
     Gen& g = *gp;
-    if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
-    g.generate();
     W->src = g.src;
     W->ptr_src = g.ptr_src;
     W->str_src = g.str_src;
     W->arg_bytes = g.arg_bytes();
     W->W = g.W;
+    W->nw = g.nw;
     W->nblk = (cfg->batch + 63) / 64;
-    auto cleanup = [&](int32_t rc) {
-        vmas_jit_world_destroy(W);
-        return rc;
-    };
-    std::vector<char> code;
-    if (int32_t rc = compile(W->src, &code)) return cleanup(rc);
-    JHIP(hipSetDevice(cfg->device));
-    if (hipModuleLoadData(&W->mod, code.data()) != hipSuccess) return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
-    if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
-        return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
     const size_t nwords = (size_t)cfg->max_substeps * W->W;
     if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
         hipMalloc((void**)&W->d_blk, (size_t)W->nblk * 2 * nwords * 4) != hipSuccess ||
@@ -822,7 +876,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
     if (g.prof_block >= 0) {
-        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kNW;
+        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW;
         if (hipMalloc((void**)&W->d_prof, W->n_prof * 8) != hipSuccess ||
             hipMemset(W->d_prof, 0, W->n_prof * 8) != hipSuccess)
             return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc profile buffer"));
@@ -969,7 +1023,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
             }
             JHIP(hipEventRecord(ev.first, stream));
         }
-        JHIP(hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, kNW * 64, 1, 1, 0, stream, nullptr, extra));
+        JHIP(hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr, extra));
         if (W->timing) {
             JHIP(hipEventRecord(ev.second, stream));
             W->ev_pending.push_back(ev);

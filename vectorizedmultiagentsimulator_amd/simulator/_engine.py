@@ -379,7 +379,8 @@ class PhysicsEngine:
         return buf.value.decode()
 
     def jit_profile(self):
-        """Phase timestamps [max_substeps*4 + 2, 8] of the profiled workgroup (VMAS_JIT_PROFILE)."""
+        """Phase timestamps [max_substeps*4 + 2, 16 wave columns] of the profiled workgroup
+        (VMAS_JIT_PROFILE); columns past the kernel's wave count stay 0."""
         if self._jit is None:
             return None
         n = self.lib.vmas_jit_world_profile(self._jit, None, 0)
@@ -388,7 +389,7 @@ class PhysicsEngine:
             return None
         out = np.zeros(n, dtype=np.uint64)
         N.check_jit(self.lib.vmas_jit_world_profile(self._jit, out.ctypes.data, n), "vmas_jit_world_profile")
-        return out.reshape(-1, 8)
+        return out.reshape(-1, 16)
 
     def jit_compile_check(self) -> str:
         """Generate and hipRTC-compile this world's specialised kernel without a device (build

@@ -162,6 +162,10 @@ class TorchUtils:
         return torch.where(mask, new_value, old_value)
 
 
+# tries consumed by the last find_random_pos_for_entity call of a given shape
+_SPAWN_HINT: Dict[tuple, int] = {}
+
+
 class ScenarioUtils:
     """Reset-time helpers (utils.py:239-330)."""
 
@@ -235,7 +239,10 @@ class ScenarioUtils:
         pos = torch.empty((batch_size, 1, 2), device=dev, dtype=torch.float32)
         resolved = torch.full((batch_size,), -1, device=dev, dtype=torch.int32)
         states = []  # generator state after each try, to rewind to the reference's consumption
-        first, n = 0, 8
+        # first batch sized from the last consumption at this call shape (over-drawn tries are
+        # rewound, so the size only trades draws for syncs)
+        key = (batch_size, occ.shape[1], float(min_dist_between_entities), tuple(x_bounds), tuple(y_bounds))
+        first, n = 0, min(64, max(4, _SPAWN_HINT.get(key, 6) + 2))
         mx, un = N._i32(0), N._i32(0)
         while True:
             cand = torch.empty((n, 2, batch_size), device=dev, dtype=torch.float32)
@@ -258,6 +265,7 @@ class ScenarioUtils:
                     "You can disable this warning by setting disable_warn=True"
                 )
         consumed = 1 if mx.value == 0 else mx.value + 2
+        _SPAWN_HINT[key] = consumed
         if consumed <= len(states):
             gen.set_state(states[consumed - 1])
         else:  # the reference's final (unused) proposal lies just past the last batch
