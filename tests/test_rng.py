@@ -1,0 +1,73 @@
+"""local_seed's numpy RNG swap (environment/_rng.py) must behave exactly like the reference's
+get_state/set_state swap (environment.py:30-46): same draws inside and outside the simulator's
+context, gaussian cache included (odd numbers of legacy normal draws on both sides)."""
+import contextlib
+import random
+
+import numpy as np
+import torch
+
+from vectorizedmultiagentsimulator_amd.simulator.environment import environment as envmod
+from vectorizedmultiagentsimulator_amd.simulator.environment._rng import numpy_global_rng
+
+
+@contextlib.contextmanager
+def reference_local_seed(state):  # the reference's swap, verbatim semantics
+    t, n, p = torch.random.get_rng_state(), np.random.get_state(), random.getstate()
+    torch.random.set_rng_state(state[0])
+    np.random.set_state(state[1])
+    random.setstate(state[2])
+    yield
+    state[0], state[1], state[2] = torch.random.get_rng_state(), np.random.get_state(), random.getstate()
+    torch.random.set_rng_state(t)
+    np.random.set_state(n)
+    random.setstate(p)
+
+
+def _script(ctx_factory):
+    """Interleaved draws inside/outside the simulator context; returns every value drawn."""
+    torch.manual_seed(11)
+    np.random.seed(11)
+    random.seed(11)
+    np.random.normal()  # the user's side has a cached gaussian when the context is entered
+    torch.manual_seed(5)
+    np.random.seed(5)
+    random.seed(5)
+    inner = [torch.random.get_rng_state(), np.random.get_state(), random.getstate()]
+    torch.manual_seed(11)
+    np.random.seed(11)
+    random.seed(11)
+    np.random.normal()
+    out = []
+    for i in range(6):
+        with ctx_factory(inner):
+            out += list(np.random.normal(size=1 + i % 2))  # odd / even gaussian counts
+            out += list(np.random.uniform(size=3))
+            out += [torch.rand(2).tolist(), random.random()]
+        out += list(np.random.normal(size=1 + (i + 1) % 2))
+        out += [np.random.randint(1000), torch.rand(1).item(), random.random()]
+    return out
+
+
+def test_fast_swap_is_active_and_exact():
+    assert numpy_global_rng().fast  # the offset probe validated on this numpy build
+    saved = np.random.get_state()
+    try:
+        expected = _script(reference_local_seed)
+        got = _script(envmod.local_seed)
+    finally:
+        np.random.set_state(saved)
+    assert len(expected) == len(got)
+    for a, b in zip(expected, got):
+        assert a == b
+
+
+def test_restore_accepts_legacy_tuples():
+    r = numpy_global_rng()
+    st = np.random.get_state()
+    np.random.seed(3)
+    a = np.random.normal(size=3)
+    r.restore(st)
+    np.random.seed(3)
+    assert np.array_equal(a, np.random.normal(size=3))
+    np.random.set_state(st)

@@ -25,23 +25,28 @@ from ..core import Agent, TorchVectorizedObject
 from ..scenario import BaseScenario
 from ..utils import AGENT_OBS_TYPE, DEVICE_TYPING, TorchUtils, override
 from . import spaces
+from ._rng import numpy_global_rng
 
 
 @contextlib.contextmanager
 def local_seed(vmas_random_state):
-    """Swap in the simulator's RNG states for torch(CPU)/numpy/python (environment.py:30-46)."""
+    """Swap in the simulator's RNG states for torch(CPU)/numpy/python (environment.py:30-46).
+
+    The numpy state is saved/restored by ``_rng.NumpyGlobalRng`` (the same state as
+    get_state/set_state, without their element-wise key copies)."""
+    npr = numpy_global_rng()
     torch_state = torch.random.get_rng_state()
-    np_state = np.random.get_state()
+    np_state = npr.snapshot()
     py_state = random.getstate()
     torch.random.set_rng_state(vmas_random_state[0])
-    np.random.set_state(vmas_random_state[1])
+    npr.restore(vmas_random_state[1])
     random.setstate(vmas_random_state[2])
     yield
     vmas_random_state[0] = torch.random.get_rng_state()
-    vmas_random_state[1] = np.random.get_state()
+    vmas_random_state[1] = npr.snapshot()
     vmas_random_state[2] = random.getstate()
     torch.random.set_rng_state(torch_state)
-    np.random.set_state(np_state)
+    npr.restore(np_state)
     random.setstate(py_state)
 
 
