@@ -284,8 +284,17 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
                               const VmasPairDesc* pairs, const VmasJointDesc* joints,
                               VmasJitWorld** out_world);
 int32_t vmas_jit_world_destroy(VmasJitWorld* world);
+/* With the batch broadphase the step is one persistent launch that runs every fixed-point pass
+ * on the device (no host wait): *iterations is then 0 and vmas_jit_world_passes reports the
+ * count.  A device-side failure (no convergence, a wait timeout) is returned by
+ * vmas_jit_world_passes and by the next vmas_jit_world_step. */
 int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
                             int32_t* iterations);
+/* Fixed-point passes of the last step (waits for it on its stream). */
+int32_t vmas_jit_world_passes(VmasJitWorld* world, int32_t* passes);
+/* Persistent grid size: > 0 cooperative launch, < 0 plain launch, 0 host-driven passes
+ * (VMAS_JIT_GRID=coop|plain|host at create). */
+int32_t vmas_jit_world_grid(const VmasJitWorld* world);
 int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
 int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
                                   int64_t* launches);

@@ -58,6 +58,39 @@ def test_jit_balance_full_size_gpu(gpu_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps,num_envs", [
+    ("balance", dict(n_agents=4), 10, 100_000),  # more 64-env groups than resident workgroups
+    ("flocking", dict(n_agents=6), None, 3000),
+    ("waterfall", dict(), None, 700),
+], ids=["balance100k", "flocking", "waterfall"])
+def test_device_fixed_point_matches_host_loop_gpu(gpu_device, monkeypatch, name, kw, substeps, num_envs):
+    """The persistent launch (fixed-point passes on the device, cooperative or plain launch)
+    is bit-identical to the host-driven pass loop and runs the same number of passes."""
+    envs = {}
+    for mode in ("host", "coop", "plain"):
+        monkeypatch.setenv("VMAS_JIT_GRID", mode)
+        envs[mode] = make(name, kw, substeps, gpu_device, num_envs=num_envs, seed=2)
+        envs[mode].world.engine._ensure()  # the mode is read when the kernel is built
+    snap = O.snapshot(envs["host"].world)
+    for mode, env in envs.items():
+        O.load_snapshot(env.world, snap)
+    for _ in range(3):
+        for env in envs.values():
+            env.world.step()
+        eng = {m: e.world.engine for m, e in envs.items()}
+        assert eng["host"].kernel_name == "k_world" and eng["host"].jit_grid == 0
+        assert eng["coop"].jit_grid > 0 and eng["plain"].jit_grid < 0
+        passes = {m: e.last_iterations for m, e in eng.items()}
+        assert passes["coop"] == passes["plain"] == passes["host"] >= 1, passes
+        a = O.snapshot(envs["host"].world)
+        for mode in ("coop", "plain"):
+            b = O.snapshot(envs[mode].world)
+            for i in a:
+                for k in a[i]:
+                    assert torch.equal(a[i][k], b[i][k]), (mode, i, k)
+
+
+@pytest.mark.gpu
 def test_oversized_world_runs_generic_kernel_gpu(gpu_device):
     env = make("pollock", dict(n_agents=8, n_lines=10, n_boxes=10), None, gpu_device, num_envs=128, seed=0)
     for rep in step_parity(env, n_steps=2):

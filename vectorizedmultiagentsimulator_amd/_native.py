@@ -69,6 +69,8 @@ EXPORTED_SYMBOLS = (
     "vmas_jit_world_source",
     "vmas_jit_compile_check",
     "vmas_jit_world_profile",
+    "vmas_jit_world_passes",
+    "vmas_jit_world_grid",
     "vmas_jit_last_error",
 )
 
@@ -318,6 +320,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_jit_compile_check.argtypes = [_vp, _vp, _vp, _vp, _vp, ctypes.c_int64]
     lib.vmas_jit_world_profile.restype = _i32
     lib.vmas_jit_world_profile.argtypes = [_vp, _vp, ctypes.c_int64]
+    lib.vmas_jit_world_passes.restype = _i32
+    lib.vmas_jit_world_passes.argtypes = [_vp, ctypes.POINTER(_i32)]
+    lib.vmas_jit_world_grid.restype = _i32
+    lib.vmas_jit_world_grid.argtypes = [_vp]
     lib.vmas_jit_last_error.restype = ctypes.c_char_p
     ver = lib.vmas_abi_version()
     if ver != VMAS_ABI_VERSION:

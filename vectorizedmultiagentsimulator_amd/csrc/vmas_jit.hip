@@ -29,11 +29,17 @@
 // Worlds beyond the kernel-argument or LDS budget return VMAS_E_INVALID from
 // vmas_jit_world_create and the caller uses vmas_world_step.
 //
-// Batch-global broadphase (core.py:2796): identical fixed-point scheme to vmas_world_step (R/Z
-// flags per block, a reduction that checks the mask, host re-run on violation).
+// Batch-global broadphase (core.py:2796): the fixed-point scheme of vmas_world_step (R/Z flags
+// per block, a reduction that checks the mask, a re-run on violation), run on the device: the
+// grid is persistent (at most the resident workgroup count, each striding over 64-env groups)
+// and workgroup 0 reduces the flags between passes while the others wait on a published state
+// word (vmas_jit_ops.hpp grid_fixed_point), so the host only launches.  VMAS_JIT_GRID=host keeps
+// the host-driven loop (one launch + reduction + host read per pass).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <dlfcn.h>
+
+#include "vmas_jit_ops.hpp"
 
 #include <algorithm>
 #include <cstdarg>
@@ -271,7 +277,10 @@ struct Gen {
             if (need_trig[e]) r_trig[e] = rows(4);
         }
         for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : res_rows(p));
-        const long lds = (long)n_rows * 256 + (long)nfl * 4 + 4 * (n_split + 1);
+        // rows + FL + DONE + the pass's mask words + the fixed point's reduction words (in the
+        // row buffer when it is large enough)
+        const long red = (long)std::max(n_rows, 1) * 64 >= nfl + 2 ? 0 : nfl + 2;
+        const long lds = (long)n_rows * 256 + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) + 4 * red;
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
             return false;
@@ -306,7 +315,7 @@ struct Gen {
     }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 3) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 5) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
     }
 
     // expressions for entity e as seen by wave w (registers when w owns it)
@@ -339,7 +348,7 @@ struct Gen {
     // done, 3 after its barrier; prologue: slots max_substeps*4 + {0, 1}
     std::string stamp(int w, const std::string& slot) const {
         if (prof_block < 0) return "";
-        return "if (blockIdx.x == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kMaxNW) + " + " +
+        return "if ((b >> 6) == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kMaxNW) + " + " +
                it(w) + "] = __builtin_amdgcn_s_memtime();\n";
     }
 
@@ -506,7 +515,8 @@ struct Gen {
 
     void wave_body(std::string& o, int w) {
         o += "template <> __device__ __forceinline__ void run<" + it(w) +
-             ">(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, int lane, int b, int bb, bool valid) {\n";
+             ">(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, "
+             "bool valid) {\n";
         // prologue: static pair entities (loaded once), dynamic entities into registers
         for (int e : wave_static[w]) {
             o += "    {  // static entity " + it(e) + "\n";
@@ -544,7 +554,7 @@ struct Gen {
         for (int e : wave_ents[w])
             for (const Item& x : items[e]) word[x.pair >> 5] = 1;
         for (int k = 0; k < W; ++k)
-            if (word[k]) o += "        const uint32_t m" + it(k) + " = a.mask[s * " + it(W) + " + " + it(k) + "];\n";
+            if (word[k]) o += "        const uint32_t m" + it(k) + " = MSK[s * " + it(W) + " + " + it(k) + "];\n";
         for (const Task& t : wave_tasks[w]) task_code(o, t, w);
         o += "        " + stamp(w, "s * 4");
         o += "        __syncthreads();\n";
@@ -610,8 +620,9 @@ struct Gen {
         std::string& o = src;
         o += "// generated by vmas_jit.hip for one world\n#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
-             "];\n    float* out[6];\n    const uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
-             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int pad;\n};\n\n";
+             "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
+             "    uint32_t* ctl;\n    uint32_t* err;\n"
+             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
              "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
@@ -626,7 +637,7 @@ struct Gen {
         for (int e = 0; e < E; ++e)
             if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + desc(e) + ";\n";
         o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
-             "uint32_t* DONE, int lane, int b, int bb, bool valid);\n\n";
+             "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid);\n\n";
         for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
         const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
@@ -635,19 +646,42 @@ struct Gen {
         o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
-        o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n"
-             "    const int b = blockIdx.x * 64 + lane;\n"
-             "    const bool valid = b < a.B;\n"
-             "    const int bb = valid ? b : (a.B - 1);\n";
-        o += "    const int nfl = 2 * a.S * " + it(W) + ";\n"
-             "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+        // LDS of the device-side fixed point: the row buffer when it is large enough (it is
+        // idle between passes), else its own array
+        const int red_words = nfl + 2;
+        o += "    __shared__ uint32_t MSK[" + it(std::max(nfl / 2, 1)) + "];\n";
+        if ((long)std::max(n_rows, 1) * 64 >= red_words)
+            o += "    uint32_t* RED = reinterpret_cast<uint32_t*>(L);\n";
+        else
+            o += "    __shared__ uint32_t RED[" + it(red_words) + "];\n";
+        o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n";
+        o += "    const int nfl = 2 * a.S * " + it(W) + ", ngrp = (a.B + 63) >> 6;\n"
              "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
-        o += "    switch (wave) {\n";
+        // Persistent launch (a.ctl set, every workgroup resident): workgroups stride over the
+        // 64-env groups and run the passes of the broadphase fixed point without the host.
+        // Otherwise one group per workgroup and one pass per launch.  DONE is back to zero at
+        // the end of every substep's pair phase, so it carries over between groups.
+        o += "    for (int pass = 0;; ++pass) {\n"
+             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+             "        for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
+             "            MSK[i] = ~__hip_atomic_load(&a.mask[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+             "        for (int g = blockIdx.x; g < ngrp; g += gridDim.x) {\n"
+             "            const int b = g * 64 + lane;\n"
+             "            const bool valid = b < a.B;\n"
+             "            const int bb = valid ? b : (a.B - 1);\n"
+             "            switch (wave) {\n";
         for (int w = 0; w < nw; ++w)
-            o += "        case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, lane, b, bb, valid); break;\n";
-        o += "        default: break;\n    }\n";
-        o += "    if (a.blk) {\n        __syncthreads();\n        uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
-             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) dst[i] = FL[i];\n    }\n}\n";
+            o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
+        o += "                default: break;\n            }\n        }\n";
+        o += "        if (!a.blk) return;\n"
+             "        __syncthreads();\n"
+             "        uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
+             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x)\n"
+             "            __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+             "        if (!a.ctl) return;\n"
+             "        if (!grid_fixed_point(a.blk, a.mask, a.ctl, a.err, a.S * " + it(W) +
+             ", pass, a.max_pass, RED)) return;\n"
+             "    }\n}\n";
     }
 };
 
@@ -711,12 +745,12 @@ __global__ void __launch_bounds__(1024) k_jit_flags_reduce(const uint32_t* blk, 
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
-        const uint32_t m = mask[w];
+        const uint32_t m = ~mask[w];  // stored inverted (zero memset = all pairs active)
         if ((m & ~R[w] & Z[w]) | (~m & R[w])) atomicOr(&viol, 1u);
     }
     __syncthreads();
     if (viol)
-        for (int w = threadIdx.x; w < nwords; w += blockDim.x) mask[w] = R[w];
+        for (int w = threadIdx.x; w < nwords; w += blockDim.x) mask[w] = ~R[w];
     if (threadIdx.x == 0) *viol_out = viol;
 }
 
@@ -783,6 +817,14 @@ struct VmasJitWorld {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
+    // persistent launch: d_ctl = [kGridCtlWords control words | inverted mask words], zeroed by
+    // one memset per step; d_err/h_err: sticky error bits and their pinned host copy
+    uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr;
+    int grid = 0;          // persistent workgroups (0: one pass per launch, host-driven loop)
+    bool coop = false;     // cooperative launch (VMAS_JIT_GRID=coop)
+    hipStream_t last_stream = nullptr;
+    int last_passes = 0;   // passes of the last host-driven step (persistent: read on demand)
+    bool last_persistent = false;
     unsigned long long* d_prof = nullptr;  // phase timestamps of one workgroup (VMAS_JIT_PROFILE)
     size_t n_prof = 0;
     bool timing = false;
@@ -805,6 +847,9 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
         if (W->d_viol) (void)hipFree(W->d_viol);
         if (W->h_viol) (void)hipHostFree(W->h_viol);
         if (W->d_prof) (void)hipFree(W->d_prof);
+        if (W->d_ctl) (void)hipFree(W->d_ctl);
+        if (W->d_err) (void)hipFree(W->d_err);
+        if (W->h_err) (void)hipHostFree(W->h_err);
         for (auto& ev : W->ev_pending) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
         for (auto& ev : W->ev_free) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     }
@@ -875,6 +920,29 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
+    if (hipMalloc((void**)&W->d_ctl, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
+        hipHostMalloc((void**)&W->h_err, 4, hipHostMallocDefault) != hipSuccess ||
+        hipMemset(W->d_err, 0, 4) != hipSuccess)
+        return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc fixed-point control words"));
+    *W->h_err = 0u;
+    // Persistent grid: as many workgroups as can be resident at once (occupancy x CUs), capped
+    // by the number of 64-env groups, launched as a plain launch: the workgroups of one launch on
+    // an in-order stream all become resident (any other kernel holding CUs finishes without
+    // waiting on this one), and every wait is bounded anyway.  VMAS_JIT_GRID=coop uses the
+    // cooperative API instead (residency guaranteed by the runtime; measured +18 us per launch),
+    // =host the host-driven loop (one launch + reduction + host read per pass).
+    {
+        const char* gm = getenv("VMAS_JIT_GRID");
+        const std::string mode = gm ? gm : "plain";
+        int per_cu = 0, cus = 0;
+        if (mode != "host" &&
+            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, W->fn, W->nw * 64, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
+            per_cu > 0 && cus > 0) {
+            W->grid = std::min(W->nblk, per_cu * cus);
+            W->coop = mode == "coop";
+        }
+    }
     if (g.prof_block >= 0) {
         W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW;
         if (hipMalloc((void**)&W->d_prof, W->n_prof * 8) != hipSuccess ||
@@ -973,10 +1041,14 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(io->out_ang_vel);
     put_ptr(io->out_force);
     put_ptr(io->out_torque);
-    put_ptr(W->d_mask);
     const bool batch_bp = io->broadphase == VMAS_BROADPHASE_BATCH;
+    const bool persistent = batch_bp && W->grid > 0;
+    uint32_t* nmask = persistent ? W->d_ctl + vmas::kGridCtlWords : W->d_mask;
+    put_ptr(nmask);
     put_ptr(batch_bp ? W->d_blk : nullptr);
     put_ptr(W->d_prof);
+    put_ptr(persistent ? W->d_ctl : nullptr);
+    put_ptr(W->d_err);
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
         int32_t v = 0;
@@ -1003,15 +1075,23 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_i32(io->substeps);
     memcpy(p, &io->sub_dt, 4);
     p += 4;
-    put_i32(0);
+    const int max_it = batch_bp ? io->substeps + 2 : 1;
+    put_i32(max_it);
     size_t size = (size_t)(p - buf.data());
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
 
+    // a fixed-point failure of an earlier persistent step (sticky device bits, copied back
+    // asynchronously after every persistent launch) surfaces here
+    if (uint32_t e = *(volatile uint32_t*)W->h_err)
+        return jfail(e & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
+                     "device-side broadphase fixed point failed in an earlier step (error bits 0x%x)", e);
+    W->last_stream = stream;
+    W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
-    JHIP(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
-    const int max_it = batch_bp ? io->substeps + 2 : 1;
-    for (int it = 0; it < max_it; ++it) {
+    if (persistent) JHIP(hipMemsetAsync(W->d_ctl, 0, (vmas::kGridCtlWords + nwords) * 4, stream));
+    else JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
+    auto timed = [&](auto&& launch) -> int32_t {
         std::pair<hipEvent_t, hipEvent_t> ev{};
         if (W->timing) {
             if (W->ev_free.empty()) {
@@ -1023,11 +1103,33 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
             }
             JHIP(hipEventRecord(ev.first, stream));
         }
-        JHIP(hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr, extra));
+        JHIP(launch());
         if (W->timing) {
             JHIP(hipEventRecord(ev.second, stream));
             W->ev_pending.push_back(ev);
         }
+        return VMAS_OK;
+    };
+    if (persistent) {
+        // one launch runs every pass; nothing waits on the host
+        void* params[] = {buf.data()};
+        if (int32_t rc = timed([&] {
+                return W->coop ? hipModuleLaunchCooperativeKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream,
+                                                                  params)
+                               : hipModuleLaunchKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr,
+                                                       extra);
+            }))
+            return rc;
+        JHIP(hipMemcpyAsync(W->h_err, W->d_err, 4, hipMemcpyDeviceToHost, stream));
+        if (iterations) *iterations = 0;  // not known without a sync: vmas_jit_world_passes
+        return VMAS_OK;
+    }
+    for (int it = 0; it < max_it; ++it) {
+        if (int32_t rc = timed([&] {
+                return hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr, extra);
+            }))
+            return rc;
+        W->last_passes = it + 1;
         if (iterations) *iterations = it + 1;
         if (!batch_bp) return VMAS_OK;
         hipLaunchKernelGGL(k_jit_flags_reduce, dim3(1), dim3(1024), 0, stream, (const uint32_t*)W->d_blk, W->nblk,
@@ -1038,6 +1140,31 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
         if (*W->h_viol == 0u) return VMAS_OK;
     }
     return jfail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
+}
+
+// Passes the last step ran (waits for it).  Also reports a device-side fixed-point failure.
+int32_t vmas_jit_world_passes(VmasJitWorld* W, int32_t* passes) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    if (!W->last_persistent) {
+        if (passes) *passes = W->last_passes;
+        return VMAS_OK;
+    }
+    JHIP(hipSetDevice(W->cfg.device));
+    JHIP(hipStreamSynchronize(W->last_stream));
+    uint32_t ctl[3] = {0, 0, 0}, err = 0;
+    JHIP(hipMemcpy(ctl, W->d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    JHIP(hipMemcpy(&err, W->d_err, 4, hipMemcpyDeviceToHost));
+    if (passes) *passes = (int32_t)ctl[2];
+    if (err)
+        return jfail(err & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
+                     "device-side broadphase fixed point failed (error bits 0x%x)", err);
+    return VMAS_OK;
+}
+
+// 0: host-driven passes; otherwise the persistent grid size (negative: plain, non-cooperative launch)
+int32_t vmas_jit_world_grid(const VmasJitWorld* W) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    return W->coop ? W->grid : -W->grid;
 }
 
 int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {

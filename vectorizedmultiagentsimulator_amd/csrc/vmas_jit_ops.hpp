@@ -74,4 +74,126 @@ __device__ __forceinline__ void integrate(const VmasEntityDesc& d, int substep, 
     }
 }
 
+#ifndef __HIP_MEMORY_SCOPE_AGENT
+#define __HIP_MEMORY_SCOPE_AGENT 4
+#endif
+
+// Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily)
+constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
+// spin bound of a waiting workgroup (~2^22 polls of >= 64 clocks: seconds, far above any pass)
+constexpr uint32_t kGridSpinLimit = 1u << 22;
+
+// Device-side fixed point of the batch-global broadphase for a persistent launch (every
+// workgroup resident).  Each workgroup has stored the OR of its R/Z activity words in
+// blk[blockIdx.x] ([2][nwords]) and arrives on a two-level counter; the LAST workgroup to
+// arrive ORs every row, applies the k_jit_flags_reduce test (was the mask a fixed point?),
+// publishes the next mask (stored inverted, so a zero memset means "all pairs active") and a
+// continue bit; the others wait for that bit.
+// ctl (zeroed per launch): [0] top arrival counter, [1] published ((pass+1) << 1 | continue),
+// [2] passes run, [32 * (1 + k)] arrival counter of the workgroups with blockIdx % 8 == k (one
+// 128-byte line each: 512 arrivals on one address serialise at the memory side).
+// RED: workgroup LDS of 2 * nwords + 2 words.  Returns whether another pass is needed.  Every
+// wait is bounded: a timeout stops the passes and sets an error bit instead of hanging.
+//
+// Everything exchanged between workgroups (blk rows, mask words, ctl) is accessed only with
+// agent-scope atomics, which are coherent across the XCDs' L2s by themselves; a writer waits
+// for its stores (s_waitcnt) before the workgroup barrier that precedes the arrival/publish
+// atomic.  Agent-scope fences are avoided: a release writes back the whole XCD L2 and an
+// acquire invalidates it (measured: per-wave fences cost 120 us per launch, one fence per
+// workgroup still 40-60 us, on a 10-70 us kernel).
+constexpr int kGridCtlWords = 32 * 9;
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err,
+                                        int nwords, int pass, int max_pass, uint32_t* RED) {
+    const uint32_t G = gridDim.x, k = blockIdx.x & 7u;
+    const uint32_t n_k = (G + 7u - k) / 8u, n_sub = G < 8u ? G : 8u;  // workgroups in sub-counter k
+    const int nw2 = 2 * nwords;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's blk stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        bool last = false;
+        if (add_agent(&ctl[32 * (1 + k)], 1u) == n_k * (uint32_t)(pass + 1) - 1u)
+            last = add_agent(&ctl[0], 1u) == n_sub * (uint32_t)(pass + 1) - 1u;
+        RED[nw2] = last ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool reducer = RED[nw2] != 0u;
+    __syncthreads();
+    if (!reducer) {
+        if (threadIdx.x == 0) {
+            uint32_t st = 0u, spins = 0u;
+            while (((st = ld_agent(&ctl[1])) >> 1) != (uint32_t)(pass + 1)) {
+                if (++spins > kGridSpinLimit) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (spins > kGridSpinLimit) {
+                atomicOr(err, kGridErrStateTimeout);
+                st = 0u;
+            }
+            RED[0] = st & 1u;
+        }
+        __syncthreads();
+        const bool more = RED[0] != 0u;
+        __syncthreads();
+        return more;
+    }
+    // the reducer: every row has arrived
+    for (int w = threadIdx.x; w < nw2 + 2; w += blockDim.x) RED[w] = 0u;
+    __syncthreads();
+    {
+        const int rows = (int)G, t = (int)threadIdx.x;
+        if (nw2 <= (int)blockDim.x) {  // rows split over blockDim / nw2 thread groups per word
+            const int per = (int)blockDim.x / nw2, w = t % nw2, g0 = t / nw2;
+            if (g0 < per) {
+                uint32_t r0 = 0u, r1 = 0u, r2 = 0u, r3 = 0u;  // independent loads in flight
+                int i = g0;
+                for (; i + 3 * per < rows; i += 4 * per) {
+                    r0 |= ld_agent(&blk[(size_t)i * nw2 + w]);
+                    r1 |= ld_agent(&blk[(size_t)(i + per) * nw2 + w]);
+                    r2 |= ld_agent(&blk[(size_t)(i + 2 * per) * nw2 + w]);
+                    r3 |= ld_agent(&blk[(size_t)(i + 3 * per) * nw2 + w]);
+                }
+                for (; i < rows; i += per) r0 |= ld_agent(&blk[(size_t)i * nw2 + w]);
+                const uint32_t r = r0 | r1 | r2 | r3;
+                if (r) atomicOr(&RED[w], r);
+            }
+        } else {
+            for (int w = t; w < nw2; w += blockDim.x) {
+                uint32_t r = 0u;
+                for (int i = 0; i < rows; ++i) r |= ld_agent(&blk[(size_t)i * nw2 + w]);
+                RED[w] = r;
+            }
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        const uint32_t m = ~ld_agent(&nmask[w]), r = RED[w], z = RED[nwords + w];
+        if ((m & ~r & z) | (~m & r)) atomicOr(&RED[nw2 + 1], 1u);
+    }
+    __syncthreads();
+    const bool viol = RED[nw2 + 1] != 0u;
+    const bool more = viol && pass + 1 < max_pass;
+    if (more)
+        for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], ~RED[w]);
+    __builtin_amdgcn_s_waitcnt(0);  // the new mask words have completed before the publish
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (viol && !more) atomicOr(err, kGridErrNoConverge);
+        st_agent(&ctl[2], (uint32_t)(pass + 1));
+        st_agent(&ctl[1], ((uint32_t)(pass + 1) << 1) | (more ? 1u : 0u));
+    }
+    __syncthreads();
+    return more;
+}
+
 }  // namespace vmas

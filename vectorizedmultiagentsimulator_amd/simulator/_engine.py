@@ -62,8 +62,24 @@ class PhysicsEngine:
         self.jit_error = None
         self.kernel_name = "k_step"
         self._dev_index = -1
-        self.last_iterations = 0
+        self._last_iterations = 0
         self.steps = 0
+
+    @property
+    def last_iterations(self) -> int:
+        """Broadphase fixed-point passes of the last step.  The specialised kernel runs them on
+        the device without a host wait, so reading this waits for the step (and raises a
+        device-side fixed-point failure)."""
+        if self._last_iterations == 0 and self._jit is not None and self.steps:
+            n = ctypes.c_int32(0)
+            N.check_jit(self.lib.vmas_jit_world_passes(self._jit, ctypes.byref(n)), "vmas_jit_world_passes")
+            self._last_iterations = n.value
+        return self._last_iterations
+
+    @property
+    def jit_grid(self) -> int:
+        """Persistent grid of the specialised kernel (>0 cooperative, <0 plain launch, 0 host loop)."""
+        return self.lib.vmas_jit_world_grid(self._jit) if self._jit is not None else 0
 
     def __del__(self):
         try:
@@ -497,7 +513,7 @@ class PhysicsEngine:
         else:
             N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
                                              ctypes.byref(iters)), "vmas_world_step")
-        self.last_iterations = iters.value
+        self._last_iterations = iters.value
         self.steps += 1
         del keep
 
