@@ -247,6 +247,29 @@ typedef struct VmasActionRef {
 int32_t vmas_check_actions(int32_t device, int32_t batch, const VmasActionRef* refs,
                            int32_t n_refs, uint8_t* flags, void* stream);
 
+/* Continuous actions of Environment._set_action (environment.py:615-709) for all agents in one
+ * pass (csrc/vmas_actions.hip), the no-communication case: per agent i, flags[2*i] = any NaN
+ * in its n_cols action columns, flags[2*i+1] = any |u| > u_range in its n_phys physical columns
+ * (never when clamp != 0), and the agent's new action.u, u[b, c] = (clamp ? min(max(x, -r), r)
+ * : x) * u_mult[c], is written to out[out_offset + b*n_phys + c] (fp32).  `flags` is a HOST
+ * array, known when the call returns: the kernel publishes them to mapped pinned memory and the
+ * host waits on a sequence word, without a stream synchronisation.  Supersedes
+ * vmas_check_actions for this case (same flags, plus u, one launch). */
+typedef struct VmasActionApplyRef {
+    const float* u;       /* [B, n_cols] action tensor (any strides) */
+    const float* u_range; /* [n_phys] u_range_tensor on the same device */
+    const float* u_mult;  /* [n_phys] u_multiplier_tensor on the same device */
+    int64_t out_offset;   /* floats into out of this agent's [B, n_phys] u */
+    int32_t s0, s1;
+    int32_t n_cols;
+    int32_t n_phys;
+    int32_t clamp;
+    int32_t pad;
+} VmasActionApplyRef;
+
+int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyRef* refs,
+                           int32_t n_refs, float* out, uint8_t* flags, void* stream);
+
 /* Distance queries; out has B floats, or B bytes of 0/1 (torch.bool) for VMAS_OVERLAP_PAIR. */
 int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
                       const VmasShapeRef* b, const float* test_point, int32_t tp_s0,

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "vmas_cast_rays",
     "vmas_distance",
     "vmas_check_actions",
+    "vmas_apply_actions",
     "vmas_spawn_resolve",
     "vmas_aux_last_error",
     "vmas_jit_world_create",
@@ -248,7 +249,22 @@ ACTION_REF_DTYPE = np.dtype(
         ("pad", "<i4"),
     ]
 )
+ACTION_APPLY_REF_DTYPE = np.dtype(
+    [
+        ("u", "<u8"),
+        ("u_range", "<u8"),
+        ("u_mult", "<u8"),
+        ("out_offset", "<i8"),
+        ("s0", "<i4"),
+        ("s1", "<i4"),
+        ("n_cols", "<i4"),
+        ("n_phys", "<i4"),
+        ("clamp", "<i4"),
+        ("pad", "<i4"),
+    ]
+)
 assert ACTION_REF_DTYPE.itemsize == 40
+assert ACTION_APPLY_REF_DTYPE.itemsize == 56
 assert ENTITY_IO_DTYPE.itemsize == 72
 assert AGENT_IO_DTYPE.itemsize == 32
 assert JOINT_IO_DTYPE.itemsize == 16
@@ -295,6 +311,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     ]
     lib.vmas_check_actions.restype = _i32
     lib.vmas_check_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp]
+    lib.vmas_apply_actions.restype = _i32
+    lib.vmas_apply_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp, _vp]
     lib.vmas_distance.restype = _i32
     lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
     lib.vmas_spawn_resolve.restype = _i32

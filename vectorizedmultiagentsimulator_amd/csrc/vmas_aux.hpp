@@ -1,0 +1,26 @@
+// vmas_aux.hpp -- shared host helpers of the auxiliary entry points (vmas_spawn.hip,
+// vmas_actions.hip): the error channel behind vmas_aux_last_error and the host-side wait on a
+// word of mapped pinned memory that a kernel publishes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+namespace vmas_aux {
+
+// record the message returned by vmas_aux_last_error; returns code (vmas_spawn.hip)
+int32_t fail(int32_t code, const char* fmt, ...);
+
+// Spin until *word == seq (a kernel on `stream` stores it with system scope).  While waiting,
+// the stream is polled every few thousand reads: an error, or an idle stream without the store,
+// ends the wait with VMAS_E_HIP instead of spinning forever.
+int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream);
+
+}  // namespace vmas_aux
+
+#define VMAS_AUX_HIP(x)                                                                               \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) return vmas_aux::fail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)

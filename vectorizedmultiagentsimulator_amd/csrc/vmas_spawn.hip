@@ -22,14 +22,16 @@
 #include <mutex>
 #include <string>
 
+#include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
 
+namespace vmas_aux {
+
 namespace {
+thread_local std::string g_aux_err;
+}
 
-std::string g_aux_err;
-std::mutex g_aux_mu;
-
-int32_t aux_fail(int32_t code, const char* fmt, ...) {
+int32_t fail(int32_t code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -39,11 +41,28 @@ int32_t aux_fail(int32_t code, const char* fmt, ...) {
     return code;
 }
 
-#define AUX_HIP(x)                                                                            \
-    do {                                                                                      \
-        hipError_t e_ = (x);                                                                  \
-        if (e_ != hipSuccess) return aux_fail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
-    } while (0)
+const char* last_error() { return g_aux_err.c_str(); }
+
+int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream) {
+    for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return VMAS_OK;
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {  // the stream drained: the store must be visible by now
+                if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return VMAS_OK;
+                return fail(VMAS_E_HIP, "kernel finished without publishing its result word");
+            }
+            if (q != hipErrorNotReady) return fail(VMAS_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+}  // namespace vmas_aux
+
+namespace {
+
+std::mutex g_aux_mu;
 
 struct SpawnArgs {
     int B, n_occ, occ_s0, occ_s1, occ_s2;
@@ -111,7 +130,7 @@ DevScratch g_scratch[64];
 
 extern "C" {
 
-const char* vmas_aux_last_error(void) { return g_aux_err.c_str(); }
+const char* vmas_aux_last_error(void) { return vmas_aux::last_error(); }
 
 int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied, int32_t n_occ,
                            int32_t occ_s0, int32_t occ_s1, int32_t occ_s2, const float* candidates,
@@ -121,7 +140,7 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
     std::lock_guard<std::mutex> lk(g_aux_mu);
     if (batch <= 0 || n_occ < 0 || n_tries <= 0 || first_try < 0 || !candidates || !pos || !resolved ||
         !max_accepted || !n_unresolved || (n_occ > 0 && !occupied))
-        return aux_fail(VMAS_E_INVALID, "vmas_spawn_resolve: bad argument");
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_resolve: bad argument");
     SpawnArgs a{batch, n_occ, occ_s0, occ_s1, occ_s2, occupied, candidates, first_try, n_tries, min_dist,
                 pos, resolved};
     if (device < 0) {
@@ -135,21 +154,21 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
         *n_unresolved = un;
         return VMAS_OK;
     }
-    if (device >= 64) return aux_fail(VMAS_E_INVALID, "vmas_spawn_resolve: device %d", device);
+    if (device >= 64) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_resolve: device %d", device);
     int cur = -1;
-    AUX_HIP(hipGetDevice(&cur));
-    if (cur != device) AUX_HIP(hipSetDevice(device));
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
     DevScratch& s = g_scratch[device];
     if (!s.d_out) {
-        AUX_HIP(hipMalloc((void**)&s.d_out, 2 * sizeof(int32_t)));
-        AUX_HIP(hipHostMalloc((void**)&s.h_out, 2 * sizeof(int32_t), hipHostMallocDefault));
+        VMAS_AUX_HIP(hipMalloc((void**)&s.d_out, 2 * sizeof(int32_t)));
+        VMAS_AUX_HIP(hipHostMalloc((void**)&s.h_out, 2 * sizeof(int32_t), hipHostMallocDefault));
     }
     hipStream_t st = (hipStream_t)stream;
-    AUX_HIP(hipMemsetAsync(s.d_out, 0, 2 * sizeof(int32_t), st));
+    VMAS_AUX_HIP(hipMemsetAsync(s.d_out, 0, 2 * sizeof(int32_t), st));
     hipLaunchKernelGGL(k_spawn_resolve, dim3((batch + 255) / 256), dim3(256), 0, st, a, s.d_out);
-    AUX_HIP(hipGetLastError());
-    AUX_HIP(hipMemcpyAsync(s.h_out, s.d_out, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    AUX_HIP(hipStreamSynchronize(st));
+    VMAS_AUX_HIP(hipGetLastError());
+    VMAS_AUX_HIP(hipMemcpyAsync(s.h_out, s.d_out, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    VMAS_AUX_HIP(hipStreamSynchronize(st));
     *max_accepted = s.h_out[0];
     *n_unresolved = s.h_out[1];
     return VMAS_OK;

@@ -14,6 +14,7 @@ host backend of the same library (same arithmetic).  There is no PyTorch fallbac
 from __future__ import annotations
 
 import ctypes
+import operator
 import os
 from typing import Callable, List
 
@@ -30,16 +31,33 @@ def _f32(x) -> float:
     return float(np.float32(x))
 
 
+_SHAPE_CODES = {}  # shape type -> VMAS_* code (isinstance resolved once per type)
+
+
 def _shape_code(shape) -> int:
+    code = _SHAPE_CODES.get(type(shape))
+    if code is not None:
+        return code
     from .core import Box, Line, Sphere
 
     if isinstance(shape, Sphere):
-        return N.VMAS_SPHERE
-    if isinstance(shape, Box):
-        return N.VMAS_BOX
-    if isinstance(shape, Line):
-        return N.VMAS_LINE
-    raise RuntimeError(f"Shape {shape} currently not handled by the engine")
+        code = N.VMAS_SPHERE
+    elif isinstance(shape, Box):
+        code = N.VMAS_BOX
+    elif isinstance(shape, Line):
+        code = N.VMAS_LINE
+    else:
+        raise RuntimeError(f"Shape {shape} currently not handled by the engine")
+    _SHAPE_CODES[type(shape)] = code
+    return code
+
+
+def _shape_dims(shape, code):
+    if code == N.VMAS_SPHERE:
+        return (shape.radius,)
+    if code == N.VMAS_BOX:
+        return (shape.length, shape.width)
+    return (shape.length,)
 
 
 def _check_grad(tensors) -> None:
@@ -62,6 +80,7 @@ class PhysicsEngine:
         self.jit_error = None
         self.kernel_name = "k_step"
         self._dev_index = -1
+        self._qrefs = {}  # distance-query shape references, see _ref
         self._last_iterations = 0
         self.steps = 0
 
@@ -115,25 +134,25 @@ class PhysicsEngine:
         return t
 
     # ---- static tables ----------------------------------------------------------------------------
+    # entity attributes the static tables are built from (compared every step; any change
+    # rebuilds the tables).  Gravity enters only as "has one" (its values are read per step).
+    _ENTITY_SIG = operator.attrgetter(
+        "_shape", "_movable", "_rotatable", "_collide", "_collision_filter", "_mass", "_drag",
+        "_linear_friction", "_angular_friction", "_max_speed", "_v_range",
+    )
+    _AGENT_SIG = operator.attrgetter("_max_f", "_f_range", "_max_t", "_t_range")
+
     def _signature(self):
         w = self.world
-        ents = w.entities
         es = []
-        for e in ents:
+        for e in w.entities:
             shape = e._shape
-            es.append(
-                (
-                    id(e), id(shape), getattr(shape, "hollow", None), e._movable, e._rotatable,
-                    e._collide, id(e._collision_filter), e._mass, e._drag, e._linear_friction,
-                    e._angular_friction, e._gravity is None, e._max_speed, e._v_range,
-                    getattr(e, "_max_f", None), getattr(e, "_f_range", None),
-                    getattr(e, "_max_t", None), getattr(e, "_t_range", None),
-                )
-            )
+            es.append((e, self._ENTITY_SIG(e), getattr(shape, "hollow", None), e._gravity is None,
+                       self._AGENT_SIG(e) if hasattr(e, "_max_f") else None))
         js = []
         for j in w._joints.values():
             fr = j.fixed_rotation
-            js.append((id(j), j.dist, j.rotate, fr if not isinstance(fr, torch.Tensor) else "tensor"))
+            js.append((j, j.dist, j.rotate, fr if not isinstance(fr, torch.Tensor) else "tensor"))
         return (
             tuple(es), tuple(js), w._drag, w._linear_friction, w._angular_friction, w._x_semidim,
             w._y_semidim, w._collision_force, w._joint_force, w._torque_constraint_force,
@@ -347,17 +366,35 @@ class PhysicsEngine:
         self.agents = agents
         self.n_out = (n_lin, n_rot, n_force, n_torque)
         self._eio = np.zeros(E, dtype=N.ENTITY_IO_DTYPE)
-        self._ent_cache = None
-        self._agent_cache = None
+        self._eio_f = {k: self._eio[k] for k in N.ENTITY_IO_DTYPE.names}  # field views
+        # per entity: the state tensors last seen ([pos, vel, rot, ang_vel, gravity], identity
+        # checked every step) and the converted tensors its pointer-table row points at
+        self._ent_seen = [None] * E
+        self._ent_keep = [None] * E
+        self._agent_seen = [None] * len(agents)
+        self._agent_keep = [None] * len(agents)
         B = w.batch_dim
+        # one output buffer per step: every (B, 2) field first ([pos x n_lin | vel x n_lin |
+        # force x n_force]), then every (B, 1) field ([rot x n_rot | ang_vel x n_rot | torque x
+        # n_torque]), so two strided views + unbind give all the new state tensors
+        n2, n1 = 2 * n_lin + n_force, 2 * n_rot + n_torque
+        self._n2, self._n1 = n2, n1
+        self._out_numel = max(n2 * B * 2 + n1 * B, 1)
+        self._out_off = (0, n_lin * B * 2, n2 * B * 2, n2 * B * 2 + n_rot * B, 2 * n_lin * B * 2,
+                         n2 * B * 2 + 2 * n_rot * B)  # floats: pos, vel, rot, ang, force, torque
         self._lin_rows = np.array([index[id(e)] for e in self.lin_slots], dtype=np.int64)
         self._rot_rows = np.array([index[id(e)] for e in self.rot_slots], dtype=np.int64)
         self._lin_slot_bytes = np.arange(len(self.lin_slots), dtype=np.uint64) * np.uint64(8 * B)
         self._rot_slot_bytes = np.arange(len(self.rot_slots), dtype=np.uint64) * np.uint64(4 * B)
-        self._is_dyn = [bool(e.movable or e.rotatable) for e in ents]
+        self._lin_idx = [index[id(e)] for e in self.lin_slots]
+        self._rot_idx = [index[id(e)] for e in self.rot_slots]
         self._aio = np.zeros(max(len(agents), 1), dtype=N.AGENT_IO_DTYPE)
+        self._aio_f = {k: self._aio[k] for k in N.AGENT_IO_DTYPE.names}
         self._jio = np.zeros(max(len(joints), 1), dtype=N.JOINT_IO_DTYPE)
         self._io = N.VmasStepIO()
+        self._io.entities, self._io.agents, self._io.joints = (
+            self._eio.ctypes.data, self._aio.ctypes.data, self._jio.ctypes.data)
+        self._step_params = None
         self._sig = sig
 
     # ---- kernel timing (bench.py roofline) --------------------------------------------------------
@@ -428,56 +465,59 @@ class PhysicsEngine:
 
     # ---- the step ---------------------------------------------------------------------------------
     def _fill_entity_row(self, i, e, dev, B):
-        """(Re)read entity i's state tensors into its pointer-table row; cache them by identity."""
+        """(Re)read entity i's state tensors into its pointer-table row; remember them by identity."""
         st = e._state
-        orig = (st._pos, st._vel, st._rot, st._ang_vel, e._gravity)
+        orig = [st._pos, st._vel, st._rot, st._ang_vel, e._gravity]
         _check_grad(orig[:4])
         pos, vel, rot, ang = (self._prep(t, dev) for t in orig[:4])
-        row = self._eio[i]
+        f = self._eio_f
         ps, vs = pos.stride(), vel.stride()
-        row["pos"], row["vel"], row["rot"], row["ang"] = pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr()
-        row["pos_s0"], row["pos_s1"], row["vel_s0"], row["vel_s1"] = ps[0], ps[1], vs[0], vs[1]
-        row["rot_s0"], row["ang_s0"] = rot.stride(0), ang.stride(0)
+        f["pos"][i], f["vel"][i], f["rot"][i], f["ang"][i] = pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr()
+        f["pos_s0"][i], f["pos_s1"][i], f["vel_s0"][i], f["vel_s1"][i] = ps[0], ps[1], vs[0], vs[1]
+        f["rot_s0"][i], f["ang_s0"][i] = rot.stride(0), ang.stride(0)
         g = orig[4]
         if g is not None:
             g = self._prep(g, dev).expand(B, 2)
-            row["grav"] = g.data_ptr()
-            row["grav_s0"], row["grav_s1"] = g.stride(0), g.stride(1)
+            f["grav"][i] = g.data_ptr()
+            f["grav_s0"][i], f["grav_s1"][i] = g.stride(0), g.stride(1)
         else:
-            row["grav"] = 0
+            f["grav"][i] = 0
         # keep the converted tensors alive as long as the row points at them
-        self._ent_cache[i] = (orig, (pos, vel, rot, ang, g))
+        self._ent_seen[i] = orig
+        self._ent_keep[i] = [pos, vel, rot, ang, g]
 
     def _fill_agent_row(self, i, a, dev):
         st = a._state
-        orig = (st._force, st._torque)
-        _check_grad(orig)
-        f, t = self._prep(orig[0], dev), self._prep(orig[1], dev)
-        row = self._aio[i]
+        force, torque = st._force, st._torque
+        if force.requires_grad or torque.requires_grad:
+            _check_grad((force, torque))
+        f = force if (force.dtype is torch.float32 and force.device == dev) else self._prep(force, dev)
+        t = torque if (torque.dtype is torch.float32 and torque.device == dev) else self._prep(torque, dev)
         fs = f.stride()
-        row["force"], row["torque"] = f.data_ptr(), t.data_ptr()
-        row["force_s0"], row["force_s1"], row["torque_s0"] = fs[0], fs[1], t.stride(0)
-        self._agent_cache[i] = (orig, (f, t))
+        af = self._aio_f
+        af["force"][i], af["torque"][i] = f.data_ptr(), t.data_ptr()
+        af["force_s0"][i], af["force_s1"][i], af["torque_s0"][i] = fs[0], fs[1], t.stride(0)
+        self._agent_seen[i] = (force, torque)
+        self._agent_keep[i] = (f, t)
 
     def step(self):
         self._ensure()
         w = self.world
         dev = self._dev
         B = w.batch_dim
-        if self._ent_cache is None:
-            self._ent_cache = [None] * len(self.entities)
-            self._agent_cache = [None] * len(self.agents)
         # pointer tables: only tensors that are not the objects seen last step are re-read
+        seen = self._ent_seen
         for i, e in enumerate(self.entities):
-            c = self._ent_cache[i]
+            c = seen[i]
             st = e._state
-            if (c is None or st._pos is not c[0][0] or st._vel is not c[0][1] or st._rot is not c[0][2]
-                    or st._ang_vel is not c[0][3] or e._gravity is not c[0][4]):
+            if (c is None or st._pos is not c[0] or st._vel is not c[1] or st._rot is not c[2]
+                    or st._ang_vel is not c[3] or e._gravity is not c[4]):
                 self._fill_entity_row(i, e, dev, B)
+        aseen = self._agent_seen
         for i, a in enumerate(self.agents):
-            c = self._agent_cache[i]
+            c = aseen[i]
             st = a._state
-            if c is None or st._force is not c[0][0] or st._torque is not c[0][1]:
+            if c is None or st._force is not c[0] or st._torque is not c[1]:
                 self._fill_agent_row(i, a, dev)
         jio = self._jio
         keep = []
@@ -493,19 +533,19 @@ class PhysicsEngine:
             else:
                 jio[i]["fixed_rotation"] = 0
 
-        # one fresh output buffer: [pos | vel] x n_lin, [rot | ang_vel] x n_rot, force, torque
-        n_lin, n_rot, n_force, n_torque = self.n_out
-        sizes = (n_lin * B * 2, n_lin * B * 2, n_rot * B, n_rot * B, n_force * B * 2, n_torque * B)
-        out = torch.empty(max(sum(sizes), 1), device=dev, dtype=torch.float32)
+        # one fresh output buffer (layout: see _build)
+        out = torch.empty(self._out_numel, device=dev, dtype=torch.float32)
         base = out.data_ptr()
-        offs = np.cumsum((0,) + sizes[:-1])
+        o_pos, o_vel, o_rot, o_ang, o_force, o_torque = self._out_off
         io = self._io
-        io.entities, io.agents, io.joints = self._eio.ctypes.data, self._aio.ctypes.data, jio.ctypes.data
-        io.out_pos, io.out_vel, io.out_rot, io.out_ang_vel, io.out_force, io.out_torque = (
-            int(base + 4 * o) for o in offs)
-        io.substeps = int(w._substeps)
-        io.sub_dt = _f32(w._dt / w._substeps)
-        io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
+        io.out_pos, io.out_vel, io.out_rot = base + 4 * o_pos, base + 4 * o_vel, base + 4 * o_rot
+        io.out_ang_vel, io.out_force, io.out_torque = base + 4 * o_ang, base + 4 * o_force, base + 4 * o_torque
+        params = (w._substeps, w._dt, w.broadphase)
+        if params != self._step_params:
+            io.substeps = int(w._substeps)
+            io.sub_dt = _f32(w._dt / w._substeps)
+            io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
+            self._step_params = params
         iters = ctypes.c_int32(0)
         if self._jit is not None:
             N.check_jit(self.lib.vmas_jit_world_step(self._jit, ctypes.byref(io), self._stream(dev),
@@ -519,44 +559,41 @@ class PhysicsEngine:
 
         # re-point the integrated fields at views of the fresh buffer (new tensor objects, as the
         # reference) and update their pointer-table rows in bulk
-        eio = self._eio
+        n_lin, n_rot, n_force, n_torque = self.n_out
+        n2, n1 = self._n2, self._n1
+        two = out.as_strided((n2, B, 2), (2 * B, 2, 1)).unbind(0) if n2 else ()
+        one = out.as_strided((n1, B, 1), (B, 1, 1), 2 * B * n2).unbind(0) if n1 else ()
+        f = self._eio_f
+        ekeep = self._ent_keep
         if n_lin:
-            pv = out.narrow(0, int(offs[0]), sizes[0]).view(n_lin, B, 2).unbind(0)
-            vv = out.narrow(0, int(offs[1]), sizes[1]).view(n_lin, B, 2).unbind(0)
             rows = self._lin_rows
-            eio["pos"][rows] = np.uint64(base + 4 * int(offs[0])) + self._lin_slot_bytes
-            eio["vel"][rows] = np.uint64(base + 4 * int(offs[1])) + self._lin_slot_bytes
-            eio["pos_s0"][rows], eio["pos_s1"][rows] = 2, 1
-            eio["vel_s0"][rows], eio["vel_s1"][rows] = 2, 1
-            for k, e in enumerate(self.lin_slots):
-                st = e._state
-                st._pos, st._vel = pv[k], vv[k]
+            f["pos"][rows] = np.uint64(base + 4 * o_pos) + self._lin_slot_bytes
+            f["vel"][rows] = np.uint64(base + 4 * o_vel) + self._lin_slot_bytes
+            f["pos_s0"][rows], f["pos_s1"][rows] = 2, 1
+            f["vel_s0"][rows], f["vel_s1"][rows] = 2, 1
+            for k, i in enumerate(self._lin_idx):
+                st = self.entities[i]._state
+                p, v = two[k], two[n_lin + k]
+                st._pos, st._vel = p, v
+                c, kc = seen[i], ekeep[i]
+                c[0] = kc[0] = p
+                c[1] = kc[1] = v
         if n_rot:
-            rv = out.narrow(0, int(offs[2]), sizes[2]).view(n_rot, B, 1).unbind(0)
-            av = out.narrow(0, int(offs[3]), sizes[3]).view(n_rot, B, 1).unbind(0)
             rows = self._rot_rows
-            eio["rot"][rows] = np.uint64(base + 4 * int(offs[2])) + self._rot_slot_bytes
-            eio["ang"][rows] = np.uint64(base + 4 * int(offs[3])) + self._rot_slot_bytes
-            eio["rot_s0"][rows], eio["ang_s0"][rows] = 1, 1
-            for k, e in enumerate(self.rot_slots):
-                st = e._state
-                st._rot, st._ang_vel = rv[k], av[k]
-        for i, e in enumerate(self.entities):
-            if self._is_dyn[i]:
-                st = e._state
-                _, conv = self._ent_cache[i]
-                c = (st._pos, st._vel, st._rot, st._ang_vel, e._gravity)
-                lin, rot = e.movable, e.rotatable
-                self._ent_cache[i] = (c, (c[0] if lin else conv[0], c[1] if lin else conv[1],
-                                          c[2] if rot else conv[2], c[3] if rot else conv[3], conv[4]))
-        if n_force:
-            fv = out.narrow(0, int(offs[4]), sizes[4]).view(n_force, B, 2).unbind(0)
-            for k, a in enumerate(self.force_slots):
-                a._state._force = fv[k]
-        if n_torque:
-            tv = out.narrow(0, int(offs[5]), sizes[5]).view(n_torque, B, 1).unbind(0)
-            for k, a in enumerate(self.torque_slots):
-                a._state._torque = tv[k]
+            f["rot"][rows] = np.uint64(base + 4 * o_rot) + self._rot_slot_bytes
+            f["ang"][rows] = np.uint64(base + 4 * o_ang) + self._rot_slot_bytes
+            f["rot_s0"][rows], f["ang_s0"][rows] = 1, 1
+            for k, i in enumerate(self._rot_idx):
+                st = self.entities[i]._state
+                r, av = one[k], one[n_rot + k]
+                st._rot, st._ang_vel = r, av
+                c, kc = seen[i], ekeep[i]
+                c[2] = kc[2] = r
+                c[3] = kc[3] = av
+        for k, a in enumerate(self.force_slots):
+            a._state._force = two[2 * n_lin + k]
+        for k, a in enumerate(self.torque_slots):
+            a._state._torque = one[2 * n_rot + k]
 
     # ---- ray casting ------------------------------------------------------------------------------
     def cast_rays(self, entity, angles: torch.Tensor, max_range: float,
@@ -611,22 +648,39 @@ class PhysicsEngine:
         return out
 
     # ---- distance queries -------------------------------------------------------------------------
-    def _ref(self, e, dev, keep) -> N.VmasShapeRef:
-        r = N.VmasShapeRef()
-        r.shape = _shape_code(e.shape)
-        p = self._prep(e.state.pos, dev)
-        rot = self._prep(e.state.rot, dev)
-        _check_grad((p, rot))
-        keep += [p, rot]
-        if r.shape == N.VMAS_SPHERE:
-            r.radius = _f32(e.shape.radius)
-            r.radius_lmd = _f32(e.shape.radius + LINE_MIN_DIST)
-        else:
-            r.length = _f32(e.shape.length)
-            if r.shape == N.VMAS_BOX:
-                r.width = _f32(e.shape.width)
+    def _ref(self, e, dev, keep, slot=0) -> N.VmasShapeRef:
+        """Shape + state reference of one entity.  The shape part is cached per entity (rebuilt
+        when the shape object or its dimensions change); the state pointers are read per call."""
+        shape = e.shape
+        code = _shape_code(shape)
+        dims = _shape_dims(shape, code)
+        key = (id(e), slot)
+        c = self._qrefs.get(key)
+        if c is None or c[0] is not e or c[1] is not shape or c[2] != dims:
+            r = N.VmasShapeRef()
+            r.shape = code
+            if code == N.VMAS_SPHERE:
+                r.radius = _f32(dims[0])
+                r.radius_lmd = _f32(dims[0] + LINE_MIN_DIST)
+            else:
+                r.length = _f32(dims[0])
+                if code == N.VMAS_BOX:
+                    r.width = _f32(dims[1])
+            c = self._qrefs[key] = (e, shape, dims, r)
+        r = c[3]
+        st = e._state
+        p, rot = st._pos, st._rot
+        if p.dtype is not torch.float32 or p.device != dev:
+            p = p.to(device=dev, dtype=torch.float32)
+        if rot.dtype is not torch.float32 or rot.device != dev:
+            rot = rot.to(device=dev, dtype=torch.float32)
+        if p.requires_grad or rot.requires_grad:
+            _check_grad((p, rot))
+        keep.append(p)
+        keep.append(rot)
+        ps = p.stride()
         r.pos, r.rot = p.data_ptr(), rot.data_ptr()
-        r.pos_s0, r.pos_s1, r.rot_s0 = p.stride(0), p.stride(1), rot.stride(0)
+        r.pos_s0, r.pos_s1, r.rot_s0 = ps[0], ps[1], rot.stride(0)
         return r
 
     def _query(self, kind, a, b=None, tp=None):
@@ -634,8 +688,8 @@ class PhysicsEngine:
         dev = self._device()
         B = w.batch_dim
         keep = []
-        ra = self._ref(a, dev, keep)
-        rb = self._ref(b, dev, keep) if b is not None else None
+        ra = self._ref(a, dev, keep, 0)
+        rb = self._ref(b, dev, keep, 1) if b is not None else None
         tptr, t0, t1 = None, 0, 0
         if tp is not None:
             tp = self._prep(torch.as_tensor(tp), dev)

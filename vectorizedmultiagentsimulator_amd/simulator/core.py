@@ -1022,9 +1022,11 @@ class World(TorchVectorizedObject):
     def is_overlapping(self, entity_a: Entity, entity_b: Entity, env_index: int = None):
         self._check_batch_index(env_index)
         value = self.engine.overlap(entity_a, entity_b)
+        if env_index is None:
+            return value
         # indexed only in the sphere branches, as core.py:1931 returns get_distance(...) < 0 directly
         point_based = isinstance(entity_a.shape, Sphere) or isinstance(entity_b.shape, Sphere)
-        return value[env_index] if (env_index is not None and point_based) else value
+        return value[env_index] if point_based else value
 
     # ---- the step (core.py:1970-2014) -------------------------------------------------------------
     def step(self):

@@ -107,6 +107,7 @@ class Environment(TorchVectorizedObject):
         self.dict_spaces = dict_spaces
         self.clamp_action = clamp_actions
         self.grad_enabled = grad_enabled
+        self._apply_cache = None  # see _apply_continuous_actions
         self.terminated_truncated = terminated_truncated
         observations = self._reset(seed=seed)
         self.multidiscrete_actions = multidiscrete_actions
@@ -248,10 +249,11 @@ class Environment(TorchVectorizedObject):
                 f"Action for agent {self.agents[i].name} has shape {actions[i].shape[1]},"
                 f" but should have shape {self.get_agent_action_size(self.agents[i])}"
             )
-        if self.continuous_actions:
-            self._validate_continuous_actions(actions)
-        for i, agent in enumerate(self.agents):
-            self._set_action(actions[i], agent, validated=self.continuous_actions)
+        if not (self.continuous_actions and self._apply_continuous_actions(actions)):
+            if self.continuous_actions:
+                self._validate_continuous_actions(actions)
+            for i, agent in enumerate(self.agents):
+                self._set_action(actions[i], agent, validated=self.continuous_actions)
         for agent in self.world.agents:
             self.scenario.env_process_action(agent)
         self.scenario.pre_step()
@@ -412,10 +414,99 @@ class Environment(TorchVectorizedObject):
                 checks.append(torch.any(torch.abs(physical) > agent.action.u_range_tensor))
             flags = torch.stack(checks).tolist()
         for i, agent in enumerate(self.agents):
-            assert not flags[2 * i]
+            if flags[2 * i] or flags[2 * i + 1]:
+                # the reference's loop has set the actions of the agents before this one
+                for j in range(i):
+                    self._set_action(actions[j], self.agents[j], validated=True)
+                if flags[2 * i]:
+                    print()  # as the reference (environment.py:621-622)
+                assert not flags[2 * i]
+                assert not flags[2 * i + 1], (
+                    f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
+                )
+
+    def _apply_continuous_actions(self, actions) -> bool:
+        """_set_action of every agent in one native call (vmas_apply_actions), for continuous fp32
+        actions without communication and without autograd: the NaN / range checks, the clamp
+        and u = physical * u_multiplier of environment.py:615-709, one launch and no stream
+        synchronisation.  Agents are then processed in order exactly as the reference loop does
+        (agent i raises before its u is assigned; the agents before it keep their new u and
+        noise).  Returns False when the case does not apply (the per-agent path runs)."""
+        agents = self.agents
+        n = len(agents)
+        if n == 0:
+            return False
+        for a in actions:
+            if a.dtype is not torch.float32 or (self.grad_enabled and a.requires_grad):
+                return False
+        dev = self.device
+        B = self.num_envs
+        c = self._apply_cache
+        key = (tuple(agents), bool(self.clamp_action), B, self.world.dim_c, str(dev))
+        if c is None or c[0] != key:
+            if self.world.dim_c > 0 and any(not ag.silent for ag in agents):
+                self._apply_cache = (key, None)
+                return False
+            from ... import _native as N
+
+            refs = np.zeros(n, dtype=N.ACTION_APPLY_REF_DTYPE)
+            sizes = [ag.action_size for ag in agents]
+            offs = np.cumsum([0] + sizes[:-1]) * B
+            tensors = []
+            for i, ag in enumerate(agents):
+                r, m = ag.action.u_range_tensor, ag.action.u_multiplier_tensor
+                if r.dtype is not torch.float32 or m.dtype is not torch.float32:
+                    self._apply_cache = (key, None)
+                    return False
+                tensors.append((r, m))
+                refs[i]["u_range"], refs[i]["u_mult"] = r.data_ptr(), m.data_ptr()
+                refs[i]["out_offset"], refs[i]["n_phys"] = int(offs[i]), sizes[i]
+                refs[i]["clamp"] = int(bool(self.clamp_action))
+            if dev.type == "cuda":
+                idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            else:
+                idx = -1
+            fields = (refs["u"], refs["s0"], refs["s1"], refs["n_cols"])
+            flags = np.zeros(2 * n, dtype=np.uint8)
+            c = self._apply_cache = (key, (refs, fields, flags, tensors, sizes, sum(sizes), idx, N))
+        st = c[1]
+        if st is None:
+            return False
+        refs, (f_u, f_s0, f_s1, f_nc), flags, tensors, sizes, total, idx, N = st
+        for i, ag in enumerate(agents):  # range / multiplier tensors are cached by the Action
+            if ag.action._u_range_tensor is not tensors[i][0] or ag.action._u_multiplier_tensor is not tensors[i][1]:
+                self._apply_cache = None
+                return self._apply_continuous_actions(actions)
+        keep = []
+        for i, a in enumerate(actions):
+            if a.device != dev:
+                a = a.to(dev)
+            keep.append(a)
+            s = a.stride()
+            f_u[i], f_s0[i], f_s1[i], f_nc[i] = a.data_ptr(), s[0], s[1], a.shape[1]
+        out = torch.empty(B * total, device=dev, dtype=torch.float32)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream) if idx >= 0 else None
+        lib = N.load_library()
+        N.check_aux(lib.vmas_apply_actions(idx, B, refs.ctypes.data, n, out.data_ptr(), flags.ctypes.data, stream),
+                    "vmas_apply_actions")
+        del keep
+        k = sizes[0]
+        if all(sz == k for sz in sizes):
+            us = out.view(n, B, k).unbind(0)
+        else:
+            us = [out.narrow(0, int(o), B * sz).view(B, sz) for o, sz in zip(refs["out_offset"], sizes)]
+        for i, ag in enumerate(agents):
+            if flags[2 * i]:
+                print()  # the reference prints an empty line before this assert (environment.py:621-622)
+                assert not flags[2 * i]
             assert not flags[2 * i + 1], (
-                f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
+                f"Physical actions of agent {ag.name} are out of its range {ag.u_range}"
             )
+            ag.action.u = us[i]
+            if ag.action.u_noise > 0:
+                noise = torch.randn(*ag.action.u.shape, device=self.device, dtype=torch.float32) * ag.u_noise
+                ag.action.u += noise
+        return True
 
     def _set_action(self, action, agent, validated: bool = False):
         # The reference clones the action so that its in-place ops never touch the caller's
