@@ -44,6 +44,9 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=6, help="timed CPU-oracle steps (0 = skip)")
     p.add_argument("--cpu-envs", type=int, default=32768)
     p.add_argument("--device", default=None, help="override device (e.g. cpu for plumbing tests)")
+    p.add_argument("--graph", default="on", choices=["on", "off"],
+                   help="on: make_env(graph_step=True) -- each step replayed as one HIP graph once warm "
+                        "(same results as eager; falls back to eager if the step cannot be captured)")
     p.add_argument("--kw", default="{}", help='extra scenario kwargs as JSON, e.g. \'{"use_agent_lidar": true}\'')
     return p.parse_args()
 
@@ -53,8 +56,9 @@ def make_world_env(args, device, seed):
 
     kw = {"n_agents": args.n_agents} if args.scenario in ("balance", "transport", "discovery", "flocking") else {}
     kw.update(json.loads(args.kw))
+    graph = args.graph == "on" and str(device).startswith("cuda")
     env = make_env(args.scenario, num_envs=args.envs if device != "cpu-baseline" else args.cpu_envs,
-                   device=device if device != "cpu-baseline" else "cpu", seed=seed, **kw)
+                   device=device if device != "cpu-baseline" else "cpu", seed=seed, graph_step=graph, **kw)
     if args.substeps:
         env.world._substeps = args.substeps
         env.world._sub_dt = env.world._dt / args.substeps
@@ -150,11 +154,13 @@ def main():
             else:
                 dist.barrier()
 
+    if on_gpu:
+        world.engine.set_timing(True)
     for _ in range(args.warmup):
         env.step(env.get_random_actions())
     if on_gpu:
-        world.engine.set_timing(True)
         world.engine.get_timing(reset=True)
+        world.engine.device_timing(reset=True)
     sync()
     barrier()
     sync()
@@ -165,7 +171,15 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    kernel_ms, launches = world.engine.get_timing(reset=True) if on_gpu else (0.0, 0)
+    kernel_ms, launches, timer = 0.0, 0, None
+    if on_gpu:
+        if env.graph_status == "graph":
+            # replayed launches: HIP records no events inside a graph; the kernel's own timer
+            kernel_ms, launches = world.engine.device_timing(reset=True)
+            timer = "in-kernel s_memrealtime (workgroup 0 start -> final reduction), graph replays"
+        else:
+            kernel_ms, launches = world.engine.get_timing(reset=True)
+            timer = "HIP events on the launch's dispatch packet (hipExtModuleLaunchKernel)"
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -175,6 +189,7 @@ def main():
     value = total_envs * args.steps / elapsed
     workload = (f"{args.scenario} {args.envs} envs/GPU, n_agents={args.n_agents}, substeps={world._substeps}, "
                 f"broadphase={args.broadphase}")
+    step_mode = env.graph_status if env.graph_status != "off" else "eager"
     if json.loads(args.kw):
         workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)
@@ -195,6 +210,7 @@ def main():
             "kernel_us_per_launch": round(per_launch_ms * 1e3, 3),
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,
+            "timer": timer,
         }
         if pmc.get("valu_insts_per_launch"):
             # the bound the kernel actually meets: VALU issue, from PMC SQ_INSTS_VALU
@@ -227,6 +243,7 @@ def main():
             "n_agents": args.n_agents,
             "substeps": world._substeps,
             "parallelism": f"replicas x{world_size} (one process per GPU, no collective in the step)",
+            "step_mode": step_mode,
         },
         "roofline": roofline,
     }

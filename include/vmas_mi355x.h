@@ -203,6 +203,9 @@ int32_t vmas_abi_version(void);
 /* Number of HIP devices visible (0 if none / no driver). */
 int32_t vmas_device_count(void);
 const char* vmas_last_error(void);
+/* Ends a stream capture left open by a failed HIP-graph capture (1 if one was ended) and clears
+ * the last HIP error (graph mode's fallback to the eager step; no reference counterpart). */
+int32_t vmas_stream_abort_capture(void* stream);
 
 int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
                           const VmasPairDesc* pairs, const VmasJointDesc* joints,
@@ -321,6 +324,12 @@ int32_t vmas_jit_world_grid(const VmasJitWorld* world);
 int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
 int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
                                   int64_t* launches);
+/* Device timer (timing on; persistent batch-broadphase launches): the kernel itself accumulates,
+ * per launch, the span from workgroup 0's start to the final fixed-point reduction, after which
+ * every workgroup exits (s_memrealtime, converted with the device's wall-clock rate).  It also times launches replayed from a HIP graph, where HIP records
+ * no events.  Waits for the device.  (bench.py's roofline timer; no reference counterpart.) */
+int32_t vmas_jit_world_device_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
+                                     int64_t* launches);
 /* Generated source of a world (length returned; copied into buf when buf != NULL). */
 int32_t vmas_jit_world_source(const VmasJitWorld* world, char* buf, int64_t cap);
 /* Generate + compile a world's kernel without a device (build checks); returns the source length. */

@@ -1,0 +1,150 @@
+"""Graph mode (make_env(..., graph_step=True), simulator/environment/_graph.py): a step replayed
+from one HIP graph returns the same observations / rewards / dones / infos and leaves the same
+world state as the eager step, bit for bit, including across reset_at / reset between steps;
+scenarios whose step cannot be captured (host syncs) stay eager with the same results."""
+
+import pytest
+import torch
+
+from vectorizedmultiagentsimulator_amd import make_env
+from vectorizedmultiagentsimulator_amd.simulator.environment import Environment
+
+
+def test_graph_step_needs_gpu_device():
+    with pytest.raises(ValueError, match="ROCm"):
+        make_env("balance", num_envs=4, device="cpu", seed=0, graph_step=True)
+
+
+def _flat(tree, acc):
+    if isinstance(tree, torch.Tensor):
+        acc.append(tree)
+    elif isinstance(tree, (list, tuple)):
+        for x in tree:
+            _flat(x, acc)
+    elif isinstance(tree, dict):
+        for k in sorted(tree):
+            _flat(tree[k], acc)
+    return acc
+
+
+def _state(env):
+    out = []
+    for e in env.world.entities:
+        s = e.state
+        out += [s.pos, s.vel, s.rot, s.ang_vel]
+    return out
+
+
+def _rng_save():
+    return ([x.clone() if isinstance(x, torch.Tensor) else x for x in Environment.vmas_random_state],
+            torch.cuda.get_rng_state())
+
+
+def _rng_load(saved):
+    Environment.vmas_random_state[:] = [x.clone() if isinstance(x, torch.Tensor) else x for x in saved[0]]
+    torch.cuda.set_rng_state(saved[1])
+
+
+def _assert_same(a, b, what):
+    fa, fb = _flat(a, []), _flat(b, [])
+    assert len(fa) == len(fb), what
+    for i, (x, y) in enumerate(zip(fa, fb)):
+        assert x.shape == y.shape and x.dtype == y.dtype, (what, i)
+        assert torch.equal(x, y), (what, i, (x.float() - y.float()).abs().max().item())
+
+
+CASES = [
+    ("balance", dict(n_agents=4), 10, "graph"),
+    ("transport", dict(n_agents=4), None, "graph"),
+    ("flocking", dict(n_agents=4), None, "eager"),     # scripted agent: range assert syncs
+    ("discovery", dict(n_agents=4), None, "eager"),    # spawn sampler: rejection loop syncs
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps,expect", CASES, ids=[c[0] for c in CASES])
+def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
+    envs = []
+    for graph in (False, True):
+        saved = _rng_save()
+        env = make_env(name, num_envs=512, device=gpu_device, seed=1, graph_step=graph, **kw)
+        if substeps:
+            env.world._substeps = substeps
+            env.world._sub_dt = env.world._dt / substeps
+        envs.append(env)
+        if not graph:
+            _rng_load(saved)
+    eager, graph = envs
+    held = None
+    for t in range(14):
+        actions = eager.get_random_actions()
+        if t == 7:  # in-place edit between steps (reset_at -> set_pos(batch_index))
+            s = _rng_save()
+            eager.reset_at(3)
+            _rng_load(s)
+            graph.reset_at(3)
+        if t == 10:  # full reset re-binds every state tensor
+            s = _rng_save()
+            eager.reset()
+            _rng_load(s)
+            graph.reset()
+        s = _rng_save()  # the step itself may draw (discovery respawns its targets)
+        out_e = eager.step([a.clone() for a in actions])
+        _rng_load(s)
+        out_g = graph.step([a.clone() for a in actions])
+        _assert_same(out_e, out_g, f"{name} outputs step {t}")
+        _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
+        if t == 4:
+            held = _flat(out_g, [])[0].clone(), _flat(out_g, [])[0]
+    # returned tensors are fresh copies: a later replay does not overwrite them
+    assert torch.equal(held[0], held[1])
+    assert graph.graph_status == expect, graph.graph_reason
+    if expect == "graph":
+        assert graph._graph.replays >= 5
+
+
+@pytest.mark.gpu
+def test_graph_parameter_change_recaptures_gpu(gpu_device):
+    env = make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=True, n_agents=4)
+    for _ in range(4):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "graph"
+    env.world.agents[0].mass = 2.0  # static-table change: the graph is dropped, then re-captured
+    env.step(env.get_random_actions())
+    assert env.graph_status == "dropped"
+    for _ in range(4):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "graph"
+
+
+@pytest.mark.gpu
+def test_graph_kernel_timing_gpu(gpu_device):
+    """The in-kernel device timer counts replayed launches (HIP records no events inside a
+    graph) and agrees with HIP events on eager launches."""
+    env = make_env("balance", num_envs=32768, device=gpu_device, seed=0, graph_step=True, n_agents=4)
+    eng = env.world.engine
+    env.step(env.get_random_actions())  # builds the engine
+    eng.set_timing(True)  # before the capture: the timer pointer is a captured kernel argument
+    for _ in range(4):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "graph"
+    eng.get_timing(reset=True)
+    eng.device_timing(reset=True)
+    for _ in range(5):
+        env.step(env.get_random_actions())
+    ms, n = eng.device_timing(reset=True)
+    assert n == 5 and ms > 0
+    eager = make_env("balance", num_envs=32768, device=gpu_device, seed=0, n_agents=4)
+    eager.step(eager.get_random_actions())
+    e2 = eager.world.engine
+    e2.set_timing(True)
+    for _ in range(3):
+        eager.step(eager.get_random_actions())
+    e2.get_timing(reset=True)
+    e2.device_timing(reset=True)
+    for _ in range(5):
+        eager.step(eager.get_random_actions())
+    ev_ms, ev_n = e2.get_timing(reset=True)
+    dt_ms, dt_n = e2.device_timing(reset=True)
+    assert ev_n == dt_n == 5
+    assert 0.7 * ev_ms < dt_ms <= 1.05 * ev_ms, (ev_ms, dt_ms)

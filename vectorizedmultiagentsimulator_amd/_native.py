@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "vmas_abi_version",
     "vmas_device_count",
     "vmas_last_error",
+    "vmas_stream_abort_capture",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -67,6 +68,7 @@ EXPORTED_SYMBOLS = (
     "vmas_jit_world_step",
     "vmas_jit_world_set_timing",
     "vmas_jit_world_get_timing",
+    "vmas_jit_world_device_timing",
     "vmas_jit_world_source",
     "vmas_jit_compile_check",
     "vmas_jit_world_profile",
@@ -295,6 +297,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_abi_version.restype = _i32
     lib.vmas_device_count.restype = _i32
     lib.vmas_last_error.restype = ctypes.c_char_p
+    lib.vmas_stream_abort_capture.restype = _i32
+    lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_world_create.restype = _i32
     lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
     lib.vmas_world_destroy.restype = _i32
@@ -340,6 +344,9 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_jit_world_profile.argtypes = [_vp, _vp, ctypes.c_int64]
     lib.vmas_jit_world_passes.restype = _i32
     lib.vmas_jit_world_passes.argtypes = [_vp, ctypes.POINTER(_i32)]
+    lib.vmas_jit_world_device_timing.restype = _i32
+    lib.vmas_jit_world_device_timing.argtypes = [_vp, _i32, ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_int64)]
     lib.vmas_jit_world_grid.restype = _i32
     lib.vmas_jit_world_grid.argtypes = [_vp]
     lib.vmas_jit_last_error.restype = ctypes.c_char_p

@@ -22,5 +22,8 @@ int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream);
 #define VMAS_AUX_HIP(x)                                                                               \
     do {                                                                                              \
         hipError_t e_ = (x);                                                                          \
-        if (e_ != hipSuccess) return vmas_aux::fail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) {                                                                       \
+            (void)hipGetLastError();                                                                  \
+            return vmas_aux::fail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_));                   \
+        }                                                                                             \
     } while (0)

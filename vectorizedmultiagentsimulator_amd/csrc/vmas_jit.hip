@@ -37,6 +37,7 @@
 // the host-driven loop (one launch + reduction + host read per pass).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <hip/hip_ext.h>
 #include <dlfcn.h>
 
 #include "vmas_jit_ops.hpp"
@@ -73,7 +74,10 @@ int32_t jfail(int32_t code, const char* fmt, ...) {
 #define JHIP(x)                                                                                 \
     do {                                                                                        \
         hipError_t e_ = (x);                                                                    \
-        if (e_ != hipSuccess) return jfail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_));    \
+        if (e_ != hipSuccess) {                                                                 \
+            (void)hipGetLastError();                                                            \
+            return jfail(VMAS_E_HIP, "%s: %s", #x, hipGetErrorString(e_));                      \
+        }                                                                                       \
     } while (0)
 
 // exact fp32 literal
@@ -315,7 +319,7 @@ struct Gen {
     }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 5) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 6) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
     }
 
     // expressions for entity e as seen by wave w (registers when w owns it)
@@ -621,7 +625,7 @@ struct Gen {
         o += "// generated by vmas_jit.hip for one world\n#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
-             "    uint32_t* ctl;\n    uint32_t* err;\n"
+             "    uint32_t* ctl;\n    uint32_t* err;\n    unsigned long long* tm;\n"
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
@@ -641,8 +645,7 @@ struct Gen {
         for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
         const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
-        o += "extern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) +
-             ") k_world(Args a) {\n";
+        o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
         o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
@@ -661,6 +664,8 @@ struct Gen {
         // 64-env groups and run the passes of the broadphase fixed point without the host.
         // Otherwise one group per workgroup and one pass per launch.  DONE is back to zero at
         // the end of every substep's pair phase, so it carries over between groups.
+        o += "    const uint32_t epoch = a.ctl ? ld_agent(&a.ctl[3]) : 0u;\n";
+        o += "    if (a.ctl) device_timer_start(a.tm);\n";
         o += "    for (int pass = 0;; ++pass) {\n"
              "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "        for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
@@ -680,8 +685,12 @@ struct Gen {
              "            __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
              "        if (!a.ctl) return;\n"
              "        if (!grid_fixed_point(a.blk, a.mask, a.ctl, a.err, a.S * " + it(W) +
-             ", pass, a.max_pass, RED)) return;\n"
-             "    }\n}\n";
+             ", pass, a.max_pass, RED, epoch, a.tm)) return;\n"
+             "    }\n}\n\n";
+        o += "extern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) +
+             ") k_world(Args a) {\n"
+             "    world_body(a);\n"
+             "}\n";
     }
 };
 
@@ -831,6 +840,11 @@ struct VmasJitWorld {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
     double timed_ms = 0.0;
     long timed_launches = 0;
+    // device timer (timing on, persistent launches): [0] workgroup 0's start, [2] accumulated
+    // ticks, [4] launches -- s_memrealtime, kept by the kernel itself so that launches replayed
+    // from a HIP graph are timed too (HIP records no events inside a graph; vmas_jit_ops.hpp)
+    unsigned long long* d_tm = nullptr;
+    int wall_khz = 0;
 };
 
 extern "C" {
@@ -852,6 +866,7 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
         if (W->h_err) (void)hipHostFree(W->h_err);
         for (auto& ev : W->ev_pending) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
         for (auto& ev : W->ev_free) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+        if (W->d_tm) (void)hipFree(W->d_tm);
     }
     delete W;
     return VMAS_OK;
@@ -922,9 +937,14 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
     if (hipMalloc((void**)&W->d_ctl, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_err, 4, hipHostMallocDefault) != hipSuccess ||
-        hipMemset(W->d_err, 0, 4) != hipSuccess)
+        hipMemset(W->d_err, 0, 4) != hipSuccess ||
+        hipMemset(W->d_ctl, 0, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc fixed-point control words"));
     *W->h_err = 0u;
+    if (hipMalloc((void**)&W->d_tm, 8 * 8) != hipSuccess || hipMemset(W->d_tm, 0, 8 * 8) != hipSuccess ||
+        hipDeviceGetAttribute(&W->wall_khz, hipDeviceAttributeWallClockRate, cfg->device) != hipSuccess ||
+        W->wall_khz <= 0)
+        return cleanup(jfail(VMAS_E_HIP, "device timer (hipMalloc / wall clock rate)"));
     // Persistent grid: as many workgroups as can be resident at once (occupancy x CUs), capped
     // by the number of 64-env groups, launched as a plain launch: the workgroups of one launch on
     // an in-order stream all become resident (any other kernel holding CUs finishes without
@@ -940,6 +960,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
             per_cu > 0 && cus > 0) {
             W->grid = std::min(W->nblk, per_cu * cus);
+            if (const char* cap = getenv("VMAS_JIT_GRID_CAP")) W->grid = std::max(1, std::min(W->grid, atoi(cap)));
             W->coop = mode == "coop";
         }
     }
@@ -1049,6 +1070,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(W->d_prof);
     put_ptr(persistent ? W->d_ctl : nullptr);
     put_ptr(W->d_err);
+    put_ptr(W->timing && persistent ? W->d_tm : nullptr);
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
         int32_t v = 0;
@@ -1089,46 +1111,61 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     W->last_stream = stream;
     W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
-    if (persistent) JHIP(hipMemsetAsync(W->d_ctl, 0, (vmas::kGridCtlWords + nwords) * 4, stream));
-    else JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
-    auto timed = [&](auto&& launch) -> int32_t {
+    // (the persistent kernel resets its own control words: see grid_fixed_point)
+    if (!persistent) JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
+    // Timing (vmas_jit_world_set_timing): the events ride on the kernel's own dispatch packet
+    // (hipExtModuleLaunchKernel), so they bracket its execution alone, as rocprofv3's kernel
+    // trace does -- events recorded around a launch on an idle queue also count the dispatch gap.
+    auto ev_pair = [&](std::pair<hipEvent_t, hipEvent_t>* ev) -> int32_t {
+        if (W->ev_free.empty()) {
+            JHIP(hipEventCreate(&ev->first));
+            JHIP(hipEventCreate(&ev->second));
+        } else {
+            *ev = W->ev_free.back();
+            W->ev_free.pop_back();
+        }
+        return VMAS_OK;
+    };
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    JHIP(hipStreamIsCapturing(stream, &cap));
+    const bool capturing = cap == hipStreamCaptureStatusActive;
+    auto launch_plain = [&](int blocks) -> int32_t {
+        const uint32_t threads = (uint32_t)W->nw * 64;
+        if (!W->timing || capturing) {  // (a captured launch is timed by the device timer)
+            JHIP(hipModuleLaunchKernel(W->fn, blocks, 1, 1, threads, 1, 1, 0, stream, nullptr, extra));
+            return VMAS_OK;
+        }
         std::pair<hipEvent_t, hipEvent_t> ev{};
-        if (W->timing) {
-            if (W->ev_free.empty()) {
-                JHIP(hipEventCreate(&ev.first));
-                JHIP(hipEventCreate(&ev.second));
-            } else {
-                ev = W->ev_free.back();
-                W->ev_free.pop_back();
-            }
-            JHIP(hipEventRecord(ev.first, stream));
-        }
-        JHIP(launch());
-        if (W->timing) {
-            JHIP(hipEventRecord(ev.second, stream));
-            W->ev_pending.push_back(ev);
-        }
+        if (int32_t rc = ev_pair(&ev)) return rc;
+        JHIP(hipExtModuleLaunchKernel(W->fn, (uint32_t)blocks * threads, 1, 1, threads, 1, 1, 0, stream, nullptr,
+                                      extra, ev.first, ev.second, 0));
+        W->ev_pending.push_back(ev);
         return VMAS_OK;
     };
     if (persistent) {
         // one launch runs every pass; nothing waits on the host
-        void* params[] = {buf.data()};
-        if (int32_t rc = timed([&] {
-                return W->coop ? hipModuleLaunchCooperativeKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream,
-                                                                  params)
-                               : hipModuleLaunchKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr,
-                                                       extra);
-            }))
+        if (W->coop && capturing) return jfail(VMAS_E_INVALID, "cooperative launches are not captured into graphs");
+        if (W->coop) {
+            void* params[] = {buf.data()};
+            std::pair<hipEvent_t, hipEvent_t> ev{};
+            if (W->timing) {
+                if (int32_t rc = ev_pair(&ev)) return rc;
+                JHIP(hipEventRecord(ev.first, stream));
+            }
+            JHIP(hipModuleLaunchCooperativeKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream, params));
+            if (W->timing) {
+                JHIP(hipEventRecord(ev.second, stream));
+                W->ev_pending.push_back(ev);
+            }
+        } else if (int32_t rc = launch_plain(W->grid)) {
             return rc;
+        }
         JHIP(hipMemcpyAsync(W->h_err, W->d_err, 4, hipMemcpyDeviceToHost, stream));
         if (iterations) *iterations = 0;  // not known without a sync: vmas_jit_world_passes
         return VMAS_OK;
     }
     for (int it = 0; it < max_it; ++it) {
-        if (int32_t rc = timed([&] {
-                return hipModuleLaunchKernel(W->fn, W->nblk, 1, 1, W->nw * 64, 1, 1, 0, stream, nullptr, extra);
-            }))
-            return rc;
+        if (int32_t rc = launch_plain(W->nblk)) return rc;
         W->last_passes = it + 1;
         if (iterations) *iterations = it + 1;
         if (!batch_bp) return VMAS_OK;
@@ -1170,6 +1207,20 @@ int32_t vmas_jit_world_grid(const VmasJitWorld* W) {
 int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
     W->timing = enable != 0;
+    return VMAS_OK;
+}
+
+// Device timer totals (timing on): every launch -- eager or replayed from a HIP graph -- adds
+// (latest workgroup end - earliest workgroup start) in s_memrealtime ticks.  Waits for the device.
+int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    JHIP(hipSetDevice(W->cfg.device));
+    JHIP(hipDeviceSynchronize());
+    unsigned long long tm[5] = {0, 0, 0, 0, 0};
+    JHIP(hipMemcpy(tm, W->d_tm, sizeof tm, hipMemcpyDeviceToHost));
+    if (total_ms) *total_ms = (double)tm[2] / (double)W->wall_khz;
+    if (launches) *launches = (int64_t)tm[4];
+    if (reset) JHIP(hipMemset(W->d_tm, 0, 8 * 8));
     return VMAS_OK;
 }
 

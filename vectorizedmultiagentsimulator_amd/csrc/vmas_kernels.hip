@@ -47,9 +47,11 @@ static int32_t fail(int32_t code, const char* fmt, ...) {
 #define HIP_TRY(x)                                                                        \
     do {                                                                                  \
         hipError_t e_ = (x);                                                              \
-        if (e_ != hipSuccess)                                                             \
+        if (e_ != hipSuccess) {                                                           \
+            (void)hipGetLastError(); /* not left for the caller's next launch check */    \
             return fail(VMAS_E_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
                         __FILE__, __LINE__);                                              \
+        }                                                                                 \
     } while (0)
 
 // ------------------------------------------------------------------------------------------------
@@ -136,6 +138,9 @@ namespace {
 constexpr size_t kSlot = 16384;   // bytes per slot
 constexpr int kSlots = 256;
 constexpr int kSegs = 8;          // kSlots / kSegs slots per segment
+// Uploads issued while the stream is being captured into a HIP graph get a slot of their own that
+// is never recycled: the captured memcpy node re-reads its pinned source at every replay.
+constexpr int kFrozen = 128;
 struct Ring {
     int device = -1;
     char* host = nullptr;
@@ -143,6 +148,9 @@ struct Ring {
     hipEvent_t ev[kSegs];
     bool ev_live[kSegs] = {};
     int next = 0;
+    char* frozen_host = nullptr;
+    char* frozen_dev = nullptr;
+    int frozen_next = 0;
 };
 std::mutex g_ring_mu;
 std::vector<Ring*> g_rings;
@@ -159,7 +167,20 @@ int32_t ring_upload(int device, const void* src, size_t n, hipStream_t stream, c
         HIP_TRY(hipHostMalloc((void**)&r->host, kSlot * kSlots, hipHostMallocDefault));
         HIP_TRY(hipMalloc((void**)&r->dev, kSlot * kSlots));
         for (int i = 0; i < kSegs; ++i) HIP_TRY(hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc((void**)&r->frozen_host, kSlot * kFrozen, hipHostMallocDefault));
+        HIP_TRY(hipMalloc((void**)&r->frozen_dev, kSlot * kFrozen));
         g_rings.push_back(r);
+    }
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(stream, &cap));
+    if (cap == hipStreamCaptureStatusActive) {
+        if (!r->frozen_host) return fail(VMAS_E_HIP, "graph-capture staging slots not allocated");
+        if (r->frozen_next >= kFrozen) return fail(VMAS_E_NOMEM, "graph-capture staging slots exhausted (%d)", kFrozen);
+        const size_t off = (size_t)r->frozen_next++ * kSlot;
+        memcpy(r->frozen_host + off, src, n);
+        HIP_TRY(hipMemcpyAsync(r->frozen_dev + off, r->frozen_host + off, n, hipMemcpyHostToDevice, stream));
+        *out = r->frozen_dev + off;
+        return VMAS_OK;
     }
     const int per = kSlots / kSegs;
     const int slot = r->next;
@@ -1010,6 +1031,26 @@ int32_t vmas_device_count(void) {
 }
 
 const char* vmas_last_error(void) { return g_err.c_str(); }
+
+// Ends a stream capture that a failed capture left open (returns 1 if one was ended, 0 if none)
+// and clears the thread's last HIP error, so that the eager step that follows can launch.
+int32_t vmas_stream_abort_capture(void* stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    int32_t ended = 0;
+    if (st != hipStreamCaptureStatusNone) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        ended = 1;
+    }
+    (void)hipGetLastError();
+    return ended;
+}
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

@@ -23,6 +23,7 @@ def make_env(
     grad_enabled: bool = False,
     terminated_truncated: bool = False,
     wrapper_kwargs: Optional[dict] = None,
+    graph_step: bool = False,
     **kwargs,
 ):
     """Create a vectorized environment.
@@ -30,6 +31,8 @@ def make_env(
     Same arguments as the reference's ``vmas.make_env``.  ``device`` may be ``"cpu"`` (host
     backend of the native engine) or a ROCm device such as ``"cuda"`` / ``"cuda:0"`` (gfx950
     kernels).  ``scenario`` is a scenario file name from ``scenarios/`` or a BaseScenario.
+    ``graph_step=True`` (ROCm devices; not in the reference) replays each step as one HIP graph
+    once the world is warm, with the same results (simulator/environment/_graph.py).
     """
     if isinstance(scenario, str):
         if not scenario.endswith(".py"):
@@ -47,6 +50,7 @@ def make_env(
         clamp_actions=clamp_actions,
         grad_enabled=grad_enabled,
         terminated_truncated=terminated_truncated,
+        graph_step=graph_step,
         **kwargs,
     )
     if wrapper is not None and isinstance(wrapper, str):

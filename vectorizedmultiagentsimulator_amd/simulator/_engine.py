@@ -409,6 +409,22 @@ class PhysicsEngine:
         if self._jit is not None:
             N.check_jit(self.lib.vmas_jit_world_set_timing(self._jit, on), "vmas_jit_world_set_timing")
 
+    def device_timing(self, reset: bool = True):
+        """(milliseconds, launches) of the specialised step kernel from its in-kernel device timer
+        (vmas_jit_world_device_timing): the timer of launches replayed from a HIP graph."""
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        if self._jit is not None:
+            N.check_jit(self.lib.vmas_jit_world_device_timing(self._jit, int(reset), ctypes.byref(ms),
+                                                              ctypes.byref(n)), "vmas_jit_world_device_timing")
+        return ms.value, n.value
+
+    def graph_token(self):
+        """What a captured step depends on besides tensor contents: the static tables (entity /
+        joint / world parameters), the kernel object and the step parameters."""
+        w = self.world
+        return (self._signature(), int(w._substeps), w._dt, w.broadphase, id(self._jit), id(self._handle))
+
     def get_timing(self, reset: bool = True):
         """(milliseconds, launches) of the step kernel (k_world or k_step) since the last reset."""
         ms = ctypes.c_double(0.0)

@@ -1,0 +1,340 @@
+"""HIP-graph replay of ``Environment.step`` (opt-in: ``make_env(..., graph_step=True)``).
+
+The reference's step is an eager tensor program: per step ~70 small kernels for balance
+(scenario rewards / observations / dones around the physics launch), each launched from Python.
+On the MI355X that host work, not the GPU, sets the step time.  Once a world is warm this module
+captures everything after the action check -- ``env_process_action``, ``pre_step``,
+``World.step`` (the k_world launch and its fixed-point control words), ``post_step``, the step
+counter and the scenario's rewards / observations / infos / dones -- into ONE HIP graph
+(``torch.cuda.CUDAGraph``: stream capture, hipGraphInstantiate, hipGraphLaunch) and replays it.
+
+What a replay must honour, and how:
+  * Actions.  The native action kernel (one launch, one host wait for the NaN / range flags, as
+    the reference's asserts) runs eagerly before the replay and writes every agent's ``u`` into
+    ONE persistent buffer, so the captured program reads the current actions.
+  * State carried across steps by re-binding.  The reference creates new tensors every step
+    (integration, core.py:2866-2907; scenario attributes such as balance's ``global_shaping``).
+    A captured program reads the tensors that were bound when it was captured (X) and writes
+    tensors of the graph pool (Y).  At capture the attributes of the simulator's objects (env,
+    scenario, world, entities, entity states, agent actions, joint constraints) are diffed:
+    every attribute re-bound from X to Y is a carried tensor, and before each replay its current
+    value is copied Y -> X (one multi-tensor copy, grouped by storage: the engine's whole output
+    buffer is one copy).
+  * Changes made between steps.  In-place edits of Y (``reset_at`` -> ``set_pos(batch_index)``)
+    travel with that copy.  A tracked attribute re-bound by the caller (``reset()``, ``set_pos``
+    without an index) is copied into the captured tensor and the attribute pointed back at it.
+    Entity / world parameter changes (mass, shape, substeps, ...) drop the graph; the next step
+    runs eagerly and captures again.
+  * Outputs.  The returned observations / rewards / dones / infos are fresh copies (the
+    reference clones them too), made by one multi-tensor copy per dtype after the replay.
+  * What cannot be captured -- a host sync inside the step (``.item()``, ``bool(t.any())``,
+    the spawn sampler's rejection loop, a scripted agent's range assert), a host-to-device copy
+    of pageable memory, discrete or communication actions -- makes the capture fail; the
+    simulator's objects are rolled back (nothing ran: capture only records) and the env stays
+    eager.  ``env.graph_status`` says which.
+  * Not detectable, so a documented requirement of graph mode: per-step Python state that feeds
+    kernel arguments (a Python-int step counter multiplied into a tensor, numpy random numbers
+    drawn inside the step) is frozen at its capture-time value.  The benchmark scenarios keep
+    all per-step state in device tensors; tests/test_graph.py checks replay == eager bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+WARM_STEPS = 2  # eager steps before the capture (JIT compile, engine tables, allocator warm)
+
+
+def _tracked_objects(env) -> List[Any]:
+    w = env.world
+    objs = [env, env.scenario, w]
+    for e in w.entities:
+        objs.append(e)
+        objs.append(e._state)
+        a = getattr(e, "_action", None)
+        if a is not None:
+            objs.append(a)
+    for jc in w._joints.values():
+        objs.append(jc)
+    seen = set()
+    out = []
+    for o in objs:
+        if id(o) not in seen and hasattr(o, "__dict__"):
+            seen.add(id(o))
+            out.append(o)
+    return out
+
+
+def _tensors(tree, acc: List[Tensor]):
+    if isinstance(tree, Tensor):
+        acc.append(tree)
+    elif isinstance(tree, (list, tuple)):
+        for x in tree:
+            _tensors(x, acc)
+    elif isinstance(tree, dict):
+        for x in tree.values():
+            _tensors(x, acc)
+    return acc
+
+
+def _rebuild(tree, it):
+    if isinstance(tree, Tensor):
+        return next(it)
+    if isinstance(tree, list):
+        return [_rebuild(x, it) for x in tree]
+    if isinstance(tree, tuple):
+        return tuple(_rebuild(x, it) for x in tree)
+    if isinstance(tree, dict):
+        return {k: _rebuild(v, it) for k, v in tree.items()}
+    return tree
+
+
+class _CapturableConstants:
+    """While a step is captured: ``torch.tensor(data, device=<gpu>)`` / ``torch.as_tensor`` of
+    host data (scenario constants such as transport's colour vectors, built every step) would be
+    a pageable host->device copy, which stream capture forbids.  They are built on the host,
+    written into a pinned arena allocated before the capture, and copied with a captured memcpy
+    from there; the arena lives as long as the graph, so every replay copies the same values."""
+
+    ARENA_BYTES = 1 << 16
+
+    def __init__(self):
+        self.arena = torch.empty(self.ARENA_BYTES, dtype=torch.uint8).pin_memory()
+        self.used = 0
+
+    def _wrap(self, orig):
+        def fn(data, *args, dtype=None, device=None, **kw):
+            if device is not None and not isinstance(data, Tensor) and torch.device(device).type == "cuda" \
+                    and not args and not kw.get("requires_grad", False):
+                host = orig(data, dtype=dtype)
+                n = host.numel() * host.element_size()
+                start = (self.used + 15) & ~15
+                if start + n > self.ARENA_BYTES:
+                    raise GraphUnsupported("too many host constants in the captured step")
+                self.used = start + n
+                slot = self.arena[start: start + n].view(host.dtype).view(host.shape)
+                slot.copy_(host)
+                out = torch.empty(host.shape, dtype=host.dtype, device=device)
+                out.copy_(slot, non_blocking=True)
+                return out
+            return orig(data, *args, dtype=dtype, device=device, **kw)
+
+        return fn
+
+    def __enter__(self):
+        self.saved = (torch.tensor, torch.as_tensor)
+        torch.tensor = self._wrap(self.saved[0])
+        torch.as_tensor = self._wrap(self.saved[1])
+        return self
+
+    def __exit__(self, *exc):
+        torch.tensor, torch.as_tensor = self.saved
+        return False
+
+
+def _storage_key(t: Tensor) -> int:
+    return t.untyped_storage().data_ptr()
+
+
+class GraphUnsupported(RuntimeError):
+    pass
+
+
+class StepGraph:
+    """Capture / replay state of one Environment (see the module docstring)."""
+
+    def __init__(self, env):
+        self.env = env
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.status = "warming"
+        self.eager_steps = 0
+        self.replays = 0
+        self._out_tree = None
+        self._out_tensors: List[Tensor] = []
+        self._carry_dst: List[Tensor] = []  # X (read by the graph)
+        self._carry_src: List[Tensor] = []  # Y (written by the graph)
+        self._watch: List[Tuple[dict, str, Tensor]] = []  # (obj.__dict__, key, bound tensor)
+        self._first_replay = True
+
+    # ---- the step -------------------------------------------------------------------------------
+    def body(self):
+        """Everything of Environment.step after the actions (environment.py:394-412)."""
+        env = self.env
+        for agent in env.world.agents:
+            env.scenario.env_process_action(agent)
+        env.scenario.pre_step()
+        env.world.step()
+        env.scenario.post_step()
+        env.steps += 1
+        return env._get_from_scenario(get_observations=True, get_infos=True, get_rewards=True, get_dones=True)
+
+    def before_actions(self):
+        """Bring the tensors a replay reads up to date, BEFORE the step's actions are applied (as
+        the eager step orders it): tensors re-bound by the caller are copied into the captured
+        ones, carried state is copied forward.  (A tracked tensor may alias the action buffer --
+        a holonomic agent's force is a view of u -- so the fresh actions must land last.)"""
+        if self.graph is None:
+            return
+        if not self._still_valid():
+            self.drop("world or entity parameters changed")
+            return
+        for d, k, t in self._watch:
+            cur = d.get(k, None)
+            if cur is not t:
+                if not isinstance(cur, Tensor) or cur.shape != t.shape or cur.dtype != t.dtype:
+                    self.drop(f"attribute {k} re-bound to a tensor of another shape")
+                    return
+                with torch.no_grad():
+                    t.copy_(cur)
+                d[k] = t
+        if not self._first_replay and self._carry_dst:
+            with torch.no_grad():
+                torch._foreach_copy_(self._carry_dst, self._carry_src)
+
+    def step(self):
+        """Run the post-action part of a step (actions already applied; before_actions ran before
+        them); returns its results."""
+        if self.graph is None:
+            if self.status in ("warming", "dropped") and self.eager_steps >= WARM_STEPS:
+                if self._capture():
+                    return self._replay()
+            self.eager_steps += 1
+            return self.body()
+        return self._replay()
+
+    def drop(self, why: str):
+        self.graph = None
+        self.status = "dropped"
+        self.why = why
+        self.eager_steps = 0
+        self._out_tree = None
+        self._out_tensors = []
+        self._carry_dst, self._carry_src, self._watch = [], [], []
+
+    # ---- capture --------------------------------------------------------------------------------
+    def _capture(self) -> bool:
+        env = self.env
+        eng = env.world.engine
+        objs = _tracked_objects(env)
+        snap = [(o, dict(o.__dict__)) for o in objs]
+        dev = env.device
+        rng = torch.cuda.get_rng_state(dev)
+        g = torch.cuda.CUDAGraph()
+        consts = _CapturableConstants()
+        side = torch.cuda.Stream(dev)
+        env._raw_outputs = True
+        try:
+            with torch.cuda.graph(g, stream=side), consts:
+                out = self.body()
+            self._consts = consts
+            self._sig = eng.graph_token()
+            self._plan(objs, snap, out)
+        except Exception as ex:  # noqa: BLE001 -- any capture failure means "stay eager"
+            from ... import _native as N
+
+            # a capture invalidated by a forbidden call may be left open: end it, so that the
+            # eager step that follows can launch
+            N.load_library().vmas_stream_abort_capture(ctypes.c_void_p(side.cuda_stream))
+            torch.cuda.synchronize(dev)
+            for o, d in snap:
+                o.__dict__.clear()
+                o.__dict__.update(d)
+            torch.cuda.set_rng_state(rng, dev)
+            self.status = "eager"
+            self.why = f"{type(ex).__name__}: {str(ex).splitlines()[0] if str(ex) else ''}"[:300]
+            self.graph = None
+            return False
+        finally:
+            env._raw_outputs = False
+        self.graph = g
+        self.status = "graph"
+        self.why = ""
+        self._first_replay = True
+        return True
+
+    def _plan(self, objs, snap, out):
+        carry: List[Tuple[Tensor, Tensor]] = []
+        names: List[str] = []
+        for o, before in snap:
+            after = o.__dict__
+            for k, v0 in before.items():
+                if not isinstance(v0, Tensor):
+                    continue
+                v1 = after.get(k, None)
+                if v1 is v0:
+                    continue
+                if not isinstance(v1, Tensor) or v1.shape != v0.shape or v1.dtype != v0.dtype \
+                        or v1.device != v0.device:
+                    raise GraphUnsupported(f"attribute {type(o).__name__}.{k} changes type/shape in the step")
+                if (_storage_key(v1) == _storage_key(v0) and v1.storage_offset() == v0.storage_offset()
+                        and v1.stride() == v0.stride()):
+                    continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
+                carry.append((v0, v1))
+                names.append(f"{type(o).__name__}.{k}")
+        x_keys = {_storage_key(x): n for (x, _), n in zip(carry, names)}
+        for (_, y), n in zip(carry, names):
+            if _storage_key(y) in x_keys:
+                raise GraphUnsupported(f"{n} is re-bound onto the storage that {x_keys[_storage_key(y)]} held "
+                                       "before the step")
+        # group carried pairs by (X storage, Y storage): same offsets / strides / storage size ->
+        # one whole-storage copy (the engine's output buffer: every dynamic field at once)
+        groups: Dict[Tuple[int, int], List[Tuple[Tensor, Tensor]]] = {}
+        for x, y in carry:
+            groups.setdefault((_storage_key(x), _storage_key(y)), []).append((x, y))
+        dst, src = [], []
+        for (_, _), pairs in groups.items():
+            x0, y0 = pairs[0]
+            sx, sy = x0.untyped_storage(), y0.untyped_storage()
+            whole = (len(pairs) > 1 and sx.nbytes() == sy.nbytes()
+                     and all(x.storage_offset() == y.storage_offset() and x.stride() == y.stride()
+                             for x, y in pairs))
+            if whole:
+                dst.append(torch.empty(0, dtype=torch.uint8, device=x0.device).set_(sx))
+                src.append(torch.empty(0, dtype=torch.uint8, device=y0.device).set_(sy))
+            else:
+                for x, y in pairs:
+                    dst.append(x)
+                    src.append(y)
+        self._carry_dst, self._carry_src = dst, src
+        # every tensor attribute of the tracked objects as bound after the capture: the caller
+        # re-binding one of them between steps is detected by identity
+        self._watch = []
+        for o in objs:
+            d = o.__dict__
+            for k, v in d.items():
+                if isinstance(v, Tensor):
+                    self._watch.append((d, k, v))
+        self._out_tree = out
+        self._out_tensors = _tensors(out, [])
+
+    def _still_valid(self) -> bool:
+        return self.env.world.engine.graph_token() == self._sig
+
+    # ---- replay ---------------------------------------------------------------------------------
+    def _replay(self):
+        self._first_replay = False
+        self.graph.replay()
+        self.replays += 1
+        return self._clone_outputs()
+
+    def _clone_outputs(self):
+        ts = self._out_tensors
+        by_dtype: Dict[torch.dtype, List[int]] = {}
+        for i, t in enumerate(ts):
+            by_dtype.setdefault(t.dtype, []).append(i)
+        fresh: List[Optional[Tensor]] = [None] * len(ts)
+        for dt, idx in by_dtype.items():
+            total = sum(ts[i].numel() for i in idx)
+            flat = torch.empty(total, dtype=dt, device=ts[idx[0]].device)
+            views, off = [], 0
+            for i in idx:
+                n = ts[i].numel()
+                v = flat[off: off + n].view(ts[i].shape)
+                off += n
+                fresh[i] = v
+                views.append(v)
+            torch._foreach_copy_(views, [ts[i] for i in idx])
+        return _rebuild(self._out_tree, iter(fresh))

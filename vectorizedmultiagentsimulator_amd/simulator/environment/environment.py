@@ -90,6 +90,7 @@ class Environment(TorchVectorizedObject):
         clamp_actions: bool = False,
         grad_enabled: bool = False,
         terminated_truncated: bool = False,
+        graph_step: bool = False,
         **kwargs,
     ):
         if multidiscrete_actions:
@@ -108,11 +109,20 @@ class Environment(TorchVectorizedObject):
         self.clamp_action = clamp_actions
         self.grad_enabled = grad_enabled
         self._apply_cache = None  # see _apply_continuous_actions
+        self._u_persist = None  # persistent action buffer of graph mode (see _apply_continuous_actions)
+        self._raw_outputs = False  # set while a step is captured (outputs are cloned after replay)
         self.terminated_truncated = terminated_truncated
         observations = self._reset(seed=seed)
         self.multidiscrete_actions = multidiscrete_actions
         self.action_space = self.get_action_space()
         self.observation_space = self.get_observation_space(observations)
+        self._graph = None
+        if graph_step:
+            if self.device.type != "cuda":
+                raise ValueError("graph_step=True needs a ROCm device (HIP graphs)")
+            from ._graph import StepGraph
+
+            self._graph = StepGraph(self)
         self.viewer = None
         self.headless = None
         self.visible_display = None
@@ -178,23 +188,26 @@ class Environment(TorchVectorizedObject):
         if get_infos:
             infos = {} if dict_agent_names else []
         # order matters: rewards may mutate state that observations read (discovery.py:180-210)
+        keep = (lambda v: v) if self._raw_outputs else _owned_or_clone
         if get_rewards:
             for agent in self.agents:
-                reward = _owned_or_clone(self.scenario.reward(agent))
+                reward = keep(self.scenario.reward(agent))
                 if dict_agent_names:
                     rewards.update({agent.name: reward})
                 else:
                     rewards.append(reward)
         if get_observations:
             for agent in self.agents:
-                observation = _owned_or_clone(self.scenario.observation(agent))
+                observation = keep(self.scenario.observation(agent))
                 if dict_agent_names:
                     obs.update({agent.name: observation})
                 else:
                     obs.append(observation)
         if get_infos:
             for agent in self.agents:
-                info = TorchUtils.recursive_clone(self.scenario.info(agent))
+                info = self.scenario.info(agent)
+                if not self._raw_outputs:
+                    info = TorchUtils.recursive_clone(info)
                 if dict_agent_names:
                     infos.update({agent.name: info})
                 else:
@@ -249,6 +262,10 @@ class Environment(TorchVectorizedObject):
                 f"Action for agent {self.agents[i].name} has shape {actions[i].shape[1]},"
                 f" but should have shape {self.get_agent_action_size(self.agents[i])}"
             )
+        if self._graph is not None and self.continuous_actions:
+            self._graph.before_actions()
+            if self._apply_continuous_actions(actions, persistent=True):
+                return self._graph.step()
         if not (self.continuous_actions and self._apply_continuous_actions(actions)):
             if self.continuous_actions:
                 self._validate_continuous_actions(actions)
@@ -425,7 +442,18 @@ class Environment(TorchVectorizedObject):
                     f"Physical actions of agent {agent.name} are out of its range {agent.u_range}"
                 )
 
-    def _apply_continuous_actions(self, actions) -> bool:
+    @property
+    def graph_status(self) -> str:
+        """Graph mode (graph_step=True): "warming" (eager steps before the capture), "graph"
+        (replaying), "eager" (the step could not be captured; see graph_reason), "dropped"
+        (parameters changed: eager, capturing again); "off" without graph mode."""
+        return "off" if self._graph is None else self._graph.status
+
+    @property
+    def graph_reason(self) -> str:
+        return "" if self._graph is None else getattr(self._graph, "why", "")
+
+    def _apply_continuous_actions(self, actions, persistent: bool = False) -> bool:
         """_set_action of every agent in one native call (vmas_apply_actions), for continuous fp32
         actions without communication and without autograd: the NaN / range checks, the clamp
         and u = physical * u_multiplier of environment.py:615-709, one launch and no stream
@@ -484,17 +512,27 @@ class Environment(TorchVectorizedObject):
             keep.append(a)
             s = a.stride()
             f_u[i], f_s0[i], f_s1[i], f_nc[i] = a.data_ptr(), s[0], s[1], a.shape[1]
-        out = torch.empty(B * total, device=dev, dtype=torch.float32)
+        if persistent:  # graph mode: every step writes the same buffer / the same u views
+            pc = self._u_persist
+            if pc is None or pc[0] is not c:
+                pc = self._u_persist = (c, torch.empty(B * total, device=dev, dtype=torch.float32), None)
+            out = pc[1]
+        else:
+            out = torch.empty(B * total, device=dev, dtype=torch.float32)
         stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream) if idx >= 0 else None
         lib = N.load_library()
         N.check_aux(lib.vmas_apply_actions(idx, B, refs.ctypes.data, n, out.data_ptr(), flags.ctypes.data, stream),
                     "vmas_apply_actions")
         del keep
         k = sizes[0]
-        if all(sz == k for sz in sizes):
+        if persistent and self._u_persist[2] is not None:
+            us = self._u_persist[2]
+        elif all(sz == k for sz in sizes):
             us = out.view(n, B, k).unbind(0)
         else:
             us = [out.narrow(0, int(o), B * sz).view(B, sz) for o, sz in zip(refs["out_offset"], sizes)]
+        if persistent and self._u_persist[2] is None:
+            self._u_persist = (self._u_persist[0], out, us)
         for i, ag in enumerate(agents):
             if flags[2 * i]:
                 print()  # the reference prints an empty line before this assert (environment.py:621-622)
