@@ -171,11 +171,13 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    kernel_ms, launches, timer = 0.0, 0, None
+    kernel_ms, launches, timer, clock_ghz = 0.0, 0, None, 0.0
     if on_gpu:
+        dev_ms, dev_n, clock_ghz = world.engine.device_timing(reset=True, with_clock=True)
         if env.graph_status == "graph":
             # replayed launches: HIP records no events inside a graph; the kernel's own timer
-            kernel_ms, launches = world.engine.device_timing(reset=True)
+            kernel_ms, launches = dev_ms, dev_n
+            world.engine.get_timing(reset=True)
             timer = "in-kernel s_memrealtime (workgroup 0 start -> final reduction), graph replays"
         else:
             kernel_ms, launches = world.engine.get_timing(reset=True)
@@ -222,6 +224,12 @@ def main():
                 "frac": round(rate / VALU_PEAK_WAVE_INSTS, 4),
                 "valu_insts_per_launch": round(pmc["valu_insts_per_launch"]),
             }
+            if clock_ghz > 0:
+                # the same peak at the shader clock the chip held inside the kernel (in-kernel
+                # s_memtime / s_memrealtime): DVFS lowers it well below 2.4 GHz under this load
+                peak_at_clock = 256 * 4 * 0.5 * clock_ghz * 1e9
+                roofline["valu_issue"]["clock_ghz"] = round(clock_ghz, 3)
+                roofline["valu_issue"]["frac_at_clock"] = round(rate / peak_at_clock, 4)
     out = {
         "metric": "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU",
         "value": round(value, 1),

@@ -206,6 +206,10 @@ const char* vmas_last_error(void);
 /* Ends a stream capture left open by a failed HIP-graph capture (1 if one was ended) and clears
  * the last HIP error (graph mode's fallback to the eager step; no reference counterpart). */
 int32_t vmas_stream_abort_capture(void* stream);
+/* Host waits on the device performed by the library so far (stream / event synchronisations and
+ * spins on published words; wraps around): graph mode runs one step between two reads of it to
+ * tell whether the step can be captured (no reference counterpart). */
+int32_t vmas_host_waits(void);
 
 int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
                           const VmasPairDesc* pairs, const VmasJointDesc* joints,
@@ -316,6 +320,9 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* world);
  * vmas_jit_world_passes and by the next vmas_jit_world_step. */
 int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
                             int32_t* iterations);
+/* Error bits the kernel has reported so far, without waiting (VMAS_OK if none): how a launch
+ * replayed from a HIP graph surfaces a device-side fixed-point failure. */
+int32_t vmas_jit_world_check(VmasJitWorld* world);
 /* Fixed-point passes of the last step (waits for it on its stream). */
 int32_t vmas_jit_world_passes(VmasJitWorld* world, int32_t* passes);
 /* Persistent grid size: > 0 cooperative launch, < 0 plain launch, 0 host-driven passes
@@ -326,10 +333,11 @@ int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* to
                                   int64_t* launches);
 /* Device timer (timing on; persistent batch-broadphase launches): the kernel itself accumulates,
  * per launch, the span from workgroup 0's start to the final fixed-point reduction, after which
- * every workgroup exits (s_memrealtime, converted with the device's wall-clock rate).  It also times launches replayed from a HIP graph, where HIP records
+ * every workgroup exits (s_memrealtime, converted with the device's wall-clock rate);
+ * *clock_ghz (may be NULL) is the in-kernel shader clock (s_memtime / s_memrealtime spans).  It also times launches replayed from a HIP graph, where HIP records
  * no events.  Waits for the device.  (bench.py's roofline timer; no reference counterpart.) */
 int32_t vmas_jit_world_device_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
-                                     int64_t* launches);
+                                     int64_t* launches, double* clock_ghz);
 /* Generated source of a world (length returned; copied into buf when buf != NULL). */
 int32_t vmas_jit_world_source(const VmasJitWorld* world, char* buf, int64_t cap);
 /* Generate + compile a world's kernel without a device (build checks); returns the source length. */

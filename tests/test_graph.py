@@ -148,3 +148,12 @@ def test_graph_kernel_timing_gpu(gpu_device):
     dt_ms, dt_n = e2.device_timing(reset=True)
     assert ev_n == dt_n == 5
     assert 0.7 * ev_ms < dt_ms <= 1.05 * ev_ms, (ev_ms, dt_ms)
+
+
+def test_trial_step_detects_host_waits():
+    """The native host-wait counter moves on a synchronising call (CPU: the host backend does
+    not wait, the counter is still exported and readable)."""
+    from vectorizedmultiagentsimulator_amd import _native as N
+
+    lib = N.load_library()
+    assert isinstance(lib.vmas_host_waits(), int)

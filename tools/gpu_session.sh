@@ -23,6 +23,7 @@ for step in ${SESSION_STEPS:-tests bench prof}; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     bench) run bench 600 python bench.py --steps "$STEPS" --warmup 10 ;;
     benchenv) run bench_env 600 python bench.py --steps "$STEPS" --warmup 10 --broadphase env --cpu-steps 0 ;;
+    breakdown) run step_breakdown 300 python tools/step_breakdown.py ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-steps 0 ;;
   esac
 done

@@ -17,7 +17,9 @@ n_agents = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if scenario in ("discov
 kw = {"n_agents": n_agents}
 if scenario == "discovery":
     kw["use_agent_lidar"] = True
-env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, **kw)
+import os  # noqa: E402
+
+env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, graph_step=os.environ.get("GRAPH", "1") == "1", **kw)
 if scenario == "balance":
     env.world._substeps = 10
     env.world._sub_dt = env.world._dt / 10
@@ -28,7 +30,7 @@ t = time.perf_counter()
 for _ in range(100):
     env.step(env.get_random_actions())
 torch.cuda.synchronize()
-print(f"{scenario} {n_envs}: {(time.perf_counter() - t) / 100 * 1e3:.3f} ms/step")
+print(f"{scenario} {n_envs}: {(time.perf_counter() - t) / 100 * 1e3:.3f} ms/step, step mode {env.graph_status}")
 
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "vmas_device_count",
     "vmas_last_error",
     "vmas_stream_abort_capture",
+    "vmas_host_waits",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -73,6 +74,7 @@ EXPORTED_SYMBOLS = (
     "vmas_jit_compile_check",
     "vmas_jit_world_profile",
     "vmas_jit_world_passes",
+    "vmas_jit_world_check",
     "vmas_jit_world_grid",
     "vmas_jit_last_error",
 )
@@ -297,6 +299,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_abi_version.restype = _i32
     lib.vmas_device_count.restype = _i32
     lib.vmas_last_error.restype = ctypes.c_char_p
+    lib.vmas_host_waits.restype = _i32
+    lib.vmas_host_waits.argtypes = []
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_world_create.restype = _i32
@@ -346,7 +350,9 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_jit_world_passes.argtypes = [_vp, ctypes.POINTER(_i32)]
     lib.vmas_jit_world_device_timing.restype = _i32
     lib.vmas_jit_world_device_timing.argtypes = [_vp, _i32, ctypes.POINTER(ctypes.c_double),
-                                                 ctypes.POINTER(ctypes.c_int64)]
+                                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+    lib.vmas_jit_world_check.restype = _i32
+    lib.vmas_jit_world_check.argtypes = [_vp]
     lib.vmas_jit_world_grid.restype = _i32
     lib.vmas_jit_world_grid.argtypes = [_vp]
     lib.vmas_jit_last_error.restype = ctypes.c_char_p

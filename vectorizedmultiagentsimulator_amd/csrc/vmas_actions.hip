@@ -4,12 +4,14 @@
 // (651-655) and u = physical * u_multiplier (709), gfx950 kernel + host backend + C ABI.
 //
 // The reference runs ~5 torch ops and one host sync per agent; here one launch covers all agents
-// and the host learns the flags without a stream synchronisation: the kernel's last workgroup
-// (device arrival counter) copies the OR-ed flags into mapped pinned host memory and then stores
-// the call's sequence number there with system scope; the host spins on that word (checking the
-// stream for errors while it waits).  The device flag words and the counter are reset by that
-// same workgroup, so no memset is launched.  u is written for every env even when a flag is set
-// (the caller raises and drops it, as the reference raises before it assigns u).
+// and the host learns the flags without a stream synchronisation: every workgroup stores its
+// flag bits into its own slot and arrives on a device counter; the last to arrive ORs the slots
+// and publishes (sequence number << 32 | flag bits) into mapped pinned host memory with ONE
+// 64-bit system-scope store -- the number and the flags land together, so no system fence is
+// needed -- and clears the counter.  The host spins on that word (checking the stream for errors
+// while it waits).  Slots are overwritten by every call; nothing is memset per call.  u is
+// written for every env even when a flag is set (the caller raises and drops it, as the
+// reference raises before it assigns u).
 //
 // Arithmetic: clamp = min(max(x, -r), r) and u = v * m in fp32, the element-wise torch ops.
 #include <hip/hip_runtime.h>
@@ -22,17 +24,17 @@
 
 namespace {
 
-constexpr int kMaxRefsPerLaunch = 8;  // refs travel in the kernel arguments
-constexpr int kThreads = 256, kPerThread = 4;
+constexpr int kMaxRefsPerLaunch = 8;  // refs travel in the kernel arguments (16 flag bits)
+constexpr int kThreads = 256, kPerThread = 8, kMaxBlocksPerRef = 64;
 
 struct ApplyArgs {
     VmasActionApplyRef r[kMaxRefsPerLaunch];
     float* out;
-    uint32_t* dflags;   // [2 * kMaxRefsPerLaunch] device OR words, zero between calls
+    uint32_t* slots;    // [kMaxRefsPerLaunch][kMaxBlocksPerRef] flag bits of each workgroup
     uint32_t* counter;  // device arrival counter, zero between calls
-    uint32_t* hsig;     // mapped host words: [0] sequence number, [1 + 2i], [2 + 2i] flags of ref i
+    uint64_t* hsig;     // mapped host word: seq << 32 | flags (bit 2i NaN, 2i+1 out of range, ref i)
     uint32_t seq;
-    int B, n, total_blocks;
+    int B, n, gx;
 };
 
 __host__ __device__ inline void apply_one(const VmasActionApplyRef& r, float* out, int b, int c,
@@ -48,7 +50,8 @@ __host__ __device__ inline void apply_one(const VmasActionApplyRef& r, float* ou
 }
 
 __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
-    const VmasActionApplyRef& r = a.r[blockIdx.y];
+    const int ref = blockIdx.y;
+    const VmasActionApplyRef& r = a.r[ref];
     const long n = (long)a.B * r.n_cols;
     bool nan_seen = false, oor = false;
     const long stride = (long)gridDim.x * kThreads;
@@ -56,35 +59,44 @@ __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
         const int b = (int)(idx / r.n_cols), c = (int)(idx - (long)b * r.n_cols);
         apply_one(r, a.out, b, c, nan_seen, oor);
     }
-    if (__any(nan_seen) && (threadIdx.x & 63) == 0) atomicOr(&a.dflags[2 * blockIdx.y], 1u);
-    if (__any(oor) && (threadIdx.x & 63) == 0) atomicOr(&a.dflags[2 * blockIdx.y + 1], 1u);
-    // last workgroup: publish the flags to the host, reset the device words
+    __shared__ uint32_t bits;
     __shared__ bool last;
+    if (threadIdx.x == 0) bits = 0u;
+    __syncthreads();
+    const uint32_t mine = (__any(nan_seen) ? 1u : 0u) | (__any(oor) ? 2u : 0u);
+    if ((threadIdx.x & 63) == 0 && mine) atomicOr(&bits, mine << (2 * ref));
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(a.counter, 1u) == (uint32_t)a.total_blocks - 1u;
+        __hip_atomic_store(&a.slots[ref * kMaxBlocksPerRef + blockIdx.x], bits, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);  // the slot store has completed before the arrival
+        last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (uint32_t)(a.gx * a.n) - 1u;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
-    if ((int)threadIdx.x < 2 * a.n) {
-        const uint32_t v = __hip_atomic_load(&a.dflags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.hsig[1 + threadIdx.x], v ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        a.dflags[threadIdx.x] = 0u;
+    // the last workgroup: OR every slot, publish, clear the counter for the next call
+    uint32_t f = 0u;
+    for (int i = threadIdx.x; i < a.gx * a.n; i += kThreads) {
+        const int rf = i / a.gx, bx = i - rf * a.gx;
+        f |= __hip_atomic_load(&a.slots[rf * kMaxBlocksPerRef + bx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if (threadIdx.x == 0) bits = 0u;
+    __syncthreads();
+    if (f) atomicOr(&bits, f);
+    __syncthreads();
     if (threadIdx.x == 0) {
-        *a.counter = 0u;
-        __threadfence_system();
-        __hip_atomic_store(&a.hsig[0], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.hsig, ((uint64_t)a.seq << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 struct DevState {
-    uint32_t* dflags = nullptr;
+    uint32_t* slots = nullptr;
     uint32_t* counter = nullptr;
-    uint32_t* hsig = nullptr;  // mapped, coherent pinned memory
+    uint64_t* hsig = nullptr;  // mapped, coherent pinned memory
+    uint64_t* dsig = nullptr;  // its device address
     uint32_t seq = 0;
 };
 DevState g_dev[64];
@@ -118,14 +130,13 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
     VMAS_AUX_HIP(hipGetDevice(&cur));
     if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
     DevState& d = g_dev[device];
-    if (!d.dflags) {
-        VMAS_AUX_HIP(hipMalloc((void**)&d.dflags, 2 * kMaxRefsPerLaunch * 4));
+    if (!d.slots) {
+        VMAS_AUX_HIP(hipMalloc((void**)&d.slots, kMaxRefsPerLaunch * kMaxBlocksPerRef * 4));
         VMAS_AUX_HIP(hipMalloc((void**)&d.counter, 4));
-        VMAS_AUX_HIP(hipMemset(d.dflags, 0, 2 * kMaxRefsPerLaunch * 4));
         VMAS_AUX_HIP(hipMemset(d.counter, 0, 4));
-        VMAS_AUX_HIP(hipHostMalloc((void**)&d.hsig, (1 + 2 * kMaxRefsPerLaunch) * 4,
-                                   hipHostMallocMapped | hipHostMallocCoherent));
-        d.hsig[0] = 0u;
+        VMAS_AUX_HIP(hipHostMalloc((void**)&d.hsig, 8, hipHostMallocMapped | hipHostMallocCoherent));
+        VMAS_AUX_HIP(hipHostGetDevicePointer((void**)&d.dsig, d.hsig, 0));
+        *d.hsig = 0u;
     }
     hipStream_t st = (hipStream_t)stream;
     for (int first = 0; first < n_refs; first += kMaxRefsPerLaunch) {
@@ -136,21 +147,25 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
             a.r[i] = refs[first + i];
             max_elems = std::max(max_elems, (long)batch * refs[first + i].n_cols);
         }
-        const int gx = (int)std::max(1L, std::min(1024L, (max_elems + kThreads * kPerThread - 1) /
-                                                               (kThreads * kPerThread)));
+        const int gx = (int)std::max(1L, std::min((long)kMaxBlocksPerRef, (max_elems + kThreads * kPerThread - 1) /
+                                                                               (kThreads * kPerThread)));
         a.out = out;
-        a.dflags = d.dflags;
+        a.slots = d.slots;
         a.counter = d.counter;
-        a.hsig = d.hsig;
+        a.hsig = d.dsig;
         a.seq = ++d.seq;
         if (a.seq == 0u) a.seq = ++d.seq;  // 0 is the "nothing published" value
         a.B = batch;
         a.n = n;
-        a.total_blocks = gx * n;
+        a.gx = gx;
         hipLaunchKernelGGL(k_apply_actions, dim3(gx, n), dim3(kThreads), 0, st, a);
         VMAS_AUX_HIP(hipGetLastError());
-        if (int32_t rc = vmas_aux::wait_host_word(d.hsig, a.seq, st)) return rc;
-        for (int i = 0; i < 2 * n; ++i) flags[2 * first + i] = d.hsig[1 + i] != 0u;
+        uint64_t v = 0;
+        if (int32_t rc = vmas_aux::wait_host_word64(d.hsig, a.seq, &v, st)) return rc;
+        for (int i = 0; i < n; ++i) {
+            flags[2 * (first + i)] = (v >> (2 * i)) & 1u;
+            flags[2 * (first + i) + 1] = (v >> (2 * i + 1)) & 1u;
+        }
     }
     return VMAS_OK;
 }

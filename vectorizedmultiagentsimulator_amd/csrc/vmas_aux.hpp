@@ -12,10 +12,17 @@ namespace vmas_aux {
 // record the message returned by vmas_aux_last_error; returns code (vmas_spawn.hip)
 int32_t fail(int32_t code, const char* fmt, ...);
 
+// Count a host wait on the device (a stream / event synchronisation or a spin on a published
+// word) for vmas_host_waits: graph mode's check that a step can be captured (vmas_spawn.hip).
+void note_host_wait();
+
 // Spin until *word == seq (a kernel on `stream` stores it with system scope).  While waiting,
 // the stream is polled every few thousand reads: an error, or an idle stream without the store,
 // ends the wait with VMAS_E_HIP instead of spinning forever.
 int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream);
+// The same for a 64-bit word whose high half is the sequence number (its low half is a payload
+// published by the same single store); the whole word goes to *value.
+int32_t wait_host_word64(const uint64_t* word, uint32_t seq, uint64_t* value, hipStream_t stream);
 
 }  // namespace vmas_aux
 

@@ -40,6 +40,7 @@
 #include <hip/hip_ext.h>
 #include <dlfcn.h>
 
+#include "vmas_aux.hpp"
 #include "vmas_jit_ops.hpp"
 
 #include <algorithm>
@@ -319,7 +320,7 @@ struct Gen {
     }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 6) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
     }
 
     // expressions for entity e as seen by wave w (registers when w owns it)
@@ -625,7 +626,7 @@ struct Gen {
         o += "// generated by vmas_jit.hip for one world\n#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
-             "    uint32_t* ctl;\n    uint32_t* err;\n    unsigned long long* tm;\n"
+             "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
@@ -665,7 +666,7 @@ struct Gen {
         // Otherwise one group per workgroup and one pass per launch.  DONE is back to zero at
         // the end of every substep's pair phase, so it carries over between groups.
         o += "    const uint32_t epoch = a.ctl ? ld_agent(&a.ctl[3]) : 0u;\n";
-        o += "    if (a.ctl) device_timer_start(a.tm);\n";
+        o += "    const TimerStart t0s = device_timer_start(a.ctl ? a.tm : nullptr);\n";
         o += "    for (int pass = 0;; ++pass) {\n"
              "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "        for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
@@ -684,8 +685,8 @@ struct Gen {
              "        for (int i = threadIdx.x; i < nfl; i += blockDim.x)\n"
              "            __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
              "        if (!a.ctl) return;\n"
-             "        if (!grid_fixed_point(a.blk, a.mask, a.ctl, a.err, a.S * " + it(W) +
-             ", pass, a.max_pass, RED, epoch, a.tm)) return;\n"
+             "        if (!grid_fixed_point(a.blk, a.mask, a.ctl, a.err, a.herr, a.S * " + it(W) +
+             ", pass, a.max_pass, RED, epoch, a.tm, t0s)) return;\n"
              "    }\n}\n\n";
         o += "extern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) +
              ") k_world(Args a) {\n"
@@ -827,8 +828,9 @@ struct VmasJitWorld {
     hipFunction_t fn = nullptr;
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
     // persistent launch: d_ctl = [kGridCtlWords control words | inverted mask words], zeroed by
-    // one memset per step; d_err/h_err: sticky error bits and their pinned host copy
-    uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr;
+    // d_err: sticky error bits; h_err: mapped host word the kernel stores them into (dh_err: its
+    // device address)
+    uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr, *dh_err = nullptr;
     int grid = 0;          // persistent workgroups (0: one pass per launch, host-driven loop)
     bool coop = false;     // cooperative launch (VMAS_JIT_GRID=coop)
     hipStream_t last_stream = nullptr;
@@ -936,7 +938,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
     if (hipMalloc((void**)&W->d_ctl, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
-        hipHostMalloc((void**)&W->h_err, 4, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&W->h_err, 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&W->dh_err, W->h_err, 0) != hipSuccess ||
         hipMemset(W->d_err, 0, 4) != hipSuccess ||
         hipMemset(W->d_ctl, 0, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc fixed-point control words"));
@@ -1070,6 +1073,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(W->d_prof);
     put_ptr(persistent ? W->d_ctl : nullptr);
     put_ptr(W->d_err);
+    put_ptr(W->dh_err);
     put_ptr(W->timing && persistent ? W->d_tm : nullptr);
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
@@ -1103,8 +1107,8 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
 
-    // a fixed-point failure of an earlier persistent step (sticky device bits, copied back
-    // asynchronously after every persistent launch) surfaces here
+    // a fixed-point failure of an earlier persistent step (sticky error bits, which the kernel
+    // stores into mapped host memory) surfaces here
     if (uint32_t e = *(volatile uint32_t*)W->h_err)
         return jfail(e & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
                      "device-side broadphase fixed point failed in an earlier step (error bits 0x%x)", e);
@@ -1160,7 +1164,6 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
         } else if (int32_t rc = launch_plain(W->grid)) {
             return rc;
         }
-        JHIP(hipMemcpyAsync(W->h_err, W->d_err, 4, hipMemcpyDeviceToHost, stream));
         if (iterations) *iterations = 0;  // not known without a sync: vmas_jit_world_passes
         return VMAS_OK;
     }
@@ -1173,6 +1176,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
                            io->substeps, W->W, W->d_mask, W->d_viol);
         JHIP(hipGetLastError());
         JHIP(hipMemcpyAsync(W->h_viol, W->d_viol, 4, hipMemcpyDeviceToHost, stream));
+        vmas_aux::note_host_wait();
         JHIP(hipStreamSynchronize(stream));
         if (*W->h_viol == 0u) return VMAS_OK;
     }
@@ -1198,6 +1202,16 @@ int32_t vmas_jit_world_passes(VmasJitWorld* W, int32_t* passes) {
     return VMAS_OK;
 }
 
+// Error bits the kernel has reported so far (no wait: launches replayed from a HIP graph surface
+// a fixed-point failure through this check).
+int32_t vmas_jit_world_check(VmasJitWorld* W) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    if (uint32_t e = *(volatile uint32_t*)W->h_err)
+        return jfail(e & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
+                     "device-side broadphase fixed point failed in an earlier step (error bits 0x%x)", e);
+    return VMAS_OK;
+}
+
 // 0: host-driven passes; otherwise the persistent grid size (negative: plain, non-cooperative launch)
 int32_t vmas_jit_world_grid(const VmasJitWorld* W) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
@@ -1210,16 +1224,19 @@ int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
     return VMAS_OK;
 }
 
-// Device timer totals (timing on): every launch -- eager or replayed from a HIP graph -- adds
-// (latest workgroup end - earliest workgroup start) in s_memrealtime ticks.  Waits for the device.
-int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches) {
+// Device timer totals (timing on, persistent launches): every launch -- eager or replayed from a
+// HIP graph -- adds (final reduction - workgroup 0 start) in s_memrealtime ticks; *clock_ghz is
+// the in-kernel shader clock of the reducing workgroups.  Waits for the device.
+int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches,
+                                     double* clock_ghz) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
     JHIP(hipSetDevice(W->cfg.device));
     JHIP(hipDeviceSynchronize());
-    unsigned long long tm[5] = {0, 0, 0, 0, 0};
+    unsigned long long tm[7] = {0, 0, 0, 0, 0, 0, 0};
     JHIP(hipMemcpy(tm, W->d_tm, sizeof tm, hipMemcpyDeviceToHost));
     if (total_ms) *total_ms = (double)tm[2] / (double)W->wall_khz;
     if (launches) *launches = (int64_t)tm[4];
+    if (clock_ghz) *clock_ghz = tm[6] ? (double)tm[5] / (double)tm[6] * (double)W->wall_khz * 1e-6 : 0.0;
     if (reset) JHIP(hipMemset(W->d_tm, 0, 8 * 8));
     return VMAS_OK;
 }

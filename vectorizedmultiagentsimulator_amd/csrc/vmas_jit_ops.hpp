@@ -95,8 +95,8 @@ constexpr uint32_t kGridSpinLimit = 1u << 22;
 // memset: the final pass's reducer, which runs after every workgroup has arrived, clears the
 // counters and the mask words for the next launch, and the epoch (read by every workgroup at its
 // start, advanced by that reducer) keeps the previous launch's published word from being read as
-// this launch's.  (A memset node in front of the kernel was also not honoured as a dependency
-// inside a HIP graph replay on ROCm 7.2: the waits timed out there.)
+// this launch's.  It also removes the memset node in front of the kernel: with one there, replays
+// of a captured HIP graph timed out in these waits on ROCm 7.2 (cause not isolated).
 // RED: workgroup LDS of 2 * nwords + 2 words.  Returns whether another pass is needed.  Every
 // wait is bounded: a timeout stops the passes and sets an error bit instead of hanging.
 //
@@ -122,15 +122,33 @@ __device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
 // its start; the final pass's reducer -- the last workgroup to arrive, after which every
 // workgroup only reads the published word and exits -- adds (now - tm[0]) to tm[2] and counts
 // the launch in tm[4].  Two stores per launch instead of per-workgroup atomics (measured: ~10 us
-// on a 512-workgroup launch).
-__device__ __forceinline__ void device_timer_start(unsigned long long* tm) {
-    if (tm && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&tm[0], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// on a 512-workgroup launch).  The reducer also adds its own s_memtime (shader clock) and
+// s_memrealtime (100 MHz-class wall clock) spans to tm[5] / tm[6]: their ratio is the in-kernel
+// shader clock (MI355X_MICROARCH.md, DVFS give-back item 6).
+struct TimerStart {
+    unsigned long long rt, sc;
+};
+__device__ __forceinline__ TimerStart device_timer_start(unsigned long long* tm) {
+    TimerStart t{0ull, 0ull};
+    if (tm && threadIdx.x == 0) {
+        t.rt = __builtin_amdgcn_s_memrealtime();
+        t.sc = __builtin_amdgcn_s_memtime();
+        if (blockIdx.x == 0) __hip_atomic_store(&tm[0], t.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return t;
 }
 
-__device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err,
+// Sticky error bits: OR-ed into the device word, and the OR so far stored into the mapped host
+// word (system scope, no fence: any nonzero value means failure), so the host sees a failure
+// without a copy in the stream.
+__device__ __forceinline__ void report_err(uint32_t* err, uint32_t* herr, uint32_t bit) {
+    const uint32_t v = atomicOr(err, bit) | bit;
+    if (herr) __hip_atomic_store(herr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
                                         int nwords, int pass, int max_pass, uint32_t* RED, uint32_t epoch,
-                                        unsigned long long* tm) {
+                                        unsigned long long* tm, TimerStart t0s) {
     const uint32_t tag = ((epoch & 0xFFFFFFu) << 8) | ((uint32_t)(pass + 1) << 1);
     const uint32_t G = gridDim.x, k = blockIdx.x & 7u;
     const uint32_t n_k = (G + 7u - k) / 8u, n_sub = G < 8u ? G : 8u;  // workgroups in sub-counter k
@@ -154,7 +172,7 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
                 __builtin_amdgcn_s_sleep(2);
             }
             if (spins > kGridSpinLimit) {
-                atomicOr(err, kGridErrStateTimeout);
+                report_err(err, herr, kGridErrStateTimeout);
                 st = 0u;
             }
             RED[0] = st & 1u;
@@ -205,7 +223,7 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
     __builtin_amdgcn_s_waitcnt(0);  // the new mask words have completed before the publish
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (viol && !more) atomicOr(err, kGridErrNoConverge);
+        if (viol && !more) report_err(err, herr, kGridErrNoConverge);
         st_agent(&ctl[2], (uint32_t)(pass + 1));
         st_agent(&ctl[1], tag | (more ? 1u : 0u));
     }
@@ -214,11 +232,16 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
         if (threadIdx.x == 0) st_agent(&ctl[0], 0u);
         if (threadIdx.x >= 1 && threadIdx.x <= 8) st_agent(&ctl[32 * threadIdx.x], 0u);
         if (threadIdx.x == 9) st_agent(&ctl[3], epoch + 1u);
-        if (tm && threadIdx.x == 10) {
+        if (tm && threadIdx.x == 0) {  // (thread 0 holds this workgroup's start stamps)
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
             const unsigned long long t0 = __hip_atomic_load(&tm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             (void)__hip_atomic_fetch_add(&tm[2], t1 > t0 ? t1 - t0 : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             (void)__hip_atomic_fetch_add(&tm[4], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c1 > t0s.sc && t1 > t0s.rt) {
+                (void)__hip_atomic_fetch_add(&tm[5], c1 - t0s.sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                (void)__hip_atomic_fetch_add(&tm[6], t1 - t0s.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     __syncthreads();

@@ -28,6 +28,7 @@
 #include <thread>
 #include <vector>
 
+#include "vmas_aux.hpp"
 #include "vmas_physics.hpp"
 
 using namespace vmas;
@@ -185,7 +186,10 @@ int32_t ring_upload(int device, const void* src, size_t n, hipStream_t stream, c
     const int per = kSlots / kSegs;
     const int slot = r->next;
     const int seg = slot / per;
-    if (slot % per == 0 && r->ev_live[seg]) HIP_TRY(hipEventSynchronize(r->ev[seg]));
+    if (slot % per == 0 && r->ev_live[seg]) {
+        vmas_aux::note_host_wait();
+        HIP_TRY(hipEventSynchronize(r->ev[seg]));
+    }
     memcpy(r->host + (size_t)slot * kSlot, src, n);
     HIP_TRY(hipMemcpyAsync(r->dev + (size_t)slot * kSlot, r->host + (size_t)slot * kSlot, n,
                            hipMemcpyHostToDevice, stream));
@@ -1333,9 +1337,12 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     const size_t nwords = (size_t)io->substeps * W->W;
     HIP_TRY(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
     const int max_it = batch_bp ? io->substeps + 2 : 1;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(stream, &cap));
+    const bool timed = W->timing && cap == hipStreamCaptureStatusNone;  // (no events inside a graph)
     for (int it = 0; it < max_it; ++it) {
         std::pair<hipEvent_t, hipEvent_t> ev{};
-        if (W->timing) {
+        if (timed) {
             if (W->ev_free.empty()) {
                 HIP_TRY(hipEventCreate(&ev.first));
                 HIP_TRY(hipEventCreate(&ev.second));
@@ -1350,7 +1357,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
         else
             hipLaunchKernelGGL(k_step<false>, dim3(W->nblk), dim3(W->nw * 64), lds, stream, k);
         HIP_TRY(hipGetLastError());
-        if (W->timing) {
+        if (timed) {
             HIP_TRY(hipEventRecord(ev.second, stream));
             W->ev_pending.push_back(ev);
         }
@@ -1360,6 +1367,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
                            W->nblk, io->substeps, W->W, W->d_mask, W->d_viol);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(W->h_viol, W->d_viol, 4, hipMemcpyDeviceToHost, stream));
+        vmas_aux::note_host_wait();
         HIP_TRY(hipStreamSynchronize(stream));
         if (*W->h_viol == 0u) return VMAS_OK;
     }
@@ -1478,6 +1486,7 @@ int32_t vmas_check_actions(int32_t device, int32_t batch, const VmasActionRef* r
                        batch, cs->d_flags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(cs->h_flags, cs->d_flags, 8 * n_refs, hipMemcpyDeviceToHost, stream));
+    vmas_aux::note_host_wait();
     HIP_TRY(hipStreamSynchronize(stream));
     for (int i = 0; i < 2 * n_refs; ++i) flags[i] = cs->h_flags[i] != 0u;
     return VMAS_OK;

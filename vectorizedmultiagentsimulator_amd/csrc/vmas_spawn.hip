@@ -16,6 +16,7 @@
 // comparison `dist < min_dist` runs in fp32.  Compiled with -ffp-contract=off like the engine.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -43,13 +44,41 @@ int32_t fail(int32_t code, const char* fmt, ...) {
 
 const char* last_error() { return g_aux_err.c_str(); }
 
+std::atomic<uint32_t> g_host_waits{0};
+void note_host_wait() { g_host_waits.fetch_add(1u, std::memory_order_relaxed); }
+
 int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream) {
+    note_host_wait();
     for (uint64_t i = 1;; ++i) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return VMAS_OK;
         if ((i & 4095) == 0) {
             const hipError_t q = hipStreamQuery(stream);
             if (q == hipSuccess) {  // the stream drained: the store must be visible by now
                 if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return VMAS_OK;
+                return fail(VMAS_E_HIP, "kernel finished without publishing its result word");
+            }
+            if (q != hipErrorNotReady) return fail(VMAS_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+int32_t wait_host_word64(const uint64_t* word, uint32_t seq, uint64_t* value, hipStream_t stream) {
+    note_host_wait();
+    for (uint64_t i = 1;; ++i) {
+        uint64_t v = __atomic_load_n(word, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(v >> 32) == seq) {
+            *value = v;
+            return VMAS_OK;
+        }
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {
+                v = __atomic_load_n(word, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(v >> 32) == seq) {
+                    *value = v;
+                    return VMAS_OK;
+                }
                 return fail(VMAS_E_HIP, "kernel finished without publishing its result word");
             }
             if (q != hipErrorNotReady) return fail(VMAS_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
@@ -132,6 +161,8 @@ extern "C" {
 
 const char* vmas_aux_last_error(void) { return vmas_aux::last_error(); }
 
+int32_t vmas_host_waits(void) { return (int32_t)vmas_aux::g_host_waits.load(std::memory_order_relaxed); }
+
 int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied, int32_t n_occ,
                            int32_t occ_s0, int32_t occ_s1, int32_t occ_s2, const float* candidates,
                            int32_t first_try, int32_t n_tries, float min_dist, float* pos,
@@ -168,6 +199,7 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
     hipLaunchKernelGGL(k_spawn_resolve, dim3((batch + 255) / 256), dim3(256), 0, st, a, s.d_out);
     VMAS_AUX_HIP(hipGetLastError());
     VMAS_AUX_HIP(hipMemcpyAsync(s.h_out, s.d_out, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    vmas_aux::note_host_wait();
     VMAS_AUX_HIP(hipStreamSynchronize(st));
     *max_accepted = s.h_out[0];
     *n_unresolved = s.h_out[1];

@@ -409,15 +409,24 @@ class PhysicsEngine:
         if self._jit is not None:
             N.check_jit(self.lib.vmas_jit_world_set_timing(self._jit, on), "vmas_jit_world_set_timing")
 
-    def device_timing(self, reset: bool = True):
-        """(milliseconds, launches) of the specialised step kernel from its in-kernel device timer
-        (vmas_jit_world_device_timing): the timer of launches replayed from a HIP graph."""
+    def device_timing(self, reset: bool = True, with_clock: bool = False):
+        """(milliseconds, launches[, shader clock GHz]) of the specialised step kernel from its
+        in-kernel device timer (vmas_jit_world_device_timing): the timer of launches replayed from
+        a HIP graph, and the clock the chip held inside the kernel."""
         ms = ctypes.c_double(0.0)
         n = ctypes.c_int64(0)
+        ghz = ctypes.c_double(0.0)
         if self._jit is not None:
             N.check_jit(self.lib.vmas_jit_world_device_timing(self._jit, int(reset), ctypes.byref(ms),
-                                                              ctypes.byref(n)), "vmas_jit_world_device_timing")
-        return ms.value, n.value
+                                                              ctypes.byref(n), ctypes.byref(ghz)),
+                        "vmas_jit_world_device_timing")
+        return (ms.value, n.value, ghz.value) if with_clock else (ms.value, n.value)
+
+    def check_device_errors(self) -> None:
+        """Raise a device-side fixed-point failure reported by any launch so far, without waiting
+        (graph replays do not pass through vmas_jit_world_step's own check)."""
+        if self._jit is not None:
+            N.check_jit(self.lib.vmas_jit_world_check(self._jit), "vmas_jit_world_check")
 
     def graph_token(self):
         """What a captured step depends on besides tensor contents: the static tables (entity /

@@ -135,12 +135,30 @@ class _CapturableConstants:
         return False
 
 
+def _bytes(t: Tensor) -> Tensor:
+    """A contiguous tensor as a flat uint8 view."""
+    return t.reshape(-1).view(torch.uint8)
+
+
 def _storage_key(t: Tensor) -> int:
     return t.untyped_storage().data_ptr()
 
 
 class GraphUnsupported(RuntimeError):
     pass
+
+
+def _reset_generator_capture_state(dev):
+    """After a failed capture torch's CUDA generator may still consider itself captured (the
+    capture epilogue never ran), which makes every later random op raise.  One tiny successful
+    capture runs the prologue / epilogue pair again; the caller restores the RNG state after."""
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            torch.empty(1, device=dev).uniform_()
+        del g
+    except Exception:  # noqa: BLE001 -- best effort; the eager step reports any real problem
+        pass
 
 
 class StepGraph:
@@ -178,6 +196,7 @@ class StepGraph:
         a holonomic agent's force is a view of u -- so the fresh actions must land last.)"""
         if self.graph is None:
             return
+        self.env.world.engine.check_device_errors()
         if not self._still_valid():
             self.drop("world or entity parameters changed")
             return
@@ -190,20 +209,59 @@ class StepGraph:
                 with torch.no_grad():
                     t.copy_(cur)
                 d[k] = t
-        if not self._first_replay and self._carry_dst:
+        if not self._first_replay:
             with torch.no_grad():
-                torch._foreach_copy_(self._carry_dst, self._carry_src)
+                if self._carry_dst:
+                    torch._foreach_copy_(self._carry_dst, self._carry_src)
+                for x, y in self._carry_other:
+                    x.copy_(y)
 
     def step(self):
         """Run the post-action part of a step (actions already applied; before_actions ran before
         them); returns its results."""
         if self.graph is None:
-            if self.status in ("warming", "dropped") and self.eager_steps >= WARM_STEPS:
-                if self._capture():
-                    return self._replay()
+            if self.status in ("warming", "dropped"):
+                if self.eager_steps >= WARM_STEPS:
+                    if self._capture():
+                        return self._replay()
+                elif self.eager_steps == WARM_STEPS - 1:
+                    self.eager_steps += 1
+                    return self._trial()
             self.eager_steps += 1
             return self.body()
         return self._replay()
+
+    def _trial(self):
+        """The last eager step before the capture, watched for host waits: torch's synchronising
+        ops (sync debug mode "warn") and the native library's (vmas_host_waits).  A step that waits
+        on the device cannot be captured -- a wait inside a capture invalidates it -- so such an
+        env stays eager without attempting one."""
+        import warnings
+
+        from ... import _native as N
+
+        lib = N.load_library()
+        w0 = lib.vmas_host_waits()
+        mode = torch.cuda.get_sync_debug_mode()
+        consts = _CapturableConstants()  # host constants go through a pinned arena, as in capture
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            torch.cuda.set_sync_debug_mode(1)
+            try:
+                with consts:
+                    out = self.body()
+            finally:
+                torch.cuda.set_sync_debug_mode(mode)
+        self._trial_consts = consts  # the arena outlives the copies that read it
+        # torch's warning: "called a synchronizing CUDA operation" (not the notice that the mode
+        # is a prototype, which set_sync_debug_mode emits itself)
+        syncs = [str(r.message).splitlines()[0] for r in rec
+                 if "synchronizing" in str(r.message) and "prototype" not in str(r.message)]
+        native = (lib.vmas_host_waits() - w0) & 0xFFFFFFFF
+        if syncs or native:
+            self.status = "eager"
+            self.why = ("host sync in the step: " + (syncs[0] if syncs else f"{native} native host wait(s)"))[:300]
+        return out
 
     def drop(self, why: str):
         self.graph = None
@@ -225,6 +283,7 @@ class StepGraph:
         g = torch.cuda.CUDAGraph()
         consts = _CapturableConstants()
         side = torch.cuda.Stream(dev)
+        prev_stream = torch.cuda.current_stream(dev)
         env._raw_outputs = True
         try:
             with torch.cuda.graph(g, stream=side), consts:
@@ -238,7 +297,11 @@ class StepGraph:
             # a capture invalidated by a forbidden call may be left open: end it, so that the
             # eager step that follows can launch
             N.load_library().vmas_stream_abort_capture(ctypes.c_void_p(side.cuda_stream))
+            # torch.cuda.graph's __exit__ leaves the capture stream current when capture_end
+            # raises: go back to the caller's stream
+            torch.cuda.set_stream(prev_stream)
             torch.cuda.synchronize(dev)
+            _reset_generator_capture_state(dev)
             for o, d in snap:
                 o.__dict__.clear()
                 o.__dict__.update(d)
@@ -298,7 +361,15 @@ class StepGraph:
                 for x, y in pairs:
                     dst.append(x)
                     src.append(y)
-        self._carry_dst, self._carry_src = dst, src
+        # one multi-tensor copy kernel: contiguous pairs as flat byte views (one dtype), the rest
+        # (non-contiguous views) copied one by one
+        self._carry_dst, self._carry_src, self._carry_other = [], [], []
+        for x, y in zip(dst, src):
+            if x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype:
+                self._carry_dst.append(_bytes(x))
+                self._carry_src.append(_bytes(y))
+            else:
+                self._carry_other.append((x, y))
         # every tensor attribute of the tracked objects as bound after the capture: the caller
         # re-binding one of them between steps is detected by identity
         self._watch = []
@@ -321,20 +392,14 @@ class StepGraph:
         return self._clone_outputs()
 
     def _clone_outputs(self):
+        """Fresh copies of the replay's outputs: one byte buffer, one multi-tensor copy kernel."""
         ts = self._out_tensors
-        by_dtype: Dict[torch.dtype, List[int]] = {}
-        for i, t in enumerate(ts):
-            by_dtype.setdefault(t.dtype, []).append(i)
-        fresh: List[Optional[Tensor]] = [None] * len(ts)
-        for dt, idx in by_dtype.items():
-            total = sum(ts[i].numel() for i in idx)
-            flat = torch.empty(total, dtype=dt, device=ts[idx[0]].device)
-            views, off = [], 0
-            for i in idx:
-                n = ts[i].numel()
-                v = flat[off: off + n].view(ts[i].shape)
-                off += n
-                fresh[i] = v
-                views.append(v)
-            torch._foreach_copy_(views, [ts[i] for i in idx])
+        offs, total = [], 0
+        for t in ts:
+            offs.append(total)
+            total = (total + t.numel() * t.element_size() + 15) & ~15
+        flat = torch.empty(total, dtype=torch.uint8, device=ts[0].device)
+        dst = [flat[o: o + t.numel() * t.element_size()] for o, t in zip(offs, ts)]
+        torch._foreach_copy_(dst, [_bytes(t if t.is_contiguous() else t.contiguous()) for t in ts])
+        fresh = [d.view(t.dtype).view(t.shape) for d, t in zip(dst, ts)]
         return _rebuild(self._out_tree, iter(fresh))
