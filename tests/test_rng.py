@@ -5,6 +5,7 @@ import contextlib
 import random
 
 import numpy as np
+import pytest
 import torch
 
 from vectorizedmultiagentsimulator_amd.simulator.environment import environment as envmod
@@ -71,3 +72,38 @@ def test_restore_accepts_legacy_tuples():
     np.random.seed(3)
     assert np.array_equal(a, np.random.normal(size=3))
     np.random.set_state(st)
+
+
+def _random_actions_both_ways(device):
+    from vectorizedmultiagentsimulator_amd import make_env
+    from vectorizedmultiagentsimulator_amd.simulator.environment import Environment
+
+    env = make_env("balance", num_envs=777, device=device, seed=5, n_agents=3)
+    cuda = env.device.type == "cuda"
+    saved = [x.clone() if isinstance(x, torch.Tensor) else x for x in Environment.vmas_random_state]
+    saved_cuda = torch.cuda.get_rng_state(env.device) if cuda else None
+    key = str(env.device)
+    Environment._COLUMN_DRAWS[key] = False  # the reference's per-column tensors + stack
+    ref = env.get_random_actions()
+    after_ref = [x.clone() if isinstance(x, torch.Tensor) else x for x in Environment.vmas_random_state]
+    after_cuda = torch.cuda.get_rng_state(env.device) if cuda else None
+    Environment.vmas_random_state[:] = saved
+    if cuda:
+        torch.cuda.set_rng_state(saved_cuda, env.device)
+    Environment._COLUMN_DRAWS.pop(key)
+    assert Environment._column_draws(env.device)
+    fast = env.get_random_actions()
+    for a, b in zip(ref, fast):
+        assert a.shape == b.shape and torch.equal(a, b)
+    assert torch.equal(Environment.vmas_random_state[0], after_ref[0])
+    if cuda:
+        assert torch.equal(torch.cuda.get_rng_state(env.device), after_cuda)
+
+
+def test_random_actions_column_draws_match_reference_pattern():
+    _random_actions_both_ways("cpu")
+
+
+@pytest.mark.gpu
+def test_random_actions_column_draws_match_reference_pattern_gpu(gpu_device):
+    _random_actions_both_ways(gpu_device)

@@ -358,6 +358,18 @@ class Environment(TorchVectorizedObject):
         return self._random_action(agent)
 
     def _random_action(self, agent: Agent) -> torch.Tensor:
+        if self.continuous_actions and self._column_draws(agent.device):
+            # each column drawn in place of the [B, n] result: the same uniform_ calls on the
+            # same numbers of elements as the reference's per-column tensors + stack, without
+            # the stack kernel (checked once per device: _column_draws)
+            n_c = self.world.dim_c if (self.world.dim_c != 0 and not agent.silent) else 0
+            out = torch.empty(agent.batch_dim, agent.action_size + n_c, device=agent.device, dtype=torch.float32)
+            for action_index in range(agent.action_size):
+                r = self._u_range_value(agent, action_index)
+                out[:, action_index].uniform_(-r, r)
+            for k in range(n_c):
+                out[:, agent.action_size + k].uniform_(0, 1)
+            return out
         if self.continuous_actions:
             actions = []
             # (uniform_ overwrites every element: empty() draws the same numbers as zeros())
@@ -388,6 +400,39 @@ class Environment(TorchVectorizedObject):
         (Drawing them on a side stream, overlapped with the previous step's graph, measured
         slower: 87-98 M vs 106-119 M env-steps/s, interleaved runs on one MI355X.)"""
         return [self._random_action(agent) for agent in self.agents]
+
+    _COLUMN_DRAWS: Dict[str, bool] = {}
+
+    @classmethod
+    def _column_draws(cls, device) -> bool:
+        """Whether uniform_ on a column view of a [B, n] tensor draws exactly what uniform_ on a
+        contiguous [B] tensor draws from the same generator state, and advances the generator
+        by the same amount (the philox counter depends on the element index, not the layout).
+        Probed once per device with the global generator saved and restored around it."""
+        key = str(device)
+        ok = cls._COLUMN_DRAWS.get(key)
+        if ok is None:
+            dev = torch.device(device)
+            B = 1031  # not a multiple of any launch geometry
+            if dev.type == "cuda":
+                gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+            else:
+                gen = torch.default_generator
+            saved = gen.get_state()
+            try:
+                a = torch.empty(B, device=dev).uniform_(-0.7, 0.7)
+                b = torch.empty(B, device=dev).uniform_(-0.3, 0.3)
+                after_ref = gen.get_state()
+                gen.set_state(saved)
+                out = torch.empty(B, 2, device=dev)
+                out[:, 0].uniform_(-0.7, 0.7)
+                out[:, 1].uniform_(-0.3, 0.3)
+                ok = (torch.equal(out[:, 0], a) and torch.equal(out[:, 1], b)
+                      and torch.equal(gen.get_state(), after_ref))
+            finally:
+                gen.set_state(saved)
+            cls._COLUMN_DRAWS[key] = ok
+        return ok
 
     def _check_discrete_action(self, action: Tensor, low: int, high: int, type: str):
         assert torch.all(
