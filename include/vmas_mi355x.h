@@ -277,6 +277,23 @@ typedef struct VmasActionApplyRef {
 int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyRef* refs,
                            int32_t n_refs, float* out, uint8_t* flags, void* stream);
 
+/* Deferred device assertions for graph mode (csrc/vmas_actions.hip).  Replaces the host sync of
+ * a reference assert on a device tensor inside the step -- Agent.action_callback's range check of
+ * a scripted action (core.py:977-980) -- when the step is captured into a HIP graph.
+ * vmas_assert_publish enqueues one kernel (capturable) that ANDs the n bytes of `cond` (torch.bool,
+ * nonzero = holds) and publishes (epoch << 32 | violated) for `slot` into mapped host memory with
+ * one system-scope store; every execution advances the slot's device epoch by one (0 skipped).
+ * vmas_assert_wait spins on the host until the slot shows epoch `seq` and returns its violated
+ * bit (polling the stream: an error or an idle stream without the store ends the wait with
+ * VMAS_E_HIP).  No reference counterpart beyond the assert it defers. */
+typedef struct VmasDeviceAssert VmasDeviceAssert;
+int32_t vmas_assert_create(int32_t device, int32_t n_slots, VmasDeviceAssert** out);
+int32_t vmas_assert_destroy(VmasDeviceAssert* ch);
+int32_t vmas_assert_publish(VmasDeviceAssert* ch, int32_t slot, const uint8_t* cond, int64_t n,
+                            void* stream);
+int32_t vmas_assert_wait(VmasDeviceAssert* ch, int32_t slot, uint32_t seq, int32_t* violated,
+                         void* stream);
+
 /* Distance queries; out has B floats, or B bytes of 0/1 (torch.bool) for VMAS_OVERLAP_PAIR. */
 int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
                       const VmasShapeRef* b, const float* test_point, int32_t tp_s0,

@@ -56,7 +56,7 @@ def _assert_same(a, b, what):
 CASES = [
     ("balance", dict(n_agents=4), 10, "graph"),
     ("transport", dict(n_agents=4), None, "graph"),
-    ("flocking", dict(n_agents=4), None, "eager"),     # scripted agent: range assert syncs
+    ("flocking", dict(n_agents=4), None, "graph"),     # scripted agent: range assert on the device
     ("discovery", dict(n_agents=4), None, "eager"),    # spawn sampler: rejection loop syncs
 ]
 
@@ -101,6 +101,31 @@ def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
     assert graph.graph_status == expect, graph.graph_reason
     if expect == "graph":
         assert graph._graph.replays >= 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph_step", [False, True], ids=["eager", "graph"])
+def test_scripted_action_assert_raised_from_step_gpu(gpu_device, graph_step):
+    """A scripted agent's out-of-range action (core.py:977-980) raises from the step() that
+    computed it, eagerly and from a replayed graph (where the check runs on the device)."""
+    env = make_env("flocking", num_envs=256, device=gpu_device, seed=0, graph_step=graph_step, n_agents=3)
+    scale = torch.ones(1, device=gpu_device)
+    sc = env.scenario
+
+    def script(agent, world):
+        t = sc.t / 30
+        agent.action.u = torch.stack([torch.cos(t), torch.sin(t)], dim=1) * scale
+
+    sc._target._action_script = script
+    for _ in range(5):
+        env.step(env.get_random_actions())
+    if graph_step:
+        assert env.graph_status == "graph", env.graph_reason
+    scale.fill_(2.0)  # read by the captured step: |u| = 2|cos t| > u_range 1 in most envs
+    with pytest.raises(AssertionError, match="Scripted physical action of target is out of range"):
+        env.step(env.get_random_actions())
+    scale.fill_(1.0)
+    env.step(env.get_random_actions())  # the channel keeps working after a raise
 
 
 @pytest.mark.gpu

@@ -62,6 +62,10 @@ EXPORTED_SYMBOLS = (
     "vmas_distance",
     "vmas_check_actions",
     "vmas_apply_actions",
+    "vmas_assert_create",
+    "vmas_assert_destroy",
+    "vmas_assert_publish",
+    "vmas_assert_wait",
     "vmas_spawn_resolve",
     "vmas_aux_last_error",
     "vmas_jit_world_create",
@@ -321,6 +325,14 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_check_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp]
     lib.vmas_apply_actions.restype = _i32
     lib.vmas_apply_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp, _vp]
+    lib.vmas_assert_create.restype = _i32
+    lib.vmas_assert_create.argtypes = [_i32, _i32, ctypes.POINTER(_vp)]
+    lib.vmas_assert_destroy.restype = _i32
+    lib.vmas_assert_destroy.argtypes = [_vp]
+    lib.vmas_assert_publish.restype = _i32
+    lib.vmas_assert_publish.argtypes = [_vp, _i32, _vp, ctypes.c_int64, _vp]
+    lib.vmas_assert_wait.restype = _i32
+    lib.vmas_assert_wait.argtypes = [_vp, _i32, ctypes.c_uint32, ctypes.POINTER(_i32), _vp]
     lib.vmas_distance.restype = _i32
     lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
     lib.vmas_spawn_resolve.restype = _i32

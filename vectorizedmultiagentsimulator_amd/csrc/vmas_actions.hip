@@ -102,7 +102,33 @@ struct DevState {
 DevState g_dev[64];
 std::mutex g_mu;
 
+// Deferred assertion of one slot: AND of n condition bytes, published with the slot's next epoch.
+__global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int64_t n, uint32_t* epoch,
+                                                        uint64_t* hsig) {
+    __shared__ uint32_t bad;
+    if (threadIdx.x == 0) bad = 0u;
+    __syncthreads();
+    bool mine = false;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mine |= cond[i] == 0;
+    if ((threadIdx.x & 63) == 0 && __any(mine)) atomicOr(&bad, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t e = *epoch + 1u;
+        if (e == 0u) e = 1u;  // 0 is the "nothing published" value
+        *epoch = e;
+        __hip_atomic_store(hsig, ((uint64_t)e << 32) | bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace
+
+struct VmasDeviceAssert {
+    int device = 0;
+    int n_slots = 0;
+    uint32_t* epoch = nullptr;  // [n_slots] device epochs
+    uint64_t* hsig = nullptr;   // [n_slots] mapped, coherent pinned words
+    uint64_t* dsig = nullptr;   // their device address
+};
 
 extern "C" {
 
@@ -167,6 +193,58 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
             flags[2 * (first + i) + 1] = (v >> (2 * i + 1)) & 1u;
         }
     }
+    return VMAS_OK;
+}
+
+int32_t vmas_assert_create(int32_t device, int32_t n_slots, VmasDeviceAssert** out) {
+    if (!out || n_slots <= 0 || n_slots > 4096 || device < 0)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_assert_create: bad arguments");
+    *out = nullptr;
+    int cur = -1;
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
+    VmasDeviceAssert* ch = new VmasDeviceAssert();
+    ch->device = device;
+    ch->n_slots = n_slots;
+    hipError_t e = hipMalloc((void**)&ch->epoch, 4 * (size_t)n_slots);
+    if (e == hipSuccess) e = hipMemset(ch->epoch, 0, 4 * (size_t)n_slots);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ch->hsig, 8 * (size_t)n_slots, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ch->dsig, ch->hsig, 0);
+    if (e == hipSuccess) e = hipDeviceSynchronize();  // the epoch memset has landed before any capture
+    if (cur != device) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        vmas_assert_destroy(ch);
+        return vmas_aux::fail(VMAS_E_HIP, "vmas_assert_create: %s", hipGetErrorString(e));
+    }
+    for (int i = 0; i < n_slots; ++i) ch->hsig[i] = 0u;
+    *out = ch;
+    return VMAS_OK;
+}
+
+int32_t vmas_assert_destroy(VmasDeviceAssert* ch) {
+    if (!ch) return VMAS_OK;
+    if (ch->epoch) (void)hipFree(ch->epoch);
+    if (ch->hsig) (void)hipHostFree(ch->hsig);
+    delete ch;
+    return VMAS_OK;
+}
+
+int32_t vmas_assert_publish(VmasDeviceAssert* ch, int32_t slot, const uint8_t* cond, int64_t n, void* stream) {
+    if (!ch || !cond || slot < 0 || slot >= ch->n_slots || n <= 0)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_assert_publish: bad arguments");
+    hipLaunchKernelGGL(k_assert_publish, dim3(1), dim3(256), 0, (hipStream_t)stream, cond, n, ch->epoch + slot,
+                       ch->dsig + slot);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_assert_wait(VmasDeviceAssert* ch, int32_t slot, uint32_t seq, int32_t* violated, void* stream) {
+    if (!ch || !violated || slot < 0 || slot >= ch->n_slots || seq == 0u)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_assert_wait: bad arguments");
+    uint64_t v = 0;
+    if (int32_t rc = vmas_aux::wait_host_word64(ch->hsig + slot, seq, &v, (hipStream_t)stream)) return rc;
+    *violated = (int32_t)(v & 1u);
     return VMAS_OK;
 }
 

@@ -768,9 +768,12 @@ class Agent(Entity):
         assert self._action.u.shape[1] == self.action_size, (
             f"Scripted action of agent {self.name} has wrong shape"
         )
-        assert (
-            (self._action.u / self.action.u_multiplier_tensor).abs() <= self.action.u_range_tensor
-        ).all(), f"Scripted physical action of {self.name} is out of range"
+        ok = ((self._action.u / self.action.u_multiplier_tensor).abs() <= self.action.u_range_tensor).all()
+        sink = world._assert_sink
+        if sink is None:
+            assert ok, f"Scripted physical action of {self.name} is out of range"
+        else:  # graph mode: checked on the device, raised from the same step() (environment/_graph.py)
+            sink(ok, f"Scripted physical action of {self.name} is out of range")
 
     @property
     def u_range(self):
@@ -899,6 +902,8 @@ class World(TorchVectorizedObject):
         self._contact_margin = contact_margin
         self._torque_constraint_force = torque_constraint_force
         self._joints = {}
+        # graph mode's sink for asserts on device tensors inside the step (None: assert eagerly)
+        self._assert_sink = None
         self._collidable_pairs = [
             {Sphere, Sphere},
             {Sphere, Box},

@@ -27,8 +27,11 @@ What a replay must honour, and how:
     runs eagerly and captures again.
   * Outputs.  The returned observations / rewards / dones / infos are fresh copies (the
     reference clones them too), made by one multi-tensor copy per dtype after the replay.
+  * Asserts on device tensors inside the step (a scripted agent's action range check,
+    core.py:977-980) are captured as device checks (``_DeviceAsserts``) and raised from the
+    same step() call after the replay.
   * What cannot be captured -- a host sync inside the step (``.item()``, ``bool(t.any())``,
-    the spawn sampler's rejection loop, a scripted agent's range assert), a host-to-device copy
+    the spawn sampler's rejection loop), a host-to-device copy
     of pageable memory, discrete or communication actions -- makes the capture fail; the
     simulator's objects are rolled back (nothing ran: capture only records) and the env stays
     eager.  ``env.graph_status`` says which.
@@ -148,6 +151,73 @@ class GraphUnsupported(RuntimeError):
     pass
 
 
+def _assert_unwatched(ok: Tensor, msg: str):
+    """The trial step's sink: the reference's eager assert, not counted as a host sync of the
+    step (a captured step defers it to the device, _DeviceAsserts)."""
+    mode = torch.cuda.get_sync_debug_mode()
+    torch.cuda.set_sync_debug_mode(0)
+    try:
+        holds = bool(ok)
+    finally:
+        torch.cuda.set_sync_debug_mode(mode)
+    assert holds, msg
+
+
+class _DeviceAsserts:
+    """Asserts on device tensors inside a captured step (a scripted agent's action range check,
+    core.py:977-980).  At capture each one becomes a native kernel (vmas_assert_publish) that
+    publishes the condition with a per-replay epoch into mapped host memory; after a replay the
+    host waits for every slot's word of that replay (the kernels run at the start of the graph,
+    so the wait overlaps the rest of it) and raises the reference's AssertionError, in order,
+    from the same step() call.  Unlike the eager step, the replay's physics has then already run."""
+
+    MAX_SLOTS = 64
+
+    def __init__(self, dev):
+        from ... import _native as N
+
+        self.N = N
+        self.lib = N.load_library()
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        N.check_aux(self.lib.vmas_assert_create(idx, self.MAX_SLOTS, ctypes.byref(h)), "vmas_assert_create")
+        self.h = h
+        self.msgs: List[str] = []
+        self.keep: List[Tensor] = []
+        self.seq = 0
+
+    def capture_sink(self, ok: Tensor, msg: str):
+        if len(self.msgs) >= self.MAX_SLOTS:
+            raise GraphUnsupported("too many device asserts in the captured step")
+        ok = ok.reshape(-1)
+        if ok.dtype is not torch.bool or not ok.is_contiguous():
+            ok = ok.to(torch.bool).contiguous()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(ok.device).cuda_stream)
+        self.N.check_aux(self.lib.vmas_assert_publish(self.h, len(self.msgs), ok.data_ptr(), ok.numel(), stream),
+                         "vmas_assert_publish")
+        self.keep.append(ok)
+        self.msgs.append(msg)
+
+    def after_replay(self, dev):
+        if not self.msgs:
+            return
+        self.seq = (self.seq + 1) & 0xFFFFFFFF or 1
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        bad = ctypes.c_int32(0)
+        for slot, msg in enumerate(self.msgs):
+            self.N.check_aux(self.lib.vmas_assert_wait(self.h, slot, self.seq, ctypes.byref(bad), stream),
+                             "vmas_assert_wait")
+            assert not bad.value, msg
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h is not None and h.value:
+            try:
+                self.lib.vmas_assert_destroy(h)
+            except Exception:  # noqa: BLE001 -- interpreter shutdown
+                pass
+
+
 def _reset_generator_capture_state(dev):
     """After a failed capture torch's CUDA generator may still consider itself captured (the
     capture epilogue never ran), which makes every later random op raise.  One tiny successful
@@ -176,6 +246,7 @@ class StepGraph:
         self._carry_src: List[Tensor] = []  # Y (written by the graph)
         self._watch: List[Tuple[dict, str, Tensor]] = []  # (obj.__dict__, key, bound tensor)
         self._first_replay = True
+        self._asserts: Optional[_DeviceAsserts] = None
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -247,10 +318,12 @@ class StepGraph:
         with warnings.catch_warnings(record=True) as rec:
             warnings.simplefilter("always")
             torch.cuda.set_sync_debug_mode(1)
+            self.env.world._assert_sink = _assert_unwatched
             try:
                 with consts:
                     out = self.body()
             finally:
+                self.env.world._assert_sink = None
                 torch.cuda.set_sync_debug_mode(mode)
         self._trial_consts = consts  # the arena outlives the copies that read it
         # torch's warning: "called a synchronizing CUDA operation" (not the notice that the mode
@@ -285,10 +358,13 @@ class StepGraph:
         side = torch.cuda.Stream(dev)
         prev_stream = torch.cuda.current_stream(dev)
         env._raw_outputs = True
+        asserts = _DeviceAsserts(dev)
         try:
+            env.world._assert_sink = asserts.capture_sink
             with torch.cuda.graph(g, stream=side), consts:
                 out = self.body()
             self._consts = consts
+            self._asserts = asserts
             self._sig = eng.graph_token()
             self._plan(objs, snap, out)
         except Exception as ex:  # noqa: BLE001 -- any capture failure means "stay eager"
@@ -312,6 +388,7 @@ class StepGraph:
             return False
         finally:
             env._raw_outputs = False
+            env.world._assert_sink = None
         self.graph = g
         self.status = "graph"
         self.why = ""
@@ -389,7 +466,9 @@ class StepGraph:
         self._first_replay = False
         self.graph.replay()
         self.replays += 1
-        return self._clone_outputs()
+        out = self._clone_outputs()
+        self._asserts.after_replay(self.env.device)
+        return out
 
     def _clone_outputs(self):
         """Fresh copies of the replay's outputs: one byte buffer, one multi-tensor copy kernel."""
