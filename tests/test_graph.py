@@ -129,6 +129,40 @@ def test_scripted_action_assert_raised_from_step_gpu(gpu_device, graph_step):
 
 
 @pytest.mark.gpu
+def test_replay_leaves_host_rng_states_as_the_swap_does_gpu(gpu_device):
+    """A replayed step skips local_seed's host RNG swap (it runs no host RNG code): the user's
+    torch / numpy / python streams and the simulator's saved states are what the swap leaves."""
+    import random
+
+    import numpy as np
+
+    env = make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=True, n_agents=4)
+    for _ in range(4):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "graph"
+    sim_before = [torch.random.get_rng_state(), np.random.get_state(), random.getstate()]
+    sim_before = list(Environment.vmas_random_state)
+    torch.manual_seed(3)
+    np.random.seed(3)
+    random.seed(3)
+    want = (torch.rand(3), np.random.rand(3), random.random())
+    torch.manual_seed(3)
+    np.random.seed(3)
+    random.seed(3)
+    env.step(env.get_random_actions())
+    got = (torch.rand(3), np.random.rand(3), random.random())
+    assert torch.equal(want[0], got[0]) and np.array_equal(want[1], got[1]) and want[2] == got[2]
+    assert torch.equal(Environment.vmas_random_state[0], sim_before[0])
+    # an exception inside a replayed step leaves the simulator's states swapped in (reference)
+    bad = env.get_random_actions()
+    bad[0][0, 0] = float("nan")
+    torch.manual_seed(99)
+    with pytest.raises(AssertionError):
+        env.step(bad)
+    assert torch.equal(torch.random.get_rng_state(), Environment.vmas_random_state[0])
+
+
+@pytest.mark.gpu
 def test_graph_parameter_change_recaptures_gpu(gpu_device):
     env = make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=True, n_agents=4)
     for _ in range(4):

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from vectorizedmultiagentsimulator_amd.simulator.environment import environment as envmod
-from vectorizedmultiagentsimulator_amd.simulator.environment._rng import numpy_global_rng
+from vectorizedmultiagentsimulator_amd.simulator.environment._rng import numpy_global_rng, python_global_rng
 
 
 @contextlib.contextmanager
@@ -52,6 +52,7 @@ def _script(ctx_factory):
 
 def test_fast_swap_is_active_and_exact():
     assert numpy_global_rng().fast  # the offset probe validated on this numpy build
+    assert python_global_rng().fast  # ... and on this CPython build
     saved = np.random.get_state()
     try:
         expected = _script(reference_local_seed)
@@ -61,6 +62,24 @@ def test_fast_swap_is_active_and_exact():
     assert len(expected) == len(got)
     for a, b in zip(expected, got):
         assert a == b
+
+
+def test_python_rng_swap_round_trips():
+    r = python_global_rng()
+    st = random.getstate()
+    try:
+        random.seed(9)
+        random.gauss(0, 1)  # leaves gauss_next cached
+        snap, want = r.snapshot(), random.getstate()
+        a = [random.random(), random.gauss(0, 1), random.getrandbits(70)]
+        random.seed(1234)
+        r.restore(snap)
+        assert random.getstate() == want
+        assert [random.random(), random.gauss(0, 1), random.getrandbits(70)] == a
+        r.restore(want)  # getstate() tuples are accepted too
+        assert random.getstate() == want
+    finally:
+        random.setstate(st)
 
 
 def test_restore_accepts_legacy_tuples():

@@ -1,0 +1,101 @@
+"""Where a graph-mode step's wall time goes (no profiler: its serialisation distorts tiny kernels).
+
+Host phases of `env.step(env.get_random_actions())` by perf_counter stamps (monkeypatched around
+the StepGraph / Environment methods), and the GPU time of the replayed graph and of the action
+kernel by HIP events recorded on the stream around them (outside the graph).
+Usage: python tools/step_timeline.py [scenario] [envs]
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from vectorizedmultiagentsimulator_amd import make_env  # noqa: E402
+from vectorizedmultiagentsimulator_amd.simulator.environment import _graph  # noqa: E402
+from vectorizedmultiagentsimulator_amd.simulator.environment.environment import Environment  # noqa: E402
+
+scenario = sys.argv[1] if len(sys.argv) > 1 else "balance"
+n_envs = int(sys.argv[2]) if len(sys.argv) > 2 else 32768
+kw = {"n_agents": 8 if scenario in ("discovery", "flocking") else 4}
+env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, graph_step=True, **kw)
+if scenario == "balance":
+    env.world._substeps = 10
+    env.world._sub_dt = env.world._dt / 10
+for _ in range(10):
+    env.step(env.get_random_actions())
+assert env.graph_status == "graph", env.graph_reason
+
+stamps = {}
+events = []
+
+
+def stamp(name):
+    stamps.setdefault(name, []).append(time.perf_counter())
+
+
+def wrap(cls, meth, before, after):
+    orig = getattr(cls, meth)
+
+    def f(*a, **k):
+        stamp(before)
+        r = orig(*a, **k)
+        stamp(after)
+        return r
+
+    setattr(cls, meth, f)
+
+
+wrap(_graph.StepGraph, "before_actions", "before_actions0", "before_actions1")
+wrap(Environment, "_apply_continuous_actions", "apply0", "apply1")
+G = env._graph
+orig_replay = G.graph.replay
+
+
+def replay():
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    stamp("replay0")
+    orig_replay()
+    stamp("replay1")
+    e1.record()
+    events.append((e0, e1))
+
+
+G.graph.replay = replay
+wrap(_graph.StepGraph, "_clone_outputs", "clone0", "clone1")
+
+N = 100
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(N):
+    stamp("draw0")
+    a = env.get_random_actions()
+    stamp("draw1")
+    env.step(a)
+    stamp("step1")
+torch.cuda.synchronize()
+wall = (time.perf_counter() - t0) / N * 1e6
+
+
+def mean_us(a, b):
+    return sum(y - x for x, y in zip(stamps[a], stamps[b])) / len(stamps[a]) * 1e6
+
+
+gpu_graph = sum(e0.elapsed_time(e1) for e0, e1 in events) / len(events) * 1e3
+out = {
+    "scenario": scenario, "envs": n_envs, "wall_us_per_step": round(wall, 1),
+    "host_us": {
+        "draw_random_actions": round(mean_us("draw0", "draw1"), 1),
+        "step_before_actions": round(mean_us("before_actions0", "before_actions1"), 1),
+        "apply_actions_incl_wait": round(mean_us("apply0", "apply1"), 1),
+        "graph_replay_launch": round(mean_us("replay0", "replay1"), 1),
+        "clone_outputs": round(mean_us("clone0", "clone1"), 1),
+        "whole_step_call": round(mean_us("draw1", "step1"), 1),
+    },
+    "gpu_us": {"graph_replay": round(gpu_graph, 1)},
+    "nodes": None,
+}
+print(json.dumps(out), flush=True)

@@ -470,15 +470,38 @@ class StepGraph:
         self._asserts.after_replay(self.env.device)
         return out
 
-    def _clone_outputs(self):
-        """Fresh copies of the replay's outputs: one byte buffer, one multi-tensor copy kernel."""
+    def _clone_plan(self):
+        """Outputs grouped by (dtype, shape): per group one allocation [n, *shape] whose unbind
+        gives the n fresh tensors; per dtype one multi-tensor copy.  Built once per capture (the
+        replay's output tensors are fixed), so a step runs a handful of host calls instead of
+        several per output tensor."""
         ts = self._out_tensors
-        offs, total = [], 0
-        for t in ts:
-            offs.append(total)
-            total = (total + t.numel() * t.element_size() + 15) & ~15
-        flat = torch.empty(total, dtype=torch.uint8, device=ts[0].device)
-        dst = [flat[o: o + t.numel() * t.element_size()] for o, t in zip(offs, ts)]
-        torch._foreach_copy_(dst, [_bytes(t if t.is_contiguous() else t.contiguous()) for t in ts])
-        fresh = [d.view(t.dtype).view(t.shape) for d, t in zip(dst, ts)]
+        groups: Dict[Tuple[torch.dtype, Tuple[int, ...]], List[int]] = {}
+        for i, t in enumerate(ts):
+            groups.setdefault((t.dtype, tuple(t.shape)), []).append(i)
+        plan = []
+        by_dtype: Dict[torch.dtype, List[Tensor]] = {}
+        for (dt, shape), idx in groups.items():
+            plan.append((dt, shape, idx))
+            by_dtype.setdefault(dt, []).extend(ts[i] for i in idx)
+        self._clone_groups = plan
+        self._clone_src = by_dtype
+        self._clone_order = [i for _, _, idx in plan for i in idx]
+
+    def _clone_outputs(self):
+        """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
+        ts = self._out_tensors
+        if getattr(self, "_clone_src_of", None) is not ts:
+            self._clone_plan()
+            self._clone_src_of = ts
+        dev = ts[0].device
+        fresh: List[Optional[Tensor]] = [None] * len(ts)
+        dst: Dict[torch.dtype, List[Tensor]] = {}
+        for dt, shape, idx in self._clone_groups:
+            views = torch.empty((len(idx),) + shape, dtype=dt, device=dev).unbind(0)
+            dst.setdefault(dt, []).extend(views)
+            for i, v in zip(idx, views):
+                fresh[i] = v
+        for dt, srcs in self._clone_src.items():
+            torch._foreach_copy_(dst[dt], srcs)
         return _rebuild(self._out_tree, iter(fresh))

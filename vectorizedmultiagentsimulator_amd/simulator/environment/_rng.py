@@ -1,4 +1,4 @@
-"""Exact save/restore of numpy's process-global legacy RNG for ``local_seed``.
+"""Exact save/restore of numpy's and Python's process-global RNGs for ``local_seed``.
 
 The reference swaps the simulator's RNG states in and out around every ``Environment`` call
 (environment.py:30-46) with ``np.random.get_state()`` / ``set_state()``.  Those copy the 624-word
@@ -13,6 +13,11 @@ The same state is two pieces:
     back to ``get_state`` / ``set_state``.
 Both paths save and restore exactly what ``get_state`` / ``set_state`` do (tests/test_rng.py
 compares every draw against the reference's swap, gaussian cache included).
+
+Python's ``random.getstate()`` / ``setstate()`` build and parse a 625-int tuple (~14 + 6 us).
+``PythonGlobalRng`` does the same swap with one memmove of the C object's ``{int index; uint32_t
+state[624]}`` (located once by a probe, validated by round trips) plus the ``gauss_next``
+attribute; tuples from ``getstate()`` are still accepted by ``restore``.
 """
 from __future__ import annotations
 
@@ -94,7 +99,78 @@ class NumpyGlobalRng:
         ctypes.c_double.from_address(base + 8).value = g
 
 
+class PythonGlobalRng:
+    """The same for ``random``'s module-level generator (``random._inst``)."""
+
+    _WORDS = 624
+
+    def __init__(self):
+        import random
+
+        self.random = random
+        self.inst = random._inst
+        self.fast = False
+        try:
+            self.off = self._find_state()
+            self.fast = self.off is not None and self._validate()
+        except Exception:
+            self.fast = False
+
+    def _find_state(self):
+        r = self.random
+        st = r.getstate()
+        try:
+            key = tuple((0x9E3779B9 * (i + 7) + 0x7F4A7C15) & 0xFFFFFFFF for i in range(self._WORDS))
+            r.setstate((st[0], key + (self._WORDS,), None))
+            pattern = np.array(key, dtype=np.uint32).tobytes()
+            mem = ctypes.string_at(id(self.inst), self.inst.__sizeof__())  # the object, no GC header
+            at = mem.find(pattern)
+            if at < 4 or mem.find(pattern, at + 1) != -1:
+                return None
+            if ctypes.c_int32.from_address(id(self.inst) + at - 4).value != self._WORDS:
+                return None
+            return at - 4  # {int index; uint32_t state[624]}
+        finally:
+            r.setstate(st)
+
+    def _validate(self) -> bool:
+        r = self.random
+        st = r.getstate()
+        try:
+            for seed, n, g in ((1, 3, None), (2, 0, 0.25), (3, 700, -1.5)):
+                r.seed(seed)
+                for _ in range(n):
+                    r.random()
+                self.inst.gauss_next = g
+                snap = self.snapshot()
+                want = r.getstate()
+                r.seed(seed + 100)
+                r.random()
+                self.restore(snap)
+                if r.getstate() != want:
+                    return False
+            return True
+        finally:
+            r.setstate(st)
+
+    def snapshot(self):
+        if not self.fast:
+            return self.random.getstate()
+        buf = ctypes.create_string_buffer(4 + 4 * self._WORDS)
+        ctypes.memmove(buf, id(self.inst) + self.off, 4 + 4 * self._WORDS)
+        return buf, self.inst.gauss_next
+
+    def restore(self, snap) -> None:
+        if isinstance(snap, tuple) and len(snap) == 3:  # a random.getstate() tuple
+            self.random.setstate(snap)
+            return
+        buf, g = snap
+        ctypes.memmove(id(self.inst) + self.off, buf, 4 + 4 * self._WORDS)
+        self.inst.gauss_next = g
+
+
 _instance = None
+_py_instance = None
 
 
 def numpy_global_rng() -> NumpyGlobalRng:
@@ -102,3 +178,10 @@ def numpy_global_rng() -> NumpyGlobalRng:
     if _instance is None:
         _instance = NumpyGlobalRng()
     return _instance
+
+
+def python_global_rng() -> PythonGlobalRng:
+    global _py_instance
+    if _py_instance is None:
+        _py_instance = PythonGlobalRng()
+    return _py_instance

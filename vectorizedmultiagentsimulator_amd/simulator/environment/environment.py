@@ -25,29 +25,30 @@ from ..core import Agent, TorchVectorizedObject
 from ..scenario import BaseScenario
 from ..utils import AGENT_OBS_TYPE, DEVICE_TYPING, TorchUtils, override
 from . import spaces
-from ._rng import numpy_global_rng
+from ._rng import numpy_global_rng, python_global_rng
 
 
 @contextlib.contextmanager
 def local_seed(vmas_random_state):
     """Swap in the simulator's RNG states for torch(CPU)/numpy/python (environment.py:30-46).
 
-    The numpy state is saved/restored by ``_rng.NumpyGlobalRng`` (the same state as
-    get_state/set_state, without their element-wise key copies)."""
-    npr = numpy_global_rng()
+    The numpy and Python states are saved/restored by ``_rng.NumpyGlobalRng`` /
+    ``PythonGlobalRng`` (the same states as get_state/set_state and getstate/setstate, without
+    their element-wise key copies)."""
+    npr, pyr = numpy_global_rng(), python_global_rng()
     torch_state = torch.random.get_rng_state()
     np_state = npr.snapshot()
-    py_state = random.getstate()
+    py_state = pyr.snapshot()
     torch.random.set_rng_state(vmas_random_state[0])
     npr.restore(vmas_random_state[1])
-    random.setstate(vmas_random_state[2])
+    pyr.restore(vmas_random_state[2])
     yield
     vmas_random_state[0] = torch.random.get_rng_state()
     vmas_random_state[1] = npr.snapshot()
-    vmas_random_state[2] = random.getstate()
+    vmas_random_state[2] = pyr.snapshot()
     torch.random.set_rng_state(torch_state)
     npr.restore(np_state)
-    random.setstate(py_state)
+    pyr.restore(py_state)
 
 
 def _f32(x) -> float:
@@ -230,12 +231,49 @@ class Environment(TorchVectorizedObject):
         random.seed(seed)
         return [seed]
 
-    @local_seed(vmas_random_state)
     def step(self, actions: Union[List, Dict]):
         """Performs a vectorized step on all sub environments using ``actions``.
 
         Returns obs, rewards, dones, infos (or obs, rewards, terminated, truncated, infos).
+
+        The reference swaps the simulator's host RNG states (torch CPU / numpy / python) in and
+        out around the step (local_seed).  A replayed graph step runs no host RNG code -- its
+        random numbers come from the device generator, and per-step host randomness is frozen at
+        capture (graph mode's documented requirement) -- so the swap is a no-op there and is
+        skipped; an exception raised there leaves the simulator's states swapped in, as the
+        reference's swap does (its restore is not in a finally).
         """
+        g = self._graph
+        if g is not None and g.graph is not None and self.continuous_actions:
+            try:
+                actions = self._check_action_list(actions)
+                g.before_actions()
+                if g.graph is not None and self._apply_continuous_actions(actions, persistent=True):
+                    return g.step()
+            except BaseException:
+                self._swap_in_simulator_rng()
+                raise
+            return self._step_seeded(actions, prepared=True)
+        return self._step_seeded(actions)
+
+    def _swap_in_simulator_rng(self):
+        s = Environment.vmas_random_state
+        torch.random.set_rng_state(s[0])
+        numpy_global_rng().restore(s[1])
+        python_global_rng().restore(s[2])
+
+    @local_seed(vmas_random_state)
+    def _step_seeded(self, actions, prepared: bool = False):
+        if not prepared:
+            actions = self._check_action_list(actions)
+            if self._graph is not None and self.continuous_actions:
+                self._graph.before_actions()
+        if self._graph is not None and self.continuous_actions:
+            if self._apply_continuous_actions(actions, persistent=True):
+                return self._graph.step()
+        return self._step_eager(actions)
+
+    def _check_action_list(self, actions):
         if isinstance(actions, Dict):
             actions_dict = actions
             actions = []
@@ -262,10 +300,9 @@ class Environment(TorchVectorizedObject):
                 f"Action for agent {self.agents[i].name} has shape {actions[i].shape[1]},"
                 f" but should have shape {self.get_agent_action_size(self.agents[i])}"
             )
-        if self._graph is not None and self.continuous_actions:
-            self._graph.before_actions()
-            if self._apply_continuous_actions(actions, persistent=True):
-                return self._graph.step()
+        return actions
+
+    def _step_eager(self, actions):
         if not (self.continuous_actions and self._apply_continuous_actions(actions)):
             if self.continuous_actions:
                 self._validate_continuous_actions(actions)
@@ -364,11 +401,12 @@ class Environment(TorchVectorizedObject):
             # the stack kernel (checked once per device: _column_draws)
             n_c = self.world.dim_c if (self.world.dim_c != 0 and not agent.silent) else 0
             out = torch.empty(agent.batch_dim, agent.action_size + n_c, device=agent.device, dtype=torch.float32)
+            cols = out.unbind(1)
             for action_index in range(agent.action_size):
                 r = self._u_range_value(agent, action_index)
-                out[:, action_index].uniform_(-r, r)
+                cols[action_index].uniform_(-r, r)
             for k in range(n_c):
-                out[:, agent.action_size + k].uniform_(0, 1)
+                cols[agent.action_size + k].uniform_(0, 1)
             return out
         if self.continuous_actions:
             actions = []
@@ -393,12 +431,19 @@ class Environment(TorchVectorizedObject):
             return torch.stack(actions, dim=-1)
         return torch.randint(low=0, high=action_space.n, size=(agent.batch_dim,), device=agent.device)
 
-    @local_seed(vmas_random_state)
     def get_random_actions(self) -> Sequence[torch.Tensor]:
-        """Random actions for all agents.  The reference swaps the RNG states once per agent
-        (environment.py:584-606); swapping once around the loop draws the identical streams.
+        """Random actions for all agents.  The reference swaps the host RNG states once per
+        agent (environment.py:584-606); swapping once around the loop draws the identical
+        streams.  Continuous actions on a GPU are drawn from the device generator only, which
+        local_seed does not swap: the swap of the host states is a no-op there and is skipped.
         (Drawing them on a side stream, overlapped with the previous step's graph, measured
         slower: 87-98 M vs 106-119 M env-steps/s, interleaved runs on one MI355X.)"""
+        if self.continuous_actions and self.device.type == "cuda":
+            return [self._random_action(agent) for agent in self.agents]
+        return self._random_actions_seeded()
+
+    @local_seed(vmas_random_state)
+    def _random_actions_seeded(self) -> Sequence[torch.Tensor]:
         return [self._random_action(agent) for agent in self.agents]
 
     _COLUMN_DRAWS: Dict[str, bool] = {}
