@@ -276,6 +276,13 @@ typedef struct VmasActionApplyRef {
 
 int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyRef* refs,
                            int32_t n_refs, float* out, uint8_t* flags, void* stream);
+/* The same split in two (GPU only, n_refs <= 8): _launch enqueues the kernel and returns the
+ * sequence number it will publish; _flags waits for it and fills flags as above.  Graph mode
+ * launches the replay between the two and rolls the step back when a flag is set. */
+int32_t vmas_apply_actions_launch(int32_t device, int32_t batch, const VmasActionApplyRef* refs,
+                                  int32_t n_refs, float* out, uint32_t* seq, void* stream);
+int32_t vmas_apply_actions_flags(int32_t device, uint32_t seq, int32_t n_refs, uint8_t* flags,
+                                 void* stream);
 
 /* Deferred device assertions for graph mode (csrc/vmas_actions.hip).  Replaces the host sync of
  * a reference assert on a device tensor inside the step -- Agent.action_callback's range check of

@@ -103,29 +103,91 @@ def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
         assert graph._graph.replays >= 5
 
 
+def _twin_envs(gpu_device, name, **kw):
+    envs = []
+    for graph in (False, True):
+        saved = _rng_save()
+        envs.append(make_env(name, num_envs=256, device=gpu_device, seed=0, graph_step=graph, **kw))
+        if not graph:
+            _rng_load(saved)
+    return envs
+
+
+def _step_both(eager, graph, actions, expect_raise=None):
+    outs = []
+    for env in (eager, graph):
+        s = _rng_save()
+        if expect_raise is not None:
+            with pytest.raises(AssertionError, match=expect_raise):
+                env.step([a.clone() for a in actions])
+            outs.append(None)
+        else:
+            outs.append(env.step([a.clone() for a in actions]))
+        if env is eager:
+            _rng_load(s)
+    return outs
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("graph_step", [False, True], ids=["eager", "graph"])
-def test_scripted_action_assert_raised_from_step_gpu(gpu_device, graph_step):
+def test_scripted_action_assert_raised_from_step_gpu(gpu_device):
     """A scripted agent's out-of-range action (core.py:977-980) raises from the step() that
-    computed it, eagerly and from a replayed graph (where the check runs on the device)."""
-    env = make_env("flocking", num_envs=256, device=gpu_device, seed=0, graph_step=graph_step, n_agents=3)
+    computed it, eagerly and from a replayed graph (where the check runs on the device); the
+    replayed step is rolled back, so both worlds continue identically."""
+    eager, graph = _twin_envs(gpu_device, "flocking", n_agents=3)
     scale = torch.ones(1, device=gpu_device)
-    sc = env.scenario
+    for env in (eager, graph):
+        sc = env.scenario
 
-    def script(agent, world):
-        t = sc.t / 30
-        agent.action.u = torch.stack([torch.cos(t), torch.sin(t)], dim=1) * scale
+        def script(agent, world, sc=sc):
+            t = sc.t / 30
+            agent.action.u = torch.stack([torch.cos(t), torch.sin(t)], dim=1) * scale
 
-    sc._target._action_script = script
+        sc._target._action_script = script
     for _ in range(5):
-        env.step(env.get_random_actions())
-    if graph_step:
-        assert env.graph_status == "graph", env.graph_reason
+        _step_both(eager, graph, eager.get_random_actions())
+    assert graph.graph_status == "graph", graph.graph_reason
     scale.fill_(2.0)  # read by the captured step: |u| = 2|cos t| > u_range 1 in most envs
-    with pytest.raises(AssertionError, match="Scripted physical action of target is out of range"):
-        env.step(env.get_random_actions())
+    _step_both(eager, graph, eager.get_random_actions(), "Scripted physical action of target is out of range")
+    _assert_same(_state(eager), _state(graph), "state after the failed step")
+    assert torch.equal(eager.scenario.t, graph.scenario.t)
     scale.fill_(1.0)
-    env.step(env.get_random_actions())  # the channel keeps working after a raise
+    for t in range(3):  # the channel keeps working and the worlds stay identical
+        out_e, out_g = _step_both(eager, graph, eager.get_random_actions())
+        _assert_same(out_e, out_g, f"outputs after the failed step {t}")
+        _assert_same(_state(eager), _state(graph), f"state after the failed step {t}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad", ["nan", "range"])
+@pytest.mark.parametrize("speculative", [False, True], ids=["wait", "speculative"])
+def test_failed_action_check_leaves_world_as_eager_gpu(gpu_device, monkeypatch, bad, speculative):
+    """A NaN / out-of-range action raises the reference's AssertionError and leaves the world as
+    the eager step leaves it -- also when the replay was launched before the action flags were
+    known (speculative, rolled back, where the agents' u are exact too: the agents before the
+    failing one hold their new u, the rest their old one)."""
+    monkeypatch.setattr(Environment, "_SPECULATE", speculative)
+    eager, graph = _twin_envs(gpu_device, "balance", n_agents=4)
+    for _ in range(5):
+        _step_both(eager, graph, eager.get_random_actions())
+    assert graph.graph_status == "graph", graph.graph_reason
+    before_u = [a.action.u.clone() for a in graph.agents]
+    actions = eager.get_random_actions()
+    actions[2][5, 1] = float("nan") if bad == "nan" else 3.0
+    _step_both(eager, graph, actions, "" if bad == "nan" else "out of its range")
+    _assert_same(_state(eager), _state(graph), "state after the failed step")
+    for i, (ae, ag) in enumerate(zip(eager.agents, graph.agents)):
+        if i < 2 or speculative:  # (documented: without speculation the failing agent and those
+            # after it hold the rejected actions in their persistent u, until the next step)
+            assert torch.equal(ae.action.u, ag.action.u), i
+        if i >= 2 and speculative:
+            assert torch.equal(ag.action.u, before_u[i]), i
+    assert torch.equal(eager.steps, graph.steps)
+    for t in range(4):
+        out_e, out_g = _step_both(eager, graph, eager.get_random_actions())
+        _assert_same(out_e, out_g, f"outputs after the failed step {t}")
+        _assert_same(_state(eager), _state(graph), f"state after the failed step {t}")
+    assert graph.graph_status == "graph"
+    assert graph._can_speculate() == speculative
 
 
 @pytest.mark.gpu
@@ -206,7 +268,9 @@ def test_graph_kernel_timing_gpu(gpu_device):
     ev_ms, ev_n = e2.get_timing(reset=True)
     dt_ms, dt_n = e2.device_timing(reset=True)
     assert ev_n == dt_n == 5
-    assert 0.7 * ev_ms < dt_ms <= 1.05 * ev_ms, (ev_ms, dt_ms)
+    # the in-kernel window misses the launch ramp and the exit tail: up to ~7 us of a ~15 us
+    # one-substep launch
+    assert 0.5 * ev_ms < dt_ms <= 1.05 * ev_ms, (ev_ms, dt_ms)
 
 
 def test_trial_step_detects_host_waits():

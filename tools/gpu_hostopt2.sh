@@ -1,0 +1,6 @@
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out/hostopt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_graph.py tests/test_rng.py -m gpu -p no:cacheprovider > gpurun_out/hostopt/pytest2.log 2>&1; rc=$?; tail -3 gpurun_out/hostopt/pytest2.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python tools/step_timeline.py balance > gpurun_out/hostopt/tl_balance2.json && cat gpurun_out/hostopt/tl_balance2.json || exit 1
+bash tools/ab_speculative.sh

@@ -96,6 +96,7 @@ out = {
         "whole_step_call": round(mean_us("draw1", "step1"), 1),
     },
     "gpu_us": {"graph_replay": round(gpu_graph, 1)},
-    "nodes": None,
+    "inplace_backed_up": [list(t.shape) for t in G._inplace],
+    "speculative": bool(env._can_speculate()),
 }
 print(json.dumps(out), flush=True)

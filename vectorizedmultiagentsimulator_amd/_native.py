@@ -62,6 +62,8 @@ EXPORTED_SYMBOLS = (
     "vmas_distance",
     "vmas_check_actions",
     "vmas_apply_actions",
+    "vmas_apply_actions_launch",
+    "vmas_apply_actions_flags",
     "vmas_assert_create",
     "vmas_assert_destroy",
     "vmas_assert_publish",
@@ -325,6 +327,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_check_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp]
     lib.vmas_apply_actions.restype = _i32
     lib.vmas_apply_actions.argtypes = [_i32, _i32, _vp, _i32, _vp, _vp, _vp]
+    lib.vmas_apply_actions_launch.restype = _i32
+    lib.vmas_apply_actions_launch.argtypes = [_i32, _i32, _vp, _i32, _vp, ctypes.POINTER(ctypes.c_uint32), _vp]
+    lib.vmas_apply_actions_flags.restype = _i32
+    lib.vmas_apply_actions_flags.argtypes = [_i32, ctypes.c_uint32, _i32, _vp, _vp]
     lib.vmas_assert_create.restype = _i32
     lib.vmas_assert_create.argtypes = [_i32, _i32, ctypes.POINTER(_vp)]
     lib.vmas_assert_destroy.restype = _i32

@@ -102,6 +102,40 @@ struct DevState {
 DevState g_dev[64];
 std::mutex g_mu;
 
+int32_t dev_init(DevState& d) {
+    if (d.slots) return VMAS_OK;
+    VMAS_AUX_HIP(hipMalloc((void**)&d.slots, kMaxRefsPerLaunch * kMaxBlocksPerRef * 4));
+    VMAS_AUX_HIP(hipMalloc((void**)&d.counter, 4));
+    VMAS_AUX_HIP(hipMemset(d.counter, 0, 4));
+    VMAS_AUX_HIP(hipHostMalloc((void**)&d.hsig, 8, hipHostMallocMapped | hipHostMallocCoherent));
+    VMAS_AUX_HIP(hipHostGetDevicePointer((void**)&d.dsig, d.hsig, 0));
+    *d.hsig = 0u;
+    return VMAS_OK;
+}
+
+// One launch over n <= kMaxRefsPerLaunch refs; returns the sequence number it publishes.
+uint32_t launch_apply(DevState& d, int batch, const VmasActionApplyRef* refs, int n, float* out, hipStream_t st) {
+    ApplyArgs a{};
+    long max_elems = 0;
+    for (int i = 0; i < n; ++i) {
+        a.r[i] = refs[i];
+        max_elems = std::max(max_elems, (long)batch * refs[i].n_cols);
+    }
+    const int gx = (int)std::max(1L, std::min((long)kMaxBlocksPerRef, (max_elems + kThreads * kPerThread - 1) /
+                                                                           (kThreads * kPerThread)));
+    a.out = out;
+    a.slots = d.slots;
+    a.counter = d.counter;
+    a.hsig = d.dsig;
+    a.seq = ++d.seq;
+    if (a.seq == 0u) a.seq = ++d.seq;  // 0 is the "nothing published" value
+    a.B = batch;
+    a.n = n;
+    a.gx = gx;
+    hipLaunchKernelGGL(k_apply_actions, dim3(gx, n), dim3(kThreads), 0, st, a);
+    return a.seq;
+}
+
 // Deferred assertion of one slot: AND of n condition bytes, published with the slot's next epoch.
 __global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int64_t n, uint32_t* epoch,
                                                         uint64_t* hsig) {
@@ -132,6 +166,39 @@ struct VmasDeviceAssert {
 
 extern "C" {
 
+int32_t vmas_apply_actions_launch(int32_t device, int32_t batch, const VmasActionApplyRef* refs, int32_t n_refs,
+                                  float* out, uint32_t* seq, void* stream) {
+    if (device < 0 || device >= 64 || n_refs <= 0 || n_refs > kMaxRefsPerLaunch || batch <= 0 || !refs || !out || !seq)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_launch: bad arguments");
+    for (int i = 0; i < n_refs; ++i)
+        if (!refs[i].u || !refs[i].u_range || !refs[i].u_mult || refs[i].n_phys > refs[i].n_cols ||
+            refs[i].n_phys < 0 || refs[i].out_offset < 0)
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_launch: bad ref %d", i);
+    std::lock_guard<std::mutex> lk(g_mu);
+    int cur = -1;
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
+    DevState& d = g_dev[device];
+    if (int32_t rc = dev_init(d)) return rc;
+    *seq = launch_apply(d, batch, refs, n_refs, out, (hipStream_t)stream);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_apply_actions_flags(int32_t device, uint32_t seq, int32_t n_refs, uint8_t* flags, void* stream) {
+    if (device < 0 || device >= 64 || n_refs <= 0 || n_refs > kMaxRefsPerLaunch || !flags || seq == 0u)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_flags: bad arguments");
+    DevState& d = g_dev[device];
+    if (!d.hsig) return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_flags: nothing launched");
+    uint64_t v = 0;
+    if (int32_t rc = vmas_aux::wait_host_word64(d.hsig, seq, &v, (hipStream_t)stream)) return rc;
+    for (int i = 0; i < n_refs; ++i) {
+        flags[2 * i] = (v >> (2 * i)) & 1u;
+        flags[2 * i + 1] = (v >> (2 * i + 1)) & 1u;
+    }
+    return VMAS_OK;
+}
+
 int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyRef* refs, int32_t n_refs,
                            float* out, uint8_t* flags, void* stream) {
     if (n_refs <= 0 || batch <= 0) return VMAS_OK;
@@ -156,38 +223,14 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
     VMAS_AUX_HIP(hipGetDevice(&cur));
     if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
     DevState& d = g_dev[device];
-    if (!d.slots) {
-        VMAS_AUX_HIP(hipMalloc((void**)&d.slots, kMaxRefsPerLaunch * kMaxBlocksPerRef * 4));
-        VMAS_AUX_HIP(hipMalloc((void**)&d.counter, 4));
-        VMAS_AUX_HIP(hipMemset(d.counter, 0, 4));
-        VMAS_AUX_HIP(hipHostMalloc((void**)&d.hsig, 8, hipHostMallocMapped | hipHostMallocCoherent));
-        VMAS_AUX_HIP(hipHostGetDevicePointer((void**)&d.dsig, d.hsig, 0));
-        *d.hsig = 0u;
-    }
+    if (int32_t rc = dev_init(d)) return rc;
     hipStream_t st = (hipStream_t)stream;
     for (int first = 0; first < n_refs; first += kMaxRefsPerLaunch) {
         const int n = std::min(kMaxRefsPerLaunch, n_refs - first);
-        ApplyArgs a{};
-        long max_elems = 0;
-        for (int i = 0; i < n; ++i) {
-            a.r[i] = refs[first + i];
-            max_elems = std::max(max_elems, (long)batch * refs[first + i].n_cols);
-        }
-        const int gx = (int)std::max(1L, std::min((long)kMaxBlocksPerRef, (max_elems + kThreads * kPerThread - 1) /
-                                                                               (kThreads * kPerThread)));
-        a.out = out;
-        a.slots = d.slots;
-        a.counter = d.counter;
-        a.hsig = d.dsig;
-        a.seq = ++d.seq;
-        if (a.seq == 0u) a.seq = ++d.seq;  // 0 is the "nothing published" value
-        a.B = batch;
-        a.n = n;
-        a.gx = gx;
-        hipLaunchKernelGGL(k_apply_actions, dim3(gx, n), dim3(kThreads), 0, st, a);
+        const uint32_t seq = launch_apply(d, batch, refs + first, n, out, st);
         VMAS_AUX_HIP(hipGetLastError());
         uint64_t v = 0;
-        if (int32_t rc = vmas_aux::wait_host_word64(d.hsig, a.seq, &v, st)) return rc;
+        if (int32_t rc = vmas_aux::wait_host_word64(d.hsig, seq, &v, st)) return rc;
         for (int i = 0; i < n; ++i) {
             flags[2 * (first + i)] = (v >> (2 * i)) & 1u;
             flags[2 * (first + i) + 1] = (v >> (2 * i + 1)) & 1u;

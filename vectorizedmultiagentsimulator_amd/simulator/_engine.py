@@ -70,6 +70,20 @@ def _check_grad(tensors) -> None:
                 )
 
 
+_DEFERRED: list = []  # (destroy function, handle) of engines collected during a stream capture
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def drain_deferred() -> None:
+    """Destroys the engines whose collection fell into a stream capture (call outside one)."""
+    while _DEFERRED and not _capturing():
+        f, h = _DEFERRED.pop()
+        f(h)
+
+
 class PhysicsEngine:
     def __init__(self, world):
         self.world = world
@@ -102,10 +116,15 @@ class PhysicsEngine:
 
     def __del__(self):
         try:
-            if self._handle is not None:
-                self.lib.vmas_world_destroy(self._handle)
-            if self._jit is not None:
-                self.lib.vmas_jit_world_destroy(self._jit)
+            handles = [(self.lib.vmas_world_destroy, self._handle), (self.lib.vmas_jit_world_destroy, self._jit)]
+            handles = [(f, h) for f, h in handles if h is not None]
+            if handles and _capturing():
+                # the garbage collector can run this while a graph-mode step is being captured:
+                # freeing device memory then aborts the process, so it waits for drain_deferred()
+                _DEFERRED.extend(handles)
+                return
+            for f, h in handles:
+                f(h)
         except Exception:
             pass
 

@@ -28,8 +28,10 @@ What a replay must honour, and how:
   * Outputs.  The returned observations / rewards / dones / infos are fresh copies (the
     reference clones them too), made by one multi-tensor copy per dtype after the replay.
   * Asserts on device tensors inside the step (a scripted agent's action range check,
-    core.py:977-980) are captured as device checks (``_DeviceAsserts``) and raised from the
-    same step() call after the replay.
+    core.py:977-980) are captured as device checks (``_DeviceAsserts``); a failed one rolls the
+    replayed step back -- the tensors the step modifies in place (found by version counters at
+    capture) from a per-step backup, the carried tensors from their pre-step copies, the device
+    generator -- and raises from the same step() call.
   * What cannot be captured -- a host sync inside the step (``.item()``, ``bool(t.any())``,
     the spawn sampler's rejection loop), a host-to-device copy
     of pageable memory, discrete or communication actions -- makes the capture fail; the
@@ -43,6 +45,7 @@ What a replay must honour, and how:
 from __future__ import annotations
 
 import ctypes
+import gc
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -169,15 +172,23 @@ class _DeviceAsserts:
     publishes the condition with a per-replay epoch into mapped host memory; after a replay the
     host waits for every slot's word of that replay (the kernels run at the start of the graph,
     so the wait overlaps the rest of it) and raises the reference's AssertionError, in order,
-    from the same step() call.  Unlike the eager step, the replay's physics has then already run."""
+    from the same step() call, after rolling the replayed step back (StepGraph._rollback: the
+    world is left as the eager step leaves it when the assert fires)."""
 
     MAX_SLOTS = 64
+    # channels of dropped graphs: freed at the next creation (outside any capture), never from
+    # __del__, which the garbage collector may run while another env's step is being captured
+    # (freeing device / pinned memory during a capture aborts the process)
+    _graveyard: List[ctypes.c_void_p] = []
 
     def __init__(self, dev):
         from ... import _native as N
 
         self.N = N
         self.lib = N.load_library()
+        if not torch.cuda.is_current_stream_capturing():
+            while _DeviceAsserts._graveyard:
+                self.lib.vmas_assert_destroy(_DeviceAsserts._graveyard.pop())
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
         h = ctypes.c_void_p()
         N.check_aux(self.lib.vmas_assert_create(idx, self.MAX_SLOTS, ctypes.byref(h)), "vmas_assert_create")
@@ -198,24 +209,27 @@ class _DeviceAsserts:
         self.keep.append(ok)
         self.msgs.append(msg)
 
-    def after_replay(self, dev):
+    def after_replay(self, dev, raise_: bool = True):
+        """Waits for this replay's words; raises the first violated assert (raise_) or only keeps
+        the sequence in step (a replay that is rolled back for another reason)."""
         if not self.msgs:
             return
         self.seq = (self.seq + 1) & 0xFFFFFFFF or 1
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         bad = ctypes.c_int32(0)
+        first = None
         for slot, msg in enumerate(self.msgs):
             self.N.check_aux(self.lib.vmas_assert_wait(self.h, slot, self.seq, ctypes.byref(bad), stream),
                              "vmas_assert_wait")
-            assert not bad.value, msg
+            if bad.value and first is None:
+                first = msg
+        if raise_:
+            assert first is None, first
 
     def __del__(self):
         h, self.h = getattr(self, "h", None), None
         if h is not None and h.value:
-            try:
-                self.lib.vmas_assert_destroy(h)
-            except Exception:  # noqa: BLE001 -- interpreter shutdown
-                pass
+            _DeviceAsserts._graveyard.append(h)
 
 
 def _reset_generator_capture_state(dev):
@@ -247,6 +261,10 @@ class StepGraph:
         self._watch: List[Tuple[dict, str, Tensor]] = []  # (obj.__dict__, key, bound tensor)
         self._first_replay = True
         self._asserts: Optional[_DeviceAsserts] = None
+        self._inplace: List[Tensor] = []
+        self._bk_src: List[Tensor] = []
+        self._bk_dst: List[Tensor] = []
+        self._bk_u: Optional[Tensor] = None
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -351,14 +369,30 @@ class StepGraph:
         eng = env.world.engine
         objs = _tracked_objects(env)
         snap = [(o, dict(o.__dict__)) for o in objs]
+        # version counters of every tracked tensor: those the step modifies in place are what a
+        # speculative replay has to back up (see replay_speculative)
+        versions = {}
+        for _, d in snap:
+            for v in d.values():
+                if isinstance(v, Tensor):
+                    versions[id(v)] = (v, v._version)
         dev = env.device
         rng = torch.cuda.get_rng_state(dev)
         g = torch.cuda.CUDAGraph()
         consts = _CapturableConstants()
         side = torch.cuda.Stream(dev)
         prev_stream = torch.cuda.current_stream(dev)
+        from .. import _engine
+
+        _engine.drain_deferred()  # engines collected during an earlier capture
         env._raw_outputs = True
         asserts = _DeviceAsserts(dev)
+        # No garbage collection inside the capture: a finalizer run there (another env's graph,
+        # engine or device buffers) would free device memory while the stream is captured, which
+        # aborts the process.  Collect now, then keep the collector off until the capture ends.
+        gc.collect()
+        gc_was_on = gc.isenabled()
+        gc.disable()
         try:
             env.world._assert_sink = asserts.capture_sink
             with torch.cuda.graph(g, stream=side), consts:
@@ -367,6 +401,10 @@ class StepGraph:
             self._asserts = asserts
             self._sig = eng.graph_token()
             self._plan(objs, snap, out)
+            self._inplace = [t for t, v in versions.values() if t._version != v]
+            self._bk_src: List[Tensor] = []
+            self._bk_dst: List[Tensor] = []
+            self._bk_u = None
         except Exception as ex:  # noqa: BLE001 -- any capture failure means "stay eager"
             from ... import _native as N
 
@@ -387,6 +425,8 @@ class StepGraph:
             self.graph = None
             return False
         finally:
+            if gc_was_on:
+                gc.enable()
             env._raw_outputs = False
             env.world._assert_sink = None
         self.graph = g
@@ -463,30 +503,117 @@ class StepGraph:
 
     # ---- replay ---------------------------------------------------------------------------------
     def _replay(self):
+        asserts = self._asserts is not None and bool(self._asserts.msgs)
+        if asserts:  # a failed device assert rolls the step back: back up what it modifies in place
+            self.backup(None)
+            rng = torch.cuda.get_rng_state(self.env.device)
         self._first_replay = False
         self.graph.replay()
         self.replays += 1
         out = self._clone_outputs()
-        self._asserts.after_replay(self.env.device)
+        if asserts:
+            try:
+                self._asserts.after_replay(self.env.device)
+            except AssertionError:
+                self._rollback(rng, restore_actions=False)
+                raise
         return out
+
+    # ---- speculative replay ---------------------------------------------------------------------
+    def backup(self, u_buf: Optional[Tensor]):
+        """Copies of the tensors the step modifies in place (found by version counters at
+        capture) -- and, before the action kernel of a speculative step, of the persistent action
+        buffer -- so that a step can be undone (one multi-tensor copy kernel)."""
+        if not self._bk_dst or (u_buf is not None and self._bk_u is not u_buf):
+            self._bk_src = [*self._inplace] + ([u_buf] if u_buf is not None else [])
+            self._bk_dst = [torch.empty_like(t) for t in self._bk_src]
+            self._bk_u = u_buf
+        n = len(self._bk_src) if u_buf is not None else len(self._inplace)
+        if n:
+            with torch.no_grad():
+                torch._foreach_copy_(self._bk_dst[:n], self._bk_src[:n])
+
+    def replay_speculative(self, flags_ok):
+        """Replays the step while the action kernel's flags are still in flight, then waits for
+        them (flags_ok(): the host wait of the eager path, now overlapping the replay).  Passing
+        flags: the replay's outputs, as _replay.  A failed flag: the step is rolled back -- the
+        in-place-modified tensors and the action buffer from the backup, then every carried
+        tensor from its pre-step copy, the device generator state -- and None is returned (the
+        caller then raises the reference's AssertionError through the eager action check).  A
+        scripted agent's failed assert rolls back everything but the policy agents' actions
+        (set, as in the reference, before the scripted agents act) and raises."""
+        dev = self.env.device
+        rng = torch.cuda.get_rng_state(dev)
+        self._first_replay = False
+        self.graph.replay()
+        self.replays += 1
+        out = self._clone_outputs()
+        if not flags_ok():
+            self._asserts.after_replay(dev, raise_=False)
+            self._rollback(rng, restore_actions=True)
+            return None
+        try:
+            self._asserts.after_replay(dev)
+        except AssertionError:
+            self._rollback(rng, restore_actions=False)
+            raise
+        return out
+
+    def _rollback(self, rng: Tensor, restore_actions: bool):
+        n = len(self._bk_src) if restore_actions else len(self._inplace)
+        with torch.no_grad():
+            if n:
+                torch._foreach_copy_(self._bk_src[:n], self._bk_dst[:n])
+            if self._carry_dst:  # carried tensors: Y <- X (X holds the pre-step values)
+                torch._foreach_copy_(self._carry_src, self._carry_dst)
+            for x, y in self._carry_other:
+                y.copy_(x)
+        torch.cuda.set_rng_state(rng, self.env.device)
 
     def _clone_plan(self):
         """Outputs grouped by (dtype, shape): per group one allocation [n, *shape] whose unbind
-        gives the n fresh tensors; per dtype one multi-tensor copy.  Built once per capture (the
-        replay's output tensors are fixed), so a step runs a handful of host calls instead of
-        several per output tensor."""
+        gives the n fresh tensors; per dtype one multi-tensor copy; the result tree rebuilt by a
+        function generated for its structure.  Built once per capture (the replay's output tensors
+        are fixed), so a step makes a handful of host calls instead of several per output."""
         ts = self._out_tensors
         groups: Dict[Tuple[torch.dtype, Tuple[int, ...]], List[int]] = {}
         for i, t in enumerate(ts):
             groups.setdefault((t.dtype, tuple(t.shape)), []).append(i)
-        plan = []
-        by_dtype: Dict[torch.dtype, List[Tensor]] = {}
-        for (dt, shape), idx in groups.items():
-            plan.append((dt, shape, idx))
-            by_dtype.setdefault(dt, []).extend(ts[i] for i in idx)
-        self._clone_groups = plan
-        self._clone_src = by_dtype
-        self._clone_order = [i for _, _, idx in plan for i in idx]
+        plan = sorted(groups.items(), key=lambda kv: str(kv[0][0]))  # same dtypes adjacent
+        self._clone_groups = [(dt, shape, len(idx)) for (dt, shape), idx in plan]
+        order = [i for _, idx in plan for i in idx]  # position in the concatenated views -> output
+        pos = {i: p for p, i in enumerate(order)}
+        spans, start = [], 0
+        for (dt, _), idx in plan:
+            if spans and spans[-1][0] == dt:
+                spans[-1] = (dt, spans[-1][1], start + len(idx))
+            else:
+                spans.append((dt, start, start + len(idx)))
+            start += len(idx)
+        self._clone_spans = [(lo, hi, [ts[order[p]] for p in range(lo, hi)]) for _, lo, hi in spans]
+        consts: List[Any] = []
+        counter = [0]
+
+        def expr(t):
+            if isinstance(t, Tensor):
+                counter[0] += 1
+                return f"v[{pos[counter[0] - 1]}]"
+            if isinstance(t, list):
+                return "[" + ", ".join(expr(x) for x in t) + "]"
+            if isinstance(t, tuple):
+                return "(" + "".join(expr(x) + ", " for x in t) + ")"
+            if isinstance(t, dict):
+                items = []
+                for k, x in t.items():
+                    consts.append(k)
+                    items.append(f"c[{len(consts) - 1}]: {expr(x)}")
+                return "{" + ", ".join(items) + "}"
+            consts.append(t)
+            return f"c[{len(consts) - 1}]"
+
+        body = expr(self._out_tree)
+        fn = eval("lambda v, c: " + body)  # noqa: S307 -- generated from the output tree's structure only
+        self._clone_build = (fn, consts)
 
     def _clone_outputs(self):
         """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
@@ -495,13 +622,10 @@ class StepGraph:
             self._clone_plan()
             self._clone_src_of = ts
         dev = ts[0].device
-        fresh: List[Optional[Tensor]] = [None] * len(ts)
-        dst: Dict[torch.dtype, List[Tensor]] = {}
-        for dt, shape, idx in self._clone_groups:
-            views = torch.empty((len(idx),) + shape, dtype=dt, device=dev).unbind(0)
-            dst.setdefault(dt, []).extend(views)
-            for i, v in zip(idx, views):
-                fresh[i] = v
-        for dt, srcs in self._clone_src.items():
-            torch._foreach_copy_(dst[dt], srcs)
-        return _rebuild(self._out_tree, iter(fresh))
+        views = ()
+        for dt, shape, n in self._clone_groups:
+            views += torch.empty((n,) + shape, dtype=dt, device=dev).unbind(0)
+        for lo, hi, srcs in self._clone_spans:
+            torch._foreach_copy_(views[lo:hi], srcs)
+        fn, consts = self._clone_build
+        return fn(views, consts)

@@ -13,6 +13,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
+import os
 import random
 import sys
 from typing import Dict, List, Optional, Sequence, Union
@@ -111,6 +112,8 @@ class Environment(TorchVectorizedObject):
         self.grad_enabled = grad_enabled
         self._apply_cache = None  # see _apply_continuous_actions
         self._u_persist = None  # persistent action buffer of graph mode (see _apply_continuous_actions)
+        self._spec_keep = None  # action tensors a speculative action launch reads
+        self._draw_plans = {}  # agent -> cached column plan of its random actions
         self._raw_outputs = False  # set while a step is captured (outputs are cloned after replay)
         self.terminated_truncated = terminated_truncated
         observations = self._reset(seed=seed)
@@ -248,8 +251,21 @@ class Environment(TorchVectorizedObject):
             try:
                 actions = self._check_action_list(actions)
                 g.before_actions()
-                if g.graph is not None and self._apply_continuous_actions(actions, persistent=True):
-                    return g.step()
+                if g.graph is not None:
+                    if self._can_speculate():
+                        # the replay is launched before the action flags are known; a failed flag
+                        # rolls the step back (StepGraph.replay_speculative) and the eager check
+                        # below raises the reference's AssertionError
+                        g.backup(self._u_persist[1])
+                        seq = self._apply_continuous_actions(actions, persistent=True, speculative=True)
+                        if seq:
+                            out = g.replay_speculative(lambda: self._speculative_flags_ok(seq))
+                            if out is not None:
+                                return out
+                            self._apply_continuous_actions(actions)
+                            raise RuntimeError("action flags differ between two checks of the same actions")
+                    if self._apply_continuous_actions(actions, persistent=True):
+                        return g.step()
             except BaseException:
                 self._swap_in_simulator_rng()
                 raise
@@ -394,19 +410,33 @@ class Environment(TorchVectorizedObject):
         """Random action with shape ``(agent.batch_dim, agent.action_size)`` (environment.py:524-582)."""
         return self._random_action(agent)
 
+    def _column_plan(self, agent: Agent):
+        """(batch, device, columns, [(low, high)] per column) of an agent's continuous random
+        action, cached per agent and u_range value (the per-call range lookups cost more host
+        time than the draws' launches)."""
+        ur = agent.action.u_range
+        key = (ur if type(ur) in (float, int) else tuple(ur), self.world.dim_c, agent.silent, agent.action_size,
+               agent.batch_dim)
+        c = self._draw_plans.get(agent)
+        if c is None or c[0] != key:
+            n_c = self.world.dim_c if (self.world.dim_c != 0 and not agent.silent) else 0
+            bounds = []
+            for action_index in range(agent.action_size):
+                r = self._u_range_value(agent, action_index)
+                bounds.append((-r, r))
+            bounds += [(0, 1)] * n_c
+            c = self._draw_plans[agent] = (key, (agent.batch_dim, agent.device, len(bounds), bounds))
+        return c[1]
+
     def _random_action(self, agent: Agent) -> torch.Tensor:
         if self.continuous_actions and self._column_draws(agent.device):
             # each column drawn in place of the [B, n] result: the same uniform_ calls on the
             # same numbers of elements as the reference's per-column tensors + stack, without
             # the stack kernel (checked once per device: _column_draws)
-            n_c = self.world.dim_c if (self.world.dim_c != 0 and not agent.silent) else 0
-            out = torch.empty(agent.batch_dim, agent.action_size + n_c, device=agent.device, dtype=torch.float32)
-            cols = out.unbind(1)
-            for action_index in range(agent.action_size):
-                r = self._u_range_value(agent, action_index)
-                cols[action_index].uniform_(-r, r)
-            for k in range(n_c):
-                cols[agent.action_size + k].uniform_(0, 1)
+            B, dev, n, bounds = self._column_plan(agent)
+            out = torch.empty(B, n, device=dev, dtype=torch.float32)
+            for col, (lo, hi) in zip(out.unbind(1), bounds):
+                col.uniform_(lo, hi)
             return out
         if self.continuous_actions:
             actions = []
@@ -547,13 +577,17 @@ class Environment(TorchVectorizedObject):
     def graph_reason(self) -> str:
         return "" if self._graph is None else getattr(self._graph, "why", "")
 
-    def _apply_continuous_actions(self, actions, persistent: bool = False) -> bool:
+    def _apply_continuous_actions(self, actions, persistent: bool = False, speculative: bool = False):
         """_set_action of every agent in one native call (vmas_apply_actions), for continuous fp32
         actions without communication and without autograd: the NaN / range checks, the clamp
         and u = physical * u_multiplier of environment.py:615-709, one launch and no stream
         synchronisation.  Agents are then processed in order exactly as the reference loop does
         (agent i raises before its u is assigned; the agents before it keep their new u and
-        noise).  Returns False when the case does not apply (the per-agent path runs)."""
+        noise).  Returns False when the case does not apply (the per-agent path runs).
+
+        speculative (graph mode, no action noise, at most 8 agents): the kernel is only launched
+        and the agents' u are bound to the persistent buffer; returns the launch's sequence number
+        (or False) and the caller checks the flags later with _finish_speculative_actions."""
         agents = self.agents
         n = len(agents)
         if n == 0:
@@ -598,7 +632,9 @@ class Environment(TorchVectorizedObject):
         for i, ag in enumerate(agents):  # range / multiplier tensors are cached by the Action
             if ag.action._u_range_tensor is not tensors[i][0] or ag.action._u_multiplier_tensor is not tensors[i][1]:
                 self._apply_cache = None
-                return self._apply_continuous_actions(actions)
+                return self._apply_continuous_actions(actions, persistent, speculative)
+        if speculative and (idx < 0 or n > 8 or any(ag.action.u_noise > 0 for ag in agents)):
+            return False
         keep = []
         for i, a in enumerate(actions):
             if a.device != dev:
@@ -609,14 +645,25 @@ class Environment(TorchVectorizedObject):
         if persistent:  # graph mode: every step writes the same buffer / the same u views
             pc = self._u_persist
             if pc is None or pc[0] is not c:
+                if self._graph is not None and self._graph.graph is not None:
+                    # the captured step reads the previous buffer's views
+                    self._graph.drop("action parameters changed")
+                    if speculative:
+                        return False
                 pc = self._u_persist = (c, torch.empty(B * total, device=dev, dtype=torch.float32), None)
             out = pc[1]
         else:
             out = torch.empty(B * total, device=dev, dtype=torch.float32)
         stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream) if idx >= 0 else None
         lib = N.load_library()
-        N.check_aux(lib.vmas_apply_actions(idx, B, refs.ctypes.data, n, out.data_ptr(), flags.ctypes.data, stream),
-                    "vmas_apply_actions")
+        if speculative:
+            seq = ctypes.c_uint32(0)
+            N.check_aux(lib.vmas_apply_actions_launch(idx, B, refs.ctypes.data, n, out.data_ptr(), ctypes.byref(seq),
+                                                      stream), "vmas_apply_actions_launch")
+            self._spec_keep = keep  # the kernel reads them: alive until the flags are in
+        else:
+            N.check_aux(lib.vmas_apply_actions(idx, B, refs.ctypes.data, n, out.data_ptr(), flags.ctypes.data, stream),
+                        "vmas_apply_actions")
         del keep
         k = sizes[0]
         if persistent and self._u_persist[2] is not None:
@@ -627,6 +674,10 @@ class Environment(TorchVectorizedObject):
             us = [out.narrow(0, int(o), B * sz).view(B, sz) for o, sz in zip(refs["out_offset"], sizes)]
         if persistent and self._u_persist[2] is None:
             self._u_persist = (self._u_persist[0], out, us)
+        if speculative:
+            for i, ag in enumerate(agents):
+                ag.action.u = us[i]
+            return seq.value
         for i, ag in enumerate(agents):
             if flags[2 * i]:
                 print()  # the reference prints an empty line before this assert (environment.py:621-622)
@@ -639,6 +690,28 @@ class Environment(TorchVectorizedObject):
                 noise = torch.randn(*ag.action.u.shape, device=self.device, dtype=torch.float32) * ag.u_noise
                 ag.action.u += noise
         return True
+
+    # Speculative replay (opt-in, VMAS_GRAPH_SPECULATIVE=1): launch the replay before the action
+    # flags are known and roll back on a failed flag.  Measured 1.5 % slower than waiting for the
+    # flags first (interleaved A/B, profiles/r01/run11_host_path): the step is host-bound, and the
+    # per-step backup adds host work that the removed wait does not repay.
+    _SPECULATE = os.environ.get("VMAS_GRAPH_SPECULATIVE", "0") == "1"
+
+    def _can_speculate(self) -> bool:
+        c = self._apply_cache
+        return (self._SPECULATE and c is not None and c[1] is not None and c[1][6] >= 0 and len(self.agents) <= 8
+                and self._u_persist is not None and self._u_persist[0] is c
+                and all(ag.action.u_noise <= 0 for ag in self.agents))
+
+    def _speculative_flags_ok(self, seq: int) -> bool:
+        """Waits for the flags of a speculative launch; True when every agent's actions pass."""
+        refs, _, flags, _, _, _, idx, N = self._apply_cache[1]
+        n = len(self.agents)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
+        N.check_aux(N.load_library().vmas_apply_actions_flags(idx, seq, n, flags.ctypes.data, stream),
+                    "vmas_apply_actions_flags")
+        self._spec_keep = None
+        return not flags[: 2 * n].any()
 
     def _set_action(self, action, agent, validated: bool = False):
         # The reference clones the action so that its in-place ops never touch the caller's
