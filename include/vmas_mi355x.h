@@ -284,6 +284,25 @@ int32_t vmas_apply_actions_launch(int32_t device, int32_t batch, const VmasActio
 int32_t vmas_apply_actions_flags(int32_t device, uint32_t seq, int32_t n_refs, uint8_t* flags,
                                  void* stream);
 
+/* Random actions (Environment.get_random_actions, environment.py:524-606): the uniform_ draws
+ * of every agent's action columns in one launch (csrc/vmas_actions.hip).  Column i gets
+ * numel floats in [from, to) written to out[k * stride], drawn exactly as a torch uniform_ call
+ * on a contiguous [numel] tensor would with the CUDA generator at (seed, offset + i * inc), where
+ * inc is that call's philox increment; *increment = n_cols * inc is what the caller adds to the
+ * generator's offset.  mode selects the fp contraction of two roundings (bit 0: the (0, 1]
+ * mapping, bit 1: rand * range + from); the host keeps the mode that reproduces torch on the
+ * device (probe) and otherwise draws with torch.  GPU only. */
+typedef struct VmasUniformColumn {
+    float* out;
+    int64_t stride;      /* elements between consecutive draws */
+    float from, to;      /* f32(low), f32(high) as torch casts them */
+    uint64_t offset;     /* set by the library */
+} VmasUniformColumn;
+
+int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformColumn* cols,
+                             int32_t n_cols, uint64_t seed, uint64_t offset, int32_t mode,
+                             uint64_t* increment, void* stream);
+
 /* Deferred device assertions for graph mode (csrc/vmas_actions.hip).  Replaces the host sync of
  * a reference assert on a device tensor inside the step -- Agent.action_callback's range check of
  * a scripted action (core.py:977-980) -- when the step is captured into a HIP graph.

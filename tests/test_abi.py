@@ -36,9 +36,10 @@ def test_struct_sizes_match_header_compilation():
 #include <stdio.h>
 #include "vmas_mi355x.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(VmasEntityDesc), sizeof(VmasPairDesc),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(VmasEntityDesc), sizeof(VmasPairDesc),
     sizeof(VmasJointDesc), sizeof(VmasWorldConfig), sizeof(VmasEntityIO), sizeof(VmasAgentIO), sizeof(VmasJointIO),
-    sizeof(VmasStepIO), sizeof(VmasRayTarget), sizeof(VmasShapeRef), sizeof(VmasActionRef), sizeof(int));
+    sizeof(VmasStepIO), sizeof(VmasRayTarget), sizeof(VmasShapeRef), sizeof(VmasActionRef), sizeof(int),
+    sizeof(VmasActionApplyRef), sizeof(VmasUniformColumn));
   return 0; }
 '''
     import tempfile
@@ -52,7 +53,8 @@ int main(void) {
     py = [ctypes.sizeof(N.VmasEntityDesc), ctypes.sizeof(N.VmasPairDesc), ctypes.sizeof(N.VmasJointDesc),
           ctypes.sizeof(N.VmasWorldConfig), N.ENTITY_IO_DTYPE.itemsize, N.AGENT_IO_DTYPE.itemsize,
           N.JOINT_IO_DTYPE.itemsize, ctypes.sizeof(N.VmasStepIO), N.RAY_TARGET_DTYPE.itemsize,
-          ctypes.sizeof(N.VmasShapeRef), N.ACTION_REF_DTYPE.itemsize, 4]
+          ctypes.sizeof(N.VmasShapeRef), N.ACTION_REF_DTYPE.itemsize, 4, N.ACTION_APPLY_REF_DTYPE.itemsize,
+          N.UNIFORM_COLUMN_DTYPE.itemsize]
     assert sizes == py
 
 

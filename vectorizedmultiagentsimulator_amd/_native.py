@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "vmas_apply_actions",
     "vmas_apply_actions_launch",
     "vmas_apply_actions_flags",
+    "vmas_uniform_columns",
     "vmas_assert_create",
     "vmas_assert_destroy",
     "vmas_assert_publish",
@@ -273,6 +274,8 @@ ACTION_APPLY_REF_DTYPE = np.dtype(
         ("pad", "<i4"),
     ]
 )
+UNIFORM_COLUMN_DTYPE = np.dtype([("out", "<u8"), ("stride", "<i8"), ("from_", "<f4"), ("to", "<f4"), ("offset", "<u8")])
+assert UNIFORM_COLUMN_DTYPE.itemsize == 32
 assert ACTION_REF_DTYPE.itemsize == 40
 assert ACTION_APPLY_REF_DTYPE.itemsize == 56
 assert ENTITY_IO_DTYPE.itemsize == 72
@@ -331,6 +334,9 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_apply_actions_launch.argtypes = [_i32, _i32, _vp, _i32, _vp, ctypes.POINTER(ctypes.c_uint32), _vp]
     lib.vmas_apply_actions_flags.restype = _i32
     lib.vmas_apply_actions_flags.argtypes = [_i32, ctypes.c_uint32, _i32, _vp, _vp]
+    lib.vmas_uniform_columns.restype = _i32
+    lib.vmas_uniform_columns.argtypes = [_i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64, ctypes.c_uint64, _i32,
+                                         ctypes.POINTER(ctypes.c_uint64), _vp]
     lib.vmas_assert_create.restype = _i32
     lib.vmas_assert_create.argtypes = [_i32, _i32, ctypes.POINTER(_vp)]
     lib.vmas_assert_destroy.restype = _i32

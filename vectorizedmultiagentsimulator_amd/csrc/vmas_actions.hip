@@ -19,6 +19,8 @@
 #include <cmath>
 #include <mutex>
 
+#include <rocrand/rocrand_philox4x32_10.h>
+
 #include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
 
@@ -154,6 +156,61 @@ __global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int
     }
 }
 
+// ---- random actions: every agent's uniform_ columns in one launch ------------------------------
+// The reference draws each action column with its own torch uniform_ call (environment.py:
+// 524-606); on ROCm that is one philox kernel per column (PyTorch's distribution kernel: thread
+// idx of a grid of min(ceil(n/256), CUs * maxThreadsPerCU/256) x 256 threads initialises
+// philox4x32-10 at (seed, subsequence = idx, offset), draws 4 numbers per grid-stride round
+// for elements idx + k * threads, maps them to floats in (0, 1] and to [from, to)).  Here one
+// launch draws all columns (blockIdx.y = column, offset of column c = offset + c * increment), with
+// rocrand's own philox engine.  The two float roundings whose contraction depends on how PyTorch
+// was compiled (v * 2^-32 + 2^-32 and rand * range + from: separate or fused) are a mode; the
+// host picks the mode that reproduces torch's draws bit for bit on this device (probe), or does
+// not use the kernel.
+constexpr int kMaxUniformCols = 32;
+constexpr int kUniformThreads = 256;
+
+struct UniformArgs {
+    VmasUniformColumn c[kMaxUniformCols];
+    unsigned long long seed;
+    long long numel;
+    int mode;  // bit 0: fused (0, 1] mapping; bit 1: fused affine transform
+};
+
+__device__ __forceinline__ float unit_float(unsigned int v, bool fused) {
+    const float inv = 2.3283064e-10f;  // ROCRAND_2POW32_INV
+    return fused ? __builtin_fmaf((float)v, inv, inv) : inv + (float)v * inv;
+}
+
+__global__ void __launch_bounds__(kUniformThreads) k_uniform_columns(UniformArgs a) {
+    const VmasUniformColumn& col = a.c[blockIdx.y];
+    const long long idx = (long long)blockIdx.x * kUniformThreads + threadIdx.x;
+    rocrand_state_philox4x32_10 st;
+    rocrand_init(a.seed, (unsigned long long)idx, col.offset, &st);
+    const long long step = (long long)kUniformThreads * gridDim.x;
+    const long long rounded = ((a.numel - 1) / (step * 4) + 1) * step * 4;
+    const float from = col.from, to = col.to, range = to - from;
+    const bool fused_unit = a.mode & 1, fused_affine = a.mode & 2;
+    for (long long li0 = idx; li0 < rounded; li0 += step * 4) {
+        const uint4 v = rocrand4(&st);
+        const unsigned int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long long li = li0 + step * k;
+            if (li < a.numel) {
+                const float r = unit_float(vv[k], fused_unit);
+                const float val = fused_affine ? __builtin_fmaf(r, range, from) : r * range + from;
+                col.out[li * col.stride] = val == to ? from : val;  // (0, 1] -> [from, to)
+            }
+        }
+    }
+}
+
+struct UniformGrid {
+    int gx = 0;
+    long long numel = -1;
+};
+
 }  // namespace
 
 struct VmasDeviceAssert {
@@ -236,6 +293,39 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
             flags[2 * (first + i) + 1] = (v >> (2 * i + 1)) & 1u;
         }
     }
+    return VMAS_OK;
+}
+
+int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformColumn* cols, int32_t n_cols,
+                             uint64_t seed, uint64_t offset, int32_t mode, uint64_t* increment, void* stream) {
+    if (device < 0 || device >= 64 || numel <= 0 || n_cols <= 0 || n_cols > kMaxUniformCols || !cols ||
+        !increment || mode < 0 || mode > 3)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_uniform_columns: bad arguments");
+    static int max_blocks[64] = {0};
+    if (!max_blocks[device]) {
+        hipDeviceProp_t prop;
+        VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
+        max_blocks[device] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / kUniformThreads);
+        if (max_blocks[device] <= 0) return vmas_aux::fail(VMAS_E_HIP, "vmas_uniform_columns: device properties");
+    }
+    const long long gx = std::min<long long>((numel + kUniformThreads - 1) / kUniformThreads, max_blocks[device]);
+    // PyTorch's per-call philox increment (counter_offset, rounded up to a multiple of 4)
+    const unsigned long long inc = (unsigned long long)((numel - 1) / (kUniformThreads * gx * 4) + 1) * 4;
+    UniformArgs a{};
+    for (int i = 0; i < n_cols; ++i) {
+        if (!cols[i].out) return vmas_aux::fail(VMAS_E_INVALID, "vmas_uniform_columns: null column %d", i);
+        a.c[i] = cols[i];
+        a.c[i].offset = offset + inc * (unsigned long long)i;
+    }
+    a.seed = seed;
+    a.numel = numel;
+    a.mode = mode;
+    int cur = -1;
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
+    hipLaunchKernelGGL(k_uniform_columns, dim3((unsigned)gx, n_cols), dim3(kUniformThreads), 0, (hipStream_t)stream, a);
+    VMAS_AUX_HIP(hipGetLastError());
+    *increment = inc * (unsigned long long)n_cols;
     return VMAS_OK;
 }
 

@@ -16,7 +16,7 @@ import math
 import os
 import random
 import sys
-from typing import Dict, List, Optional, Sequence, Union
+from typing import Dict, List, Optional, Sequence, Union, Any
 
 import numpy as np
 import torch
@@ -114,6 +114,7 @@ class Environment(TorchVectorizedObject):
         self._u_persist = None  # persistent action buffer of graph mode (see _apply_continuous_actions)
         self._spec_keep = None  # action tensors a speculative action launch reads
         self._draw_plans = {}  # agent -> cached column plan of its random actions
+        self._uniform_cache = None  # see _fused_random_actions
         self._raw_outputs = False  # set while a step is captured (outputs are cloned after replay)
         self.terminated_truncated = terminated_truncated
         observations = self._reset(seed=seed)
@@ -469,8 +470,104 @@ class Environment(TorchVectorizedObject):
         (Drawing them on a side stream, overlapped with the previous step's graph, measured
         slower: 87-98 M vs 106-119 M env-steps/s, interleaved runs on one MI355X.)"""
         if self.continuous_actions and self.device.type == "cuda":
+            fused = self._fused_random_actions()
+            if fused is not None:
+                return fused
             return [self._random_action(agent) for agent in self.agents]
         return self._random_actions_seeded()
+
+    # ---- every agent's random action columns in one native launch (GPU) ---------------------------
+    _UNIFORM_MODES: Dict[Any, Optional[int]] = {}
+
+    @classmethod
+    def _uniform_mode(cls, device: torch.device, B: int) -> Optional[int]:
+        """The vmas_uniform_columns mode whose draws equal torch's uniform_ calls bit for bit on
+        this device at batch B -- per-column [B] tensors, as the reference draws them -- and whose
+        generator advance equals theirs; None if no mode does.  Probed once per (device, B) with
+        the device generator saved and restored around it."""
+        key = (str(device), B)
+        if key in cls._UNIFORM_MODES:
+            return cls._UNIFORM_MODES[key]
+        from ... import _native as N
+
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        gen = torch.cuda.default_generators[idx]
+        saved = gen.get_state()
+        bounds = [(-0.7, 0.7), (-1.0, 1.0), (0.0, 1.0), (-0.30000001192092896, 0.30000001192092896)]
+        found = None
+        try:
+            ref = [torch.empty(B, device=device, dtype=torch.float32).uniform_(lo, hi) for lo, hi in bounds]
+            after = gen.get_state()
+            for mode in (3, 0, 1, 2):
+                gen.set_state(saved)
+                out = torch.empty(B, len(bounds), device=device, dtype=torch.float32)
+                cols = np.zeros(len(bounds), dtype=N.UNIFORM_COLUMN_DTYPE)
+                for i, (lo, hi) in enumerate(bounds):
+                    cols[i] = (out.data_ptr() + 4 * i, len(bounds), lo, hi, 0)
+                cls._launch_uniform(N, idx, B, cols, mode, gen)
+                if all(torch.equal(out[:, i], r) for i, r in enumerate(ref)) and torch.equal(gen.get_state(), after):
+                    found = mode
+                    break
+        finally:
+            gen.set_state(saved)
+        cls._UNIFORM_MODES[key] = found
+        return found
+
+    @staticmethod
+    def _launch_uniform(N, idx, B, cols, mode, gen):
+        inc = ctypes.c_uint64(0)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
+        N.check_aux(N.load_library().vmas_uniform_columns(idx, B, cols.ctypes.data, len(cols), gen.initial_seed(),
+                                                           gen.get_offset(), mode, ctypes.byref(inc), stream),
+                    "vmas_uniform_columns")
+        gen.set_offset(gen.get_offset() + inc.value)
+
+    def _fused_random_actions(self):
+        """get_random_actions for continuous actions on a GPU: every agent's [B, n] action, drawn
+        column by column with the same numbers and generator advance as the reference's per-column
+        uniform_ calls (checked by _uniform_mode), in one launch instead of one per column."""
+        agents = self.agents
+        if not agents:
+            return None
+        plans = [self._column_plan(a) for a in agents]
+        B, dev = plans[0][0], plans[0][1]
+        c = self._uniform_cache
+        if c is None or len(c[0]) != len(plans) or any(a is not b for a, b in zip(c[0], plans)):
+            key = tuple(plans)
+            n_cols = sum(p[2] for p in plans)
+            ok = (n_cols <= 32 and all(p[0] == B and p[1] == dev for p in plans)
+                  and self._column_draws(dev) and self._uniform_mode(torch.device(dev), B) is not None)
+            if not ok:
+                self._uniform_cache = (key, None)
+                return None
+            from ... import _native as N
+
+            cols = np.zeros(n_cols, dtype=N.UNIFORM_COLUMN_DTYPE)
+            k = 0
+            for p in plans:
+                for j, (lo, hi) in enumerate(p[3]):
+                    cols[k]["stride"], cols[k]["from_"], cols[k]["to"] = p[2], lo, hi
+                    k += 1
+            d = torch.device(dev)
+            idx = d.index if d.index is not None else torch.cuda.current_device()
+            c = self._uniform_cache = (key, (N, cols, [p[2] for p in plans], idx,
+                                             self._uniform_mode(d, B), torch.cuda.default_generators[idx]))
+        st = c[1]
+        if st is None:
+            return None
+        N, cols, widths, idx, mode, gen = st
+        outs = []
+        k = 0
+        f_out = cols["out"]
+        for n in widths:
+            out = torch.empty(B, n, device=dev, dtype=torch.float32)
+            base = out.data_ptr()
+            for j in range(n):
+                f_out[k] = base + 4 * j
+                k += 1
+            outs.append(out)
+        self._launch_uniform(N, idx, B, cols, mode, gen)
+        return outs
 
     @local_seed(vmas_random_state)
     def _random_actions_seeded(self) -> Sequence[torch.Tensor]:
