@@ -206,6 +206,10 @@ const char* vmas_last_error(void);
 /* Ends a stream capture left open by a failed HIP-graph capture (1 if one was ended) and clears
  * the last HIP error (graph mode's fallback to the eager step; no reference counterpart). */
 int32_t vmas_stream_abort_capture(void* stream);
+/* Launches an instantiated HIP graph (hipGraphExec_t) on a stream: graph mode's replay of a step
+ * graph that draws no random numbers, without torch's generator-state prologue (no reference
+ * counterpart). */
+int32_t vmas_graph_launch(void* graph_exec, void* stream);
 /* Host waits on the device performed by the library so far (stream / event synchronisations and
  * spins on published words; wraps around): graph mode runs one step between two reads of it to
  * tell whether the step can be captured (no reference counterpart). */

@@ -24,6 +24,10 @@ env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, graph_step=Tr
 if scenario == "balance":
     env.world._substeps = 10
     env.world._sub_dt = env.world._dt / 10
+import os  # noqa: E402
+
+if os.environ.get("SKIP_PHYSICS") == "1":  # diagnostic: the step without World.step (scenario nodes only)
+    env.world.step = lambda: None
 for _ in range(10):
     env.step(env.get_random_actions())
 assert env.graph_status == "graph", env.graph_reason
@@ -51,20 +55,20 @@ def wrap(cls, meth, before, after):
 wrap(_graph.StepGraph, "before_actions", "before_actions0", "before_actions1")
 wrap(Environment, "_apply_continuous_actions", "apply0", "apply1")
 G = env._graph
-orig_replay = G.graph.replay
+orig_launch = _graph.StepGraph._launch
 
 
-def replay():
+def launch(self):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     stamp("replay0")
-    orig_replay()
+    orig_launch(self)
     stamp("replay1")
     e1.record()
     events.append((e0, e1))
 
 
-G.graph.replay = replay
+_graph.StepGraph._launch = launch
 wrap(_graph.StepGraph, "_clone_outputs", "clone0", "clone1")
 
 N = 100
@@ -98,5 +102,6 @@ out = {
     "gpu_us": {"graph_replay": round(gpu_graph, 1)},
     "inplace_backed_up": [list(t.shape) for t in G._inplace],
     "speculative": bool(env._can_speculate()),
+    "raw_graph_launch": G._raw_exec is not None,
 }
 print(json.dumps(out), flush=True)

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "vmas_device_count",
     "vmas_last_error",
     "vmas_stream_abort_capture",
+    "vmas_graph_launch",
     "vmas_host_waits",
     "vmas_world_create",
     "vmas_world_destroy",
@@ -312,6 +313,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_host_waits.argtypes = []
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
+    lib.vmas_graph_launch.restype = _i32
+    lib.vmas_graph_launch.argtypes = [_vp, _vp]
     lib.vmas_world_create.restype = _i32
     lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
     lib.vmas_world_destroy.restype = _i32

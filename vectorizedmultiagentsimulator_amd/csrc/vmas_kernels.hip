@@ -1056,6 +1056,19 @@ int32_t vmas_stream_abort_capture(void* stream_) {
     return ended;
 }
 
+// Launches an instantiated graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) on a stream
+// without torch's replay prologue, whose two generator-state fill kernels serve only graphs
+// that draw random numbers (graph mode checks that the step's graph does not).
+int32_t vmas_graph_launch(void* graph_exec, void* stream) {
+    if (!graph_exec) return fail(VMAS_E_INVALID, "vmas_graph_launch: null graph");
+    const hipError_t e = hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VMAS_E_HIP, "vmas_graph_launch: %s", hipGetErrorString(e));
+    }
+    return VMAS_OK;
+}
+
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,

@@ -46,6 +46,7 @@ from __future__ import annotations
 
 import ctypes
 import gc
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -265,6 +266,7 @@ class StepGraph:
         self._bk_src: List[Tensor] = []
         self._bk_dst: List[Tensor] = []
         self._bk_u: Optional[Tensor] = None
+        self._raw_exec: Optional[ctypes.c_void_p] = None
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -356,6 +358,7 @@ class StepGraph:
 
     def drop(self, why: str):
         self.graph = None
+        self._raw_exec = None
         self.status = "dropped"
         self.why = why
         self.eager_steps = 0
@@ -430,6 +433,8 @@ class StepGraph:
             env._raw_outputs = False
             env.world._assert_sink = None
         self.graph = g
+        self._raw_exec = None
+        self.replays = 0
         self.status = "graph"
         self.why = ""
         self._first_replay = True
@@ -502,13 +507,34 @@ class StepGraph:
         return self.env.world.engine.graph_token() == self._sig
 
     # ---- replay ---------------------------------------------------------------------------------
+    def _launch(self):
+        """One replay.  The first goes through torch (its prologue refreshes the generator state
+        that captured random ops read); if it did not advance the device generator, the graph
+        draws no random numbers and later replays launch the instantiated graph directly
+        (vmas_graph_launch), without the prologue's two fill kernels."""
+        if self._raw_exec is not None:
+            from ... import _native as N
+
+            dev = self.env.device
+            stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            N.check(N.load_library().vmas_graph_launch(self._raw_exec, stream), "vmas_graph_launch")
+            return
+        dev = self.env.device
+        gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+        before = gen.get_offset()
+        self.graph.replay()
+        if self.replays == 0 and gen.get_offset() == before and self._RAW_LAUNCH:
+            self._raw_exec = ctypes.c_void_p(self.graph.raw_cuda_graph_exec())
+
+    _RAW_LAUNCH = os.environ.get("VMAS_GRAPH_RAW_LAUNCH", "1") != "0"  # (A/B knob)
+
     def _replay(self):
         asserts = self._asserts is not None and bool(self._asserts.msgs)
         if asserts:  # a failed device assert rolls the step back: back up what it modifies in place
             self.backup(None)
             rng = torch.cuda.get_rng_state(self.env.device)
         self._first_replay = False
-        self.graph.replay()
+        self._launch()
         self.replays += 1
         out = self._clone_outputs()
         if asserts:
@@ -545,7 +571,7 @@ class StepGraph:
         dev = self.env.device
         rng = torch.cuda.get_rng_state(dev)
         self._first_replay = False
-        self.graph.replay()
+        self._launch()
         self.replays += 1
         out = self._clone_outputs()
         if not flags_ok():
