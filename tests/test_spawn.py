@@ -15,7 +15,10 @@ class _W:
 
 def _gen(device):
     d = torch.device(device)
-    return torch.cuda.default_generators[d.index or 0] if d.type == "cuda" else torch.default_generator
+    if d.type == "cuda":
+        torch.cuda.init()  # default_generators is filled when CUDA initialises
+        return torch.cuda.default_generators[d.index or 0]
+    return torch.default_generator
 
 
 def _case(device, b, n_occ, min_dist, seed, bounds=(-1.0, 1.0), env_index=None):
@@ -48,5 +51,9 @@ def test_spawn_single_env_index_cpu():
 @pytest.mark.parametrize("b,n_occ,min_dist", [(1, 3, 0.2), (64, 0, 0.2), (16384, 14, 0.3), (32768, 13, 0.25),
                                                (4096, 20, 0.45)])
 def test_spawn_matches_reference_loop_gpu(gpu_device, b, n_occ, min_dist):
+    from vectorizedmultiagentsimulator_amd.simulator.environment import _uniform
+
     for seed in range(3):
         _case(gpu_device, b, n_occ, min_dist, seed)
+    if n_occ:  # the tries were drawn by the fused native launch (vmas_uniform_columns)
+        assert _uniform.MODES.get((str(torch.device(gpu_device)), b)) is not None

@@ -95,6 +95,7 @@ class PhysicsEngine:
         self.kernel_name = "k_step"
         self._dev_index = -1
         self._qrefs = {}  # distance-query shape references, see _ref
+        self._ray_tables = {}  # LIDAR target tables, see _ray_table
         self._last_iterations = 0
         self.steps = 0
 
@@ -659,22 +660,19 @@ class PhysicsEngine:
             ang = ang.unsqueeze(-1)
         R = ang.shape[-1]
         assert ang.shape[0] == B
-        tg = np.zeros(max(len(targets), 1), dtype=N.RAY_TARGET_DTYPE)
-        for i, e in enumerate(targets):
-            code = _shape_code(e.shape)
-            p = self._prep(e.state.pos, dev)
-            r = self._prep(e.state.rot, dev)
-            _check_grad((p, r))
-            keep += [p, r]
-            row = tg[i]
-            row["shape"] = code
-            if code == N.VMAS_SPHERE:
-                row["radius"] = _f32(e.shape.radius)
-            else:
-                row["length"] = _f32(e.shape.length)
-                row["width"] = _f32(e.shape.width) if code == N.VMAS_BOX else 0.0
-            row["pos"], row["rot"] = p.data_ptr(), r.data_ptr()
-            row["pos_s0"], row["pos_s1"], row["rot_s0"] = p.stride(0), p.stride(1), r.stride(0)
+        tg = self._ray_table(targets)
+        if targets:
+            ps = [self._prep(e.state.pos, dev) for e in targets]
+            rs = [self._prep(e.state.rot, dev) for e in targets]
+            _check_grad(ps)
+            _check_grad(rs)
+            keep += ps + rs
+            # the per-call fields, one vectorised write each (the shape fields are cached)
+            tg["pos"] = [p.data_ptr() for p in ps]
+            tg["rot"] = [r.data_ptr() for r in rs]
+            tg["pos_s0"] = [p.stride(0) for p in ps]
+            tg["pos_s1"] = [p.stride(1) for p in ps]
+            tg["rot_s0"] = [r.stride(0) for r in rs]
         out = torch.empty((B, R), device=dev, dtype=torch.float32)
         rot_ptr, rot_s0 = None, 0
         if rot_offset is not None:
@@ -690,6 +688,30 @@ class PhysicsEngine:
             "vmas_cast_rays",
         )
         return out
+
+    def _ray_table(self, targets) -> np.ndarray:
+        """The VmasRayTarget rows of a target list with their shape fields filled; cached per
+        list of (entity, shape object, dimensions) -- the state pointers are written per call."""
+        sig = tuple((e, e.shape, _shape_dims(e.shape, _shape_code(e.shape))) for e in targets)
+        key = tuple(id(e) for e in targets)
+        c = self._ray_tables.get(key)
+        if c is not None and len(c[0]) == len(sig) and all(
+                a[0] is b[0] and a[1] is b[1] and a[2] == b[2] for a, b in zip(c[0], sig)):
+            return c[1]
+        tg = np.zeros(max(len(targets), 1), dtype=N.RAY_TARGET_DTYPE)
+        for i, (e, shape, dims) in enumerate(sig):
+            code = _shape_code(shape)
+            row = tg[i]
+            row["shape"] = code
+            if code == N.VMAS_SPHERE:
+                row["radius"] = _f32(dims[0])
+            else:
+                row["length"] = _f32(dims[0])
+                row["width"] = _f32(dims[1]) if code == N.VMAS_BOX else 0.0
+        if len(self._ray_tables) > 64:
+            self._ray_tables.clear()
+        self._ray_tables[key] = (sig, tg)
+        return tg
 
     # ---- distance queries -------------------------------------------------------------------------
     def _ref(self, e, dev, keep, slot=0) -> N.VmasShapeRef:

@@ -26,6 +26,7 @@ from ..core import Agent, TorchVectorizedObject
 from ..scenario import BaseScenario
 from ..utils import AGENT_OBS_TYPE, DEVICE_TYPING, TorchUtils, override
 from . import spaces
+from . import _uniform
 from ._rng import numpy_global_rng, python_global_rng
 
 
@@ -477,55 +478,12 @@ class Environment(TorchVectorizedObject):
         return self._random_actions_seeded()
 
     # ---- every agent's random action columns in one native launch (GPU) ---------------------------
-    _UNIFORM_MODES: Dict[Any, Optional[int]] = {}
-
-    @classmethod
-    def _uniform_mode(cls, device: torch.device, B: int) -> Optional[int]:
-        """The vmas_uniform_columns mode whose draws equal torch's uniform_ calls bit for bit on
-        this device at batch B -- per-column [B] tensors, as the reference draws them -- and whose
-        generator advance equals theirs; None if no mode does.  Probed once per (device, B) with
-        the device generator saved and restored around it."""
-        key = (str(device), B)
-        if key in cls._UNIFORM_MODES:
-            return cls._UNIFORM_MODES[key]
-        from ... import _native as N
-
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        gen = torch.cuda.default_generators[idx]
-        saved = gen.get_state()
-        bounds = [(-0.7, 0.7), (-1.0, 1.0), (0.0, 1.0), (-0.30000001192092896, 0.30000001192092896)]
-        found = None
-        try:
-            ref = [torch.empty(B, device=device, dtype=torch.float32).uniform_(lo, hi) for lo, hi in bounds]
-            after = gen.get_state()
-            for mode in (3, 0, 1, 2):
-                gen.set_state(saved)
-                out = torch.empty(B, len(bounds), device=device, dtype=torch.float32)
-                cols = np.zeros(len(bounds), dtype=N.UNIFORM_COLUMN_DTYPE)
-                for i, (lo, hi) in enumerate(bounds):
-                    cols[i] = (out.data_ptr() + 4 * i, len(bounds), lo, hi, 0)
-                cls._launch_uniform(N, idx, B, cols, mode, gen)
-                if all(torch.equal(out[:, i], r) for i, r in enumerate(ref)) and torch.equal(gen.get_state(), after):
-                    found = mode
-                    break
-        finally:
-            gen.set_state(saved)
-        cls._UNIFORM_MODES[key] = found
-        return found
-
-    @staticmethod
-    def _launch_uniform(N, idx, B, cols, mode, gen):
-        inc = ctypes.c_uint64(0)
-        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
-        N.check_aux(N.load_library().vmas_uniform_columns(idx, B, cols.ctypes.data, len(cols), gen.initial_seed(),
-                                                           gen.get_offset(), mode, ctypes.byref(inc), stream),
-                    "vmas_uniform_columns")
-        gen.set_offset(gen.get_offset() + inc.value)
+    _UNIFORM_MODES = _uniform.MODES  # (device, batch) -> probed vmas_uniform_columns mode
 
     def _fused_random_actions(self):
         """get_random_actions for continuous actions on a GPU: every agent's [B, n] action, drawn
         column by column with the same numbers and generator advance as the reference's per-column
-        uniform_ calls (checked by _uniform_mode), in one launch instead of one per column."""
+        uniform_ calls (checked by _uniform.mode), in one launch instead of one per column."""
         agents = self.agents
         if not agents:
             return None
@@ -536,7 +494,7 @@ class Environment(TorchVectorizedObject):
             key = tuple(plans)
             n_cols = sum(p[2] for p in plans)
             ok = (n_cols <= 32 and all(p[0] == B and p[1] == dev for p in plans)
-                  and self._column_draws(dev) and self._uniform_mode(torch.device(dev), B) is not None)
+                  and self._column_draws(dev) and _uniform.mode(torch.device(dev), B) is not None)
             if not ok:
                 self._uniform_cache = (key, None)
                 return None
@@ -551,7 +509,7 @@ class Environment(TorchVectorizedObject):
             d = torch.device(dev)
             idx = d.index if d.index is not None else torch.cuda.current_device()
             c = self._uniform_cache = (key, (N, cols, [p[2] for p in plans], idx,
-                                             self._uniform_mode(d, B), torch.cuda.default_generators[idx]))
+                                             _uniform.mode(d, B), torch.cuda.default_generators[idx]))
         st = c[1]
         if st is None:
             return None
@@ -566,7 +524,7 @@ class Environment(TorchVectorizedObject):
                 f_out[k] = base + 4 * j
                 k += 1
             outs.append(out)
-        self._launch_uniform(N, idx, B, cols, mode, gen)
+        _uniform.launch(idx, B, cols, mode, gen)
         return outs
 
     @local_seed(vmas_random_state)

@@ -13,6 +13,7 @@ from abc import ABC, abstractmethod
 from enum import Enum
 from typing import Dict, List, Sequence, Tuple, Union
 
+import numpy as np
 import torch
 from torch import Tensor
 
@@ -239,6 +240,18 @@ class ScenarioUtils:
         pos = torch.empty((batch_size, 1, 2), device=dev, dtype=torch.float32)
         resolved = torch.full((batch_size,), -1, device=dev, dtype=torch.int32)
         states = []  # generator state after each try, to rewind to the reference's consumption
+        # On a GPU the tries of a batch are drawn in one launch (vmas_uniform_columns: the same
+        # numbers and generator advance as their uniform_ calls, probed per device and batch);
+        # the rewind is then an offset: start + tries * (offset advance per try).
+        fused = None
+        if dev.type == "cuda":
+            from .environment import _uniform
+
+            m = _uniform.mode(torch.device("cuda", dev_index), batch_size)
+            if m is not None:
+                f32 = lambda v: float(np.float32(v))  # noqa: E731 -- torch casts the bounds to float
+                fused = (m, gen.get_offset(), f32(x_bounds[0]), f32(x_bounds[1]), f32(y_bounds[0]), f32(y_bounds[1]))
+        drawn = 0
         # first batch sized from the last consumption at this call shape (over-drawn tries are
         # rewound, so the size only trades draws for syncs)
         key = (batch_size, occ.shape[1], float(min_dist_between_entities), tuple(x_bounds), tuple(y_bounds))
@@ -246,9 +259,22 @@ class ScenarioUtils:
         mx, un = N._i32(0), N._i32(0)
         while True:
             cand = torch.empty((n, 2, batch_size), device=dev, dtype=torch.float32)
-            for k in range(n):
-                draw(None, cand[k, 0], cand[k, 1])
-                states.append(gen.get_state())
+            if fused is not None:
+                m, _, x0, x1, y0, y1 = fused
+                base = cand.data_ptr()
+                for k0 in range(0, n, 16):  # <= 32 columns per launch
+                    k1 = min(n, k0 + 16)
+                    cols = np.zeros(2 * (k1 - k0), dtype=N.UNIFORM_COLUMN_DTYPE)
+                    for k in range(k0, k1):
+                        j = 2 * (k - k0)
+                        cols[j] = (base + 4 * (2 * k) * batch_size, 1, x0, x1, 0)
+                        cols[j + 1] = (base + 4 * (2 * k + 1) * batch_size, 1, y0, y1, 0)
+                    _uniform.launch(dev_index, batch_size, cols, m, gen)
+            else:
+                for k in range(n):
+                    draw(None, cand[k, 0], cand[k, 1])
+                    states.append(gen.get_state())
+            drawn += n
             N.check_aux(lib.vmas_spawn_resolve(
                 dev_index, batch_size, occ.data_ptr(), occ.shape[1], occ.stride(0), occ.stride(1), occ.stride(2),
                 cand.data_ptr(), first, n, float(torch.tensor(min_dist_between_entities, dtype=torch.float32)),
@@ -266,7 +292,13 @@ class ScenarioUtils:
                 )
         consumed = 1 if mx.value == 0 else mx.value + 2
         _SPAWN_HINT[key] = consumed
-        if consumed <= len(states):
+        if fused is not None:
+            start = fused[1]
+            per_try = (gen.get_offset() - start) // drawn
+            gen.set_offset(start + min(consumed, drawn) * per_try)
+            if consumed > drawn:  # the reference's final (unused) proposal lies just past the last batch
+                draw((batch_size, 1, 1))
+        elif consumed <= len(states):
             gen.set_state(states[consumed - 1])
         else:  # the reference's final (unused) proposal lies just past the last batch
             draw((batch_size, 1, 1))
