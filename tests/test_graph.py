@@ -57,7 +57,7 @@ CASES = [
     ("balance", dict(n_agents=4), 10, "graph"),
     ("transport", dict(n_agents=4), None, "graph"),
     ("flocking", dict(n_agents=4), None, "graph"),     # scripted agent: range assert on the device
-    ("discovery", dict(n_agents=4), None, "eager"),    # spawn sampler: rejection loop syncs
+    ("discovery", dict(n_agents=4), None, "graph"),    # spawn sampler: host holes between graphs
 ]
 
 
@@ -101,6 +101,9 @@ def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
     assert graph.graph_status == expect, graph.graph_reason
     if expect == "graph":
         assert graph._graph.replays >= 5
+    if name == "discovery":  # one graph per stretch between the 7 targets' spawn-sampler holes
+        n_holes, n_segments = len(graph._graph._holes), len(graph._graph._segments)
+        assert (n_holes, n_segments) == (7, 8)
 
 
 def _twin_envs(gpu_device, name, **kw):
@@ -158,22 +161,44 @@ def test_scripted_action_assert_raised_from_step_gpu(gpu_device):
 
 
 @pytest.mark.gpu
+def test_failed_segmented_capture_restores_state_gpu(gpu_device):
+    """A capture that fails after host holes already ran the graphs before them (discovery's
+    spawn sampler) restores the world and the generator, and the env continues eagerly with the
+    eager twin's results."""
+    eager, graph = _twin_envs(gpu_device, "discovery", n_agents=4)
+    orig = graph.scenario.info
+
+    def info(agent):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("injected capture failure")
+        return orig(agent)
+
+    graph.scenario.info = info
+    for t in range(6):
+        out_e, out_g = _step_both(eager, graph, eager.get_random_actions())
+        _assert_same(out_e, out_g, f"outputs step {t}")
+        _assert_same(_state(eager), _state(graph), f"state step {t}")
+    assert graph.graph_status == "eager" and "injected" in graph.graph_reason
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["balance", "discovery"])
 @pytest.mark.parametrize("bad", ["nan", "range"])
 @pytest.mark.parametrize("speculative", [False, True], ids=["wait", "speculative"])
-def test_failed_action_check_leaves_world_as_eager_gpu(gpu_device, monkeypatch, bad, speculative):
+def test_failed_action_check_leaves_world_as_eager_gpu(gpu_device, monkeypatch, bad, speculative, name):
     """A NaN / out-of-range action raises the reference's AssertionError and leaves the world as
     the eager step leaves it -- also when the replay was launched before the action flags were
     known (speculative, rolled back, where the agents' u are exact too: the agents before the
     failing one hold their new u, the rest their old one)."""
     monkeypatch.setattr(Environment, "_SPECULATE", speculative)
-    eager, graph = _twin_envs(gpu_device, "balance", n_agents=4)
+    eager, graph = _twin_envs(gpu_device, name, n_agents=4)
     for _ in range(5):
         _step_both(eager, graph, eager.get_random_actions())
     assert graph.graph_status == "graph", graph.graph_reason
     before_u = [a.action.u.clone() for a in graph.agents]
     actions = eager.get_random_actions()
     actions[2][5, 1] = float("nan") if bad == "nan" else 3.0
-    _step_both(eager, graph, actions, "" if bad == "nan" else "out of its range")
+    _step_both(eager, graph, actions, "^$" if bad == "nan" else "out of its range")
     _assert_same(_state(eager), _state(graph), "state after the failed step")
     for i, (ae, ag) in enumerate(zip(eager.agents, graph.agents)):
         if i < 2 or speculative:  # (documented: without speculation the failing agent and those

@@ -1,0 +1,7 @@
+#!/bin/bash
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out/holes
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_graph.py tests/test_spawn.py -m gpu -p no:cacheprovider > gpurun_out/holes/pytest.log 2>&1; rc=$?; tail -22 gpurun_out/holes/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --scenario discovery --envs 16384 --n-agents 8 --substeps 0 --kw '{"use_agent_lidar": true}' --steps 50 --warmup 10 --cpu-steps 0 > gpurun_out/holes/c4.json 2> gpurun_out/holes/c4.log && python -c "import json; d=json.load(open('gpurun_out/holes/c4.json')); print('discovery', round(d['value']/1e6,2), d['ms_per_step'], d['config']['step_mode'])" || exit 1
+timeout -k 10 300 python bench.py --steps 100 --warmup 10 --cpu-steps 0 > gpurun_out/holes/c2.json 2> gpurun_out/holes/c2.log && python -c "import json; d=json.load(open('gpurun_out/holes/c2.json')); print('balance', round(d['value']/1e6,2), d['ms_per_step'], d['config']['step_mode'])"

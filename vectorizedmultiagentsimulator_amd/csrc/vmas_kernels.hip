@@ -187,7 +187,8 @@ int32_t ring_upload(int device, const void* src, size_t n, hipStream_t stream, c
     const int slot = r->next;
     const int seg = slot / per;
     if (slot % per == 0 && r->ev_live[seg]) {
-        vmas_aux::note_host_wait();
+        // (not counted by vmas_host_waits: a ring wrap waits for old work only, and a captured
+        // step takes frozen slots instead, so it does not make a step uncapturable)
         HIP_TRY(hipEventSynchronize(r->ev[seg]));
     }
     memcpy(r->host + (size_t)slot * kSlot, src, n);

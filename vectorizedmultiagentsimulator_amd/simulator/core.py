@@ -904,6 +904,9 @@ class World(TorchVectorizedObject):
         self._joints = {}
         # graph mode's sink for asserts on device tensors inside the step (None: assert eagerly)
         self._assert_sink = None
+        # graph mode's sink for host code that waits on the device inside the step (the spawn
+        # sampler; None: run it inline)
+        self._hole_sink = None
         self._collidable_pairs = [
             {Sphere, Sphere},
             {Sphere, Box},

@@ -246,6 +246,49 @@ def _reset_generator_capture_state(dev):
         pass
 
 
+class _Segments:
+    """Capture of a step that contains host holes: code that must run on the host every step
+    because it waits on the device -- the spawn sampler's rejection loop (utils.py:272-319),
+    whose number of tries, and so the generator's advance, depends on the device data.  Such
+    code reaches the capture through ``world._hole_sink`` (``ScenarioUtils.find_random_pos_for_
+    entity``).  The capture ends the current graph there, runs that graph for real, runs the
+    hole eagerly (its waits are now allowed) and captures the rest of the step into the next
+    graph, all graphs in one memory pool.  A replay runs graph 0, hole 0 (writing into the same
+    output tensor the next graph reads), graph 1, ... -- the reference's order of device work
+    and of generator use.  Without holes it is a single graph, captured as torch.cuda.graph
+    does."""
+
+    def __init__(self, side: torch.cuda.Stream):
+        self.side = side
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.holes: List[Tuple[Any, tuple, Tensor]] = []
+        self.cur: Optional[torch.cuda.CUDAGraph] = None
+        self.ran = False
+
+    def begin(self):
+        self.cur = torch.cuda.CUDAGraph()
+        self.cur.capture_begin(pool=self.pool)
+
+    def end(self):
+        g, self.cur = self.cur, None
+        g.capture_end()
+        self.graphs.append(g)
+
+    def hole(self, fn, args):
+        if not isinstance(args, tuple):
+            raise GraphUnsupported("host hole arguments must be a tuple")
+        self.end()
+        self.ran = True
+        self.graphs[-1].replay()  # the work before the hole, for real
+        res = fn(*args)
+        if not isinstance(res, Tensor):
+            raise GraphUnsupported("a host hole must return one tensor")
+        self.holes.append((fn, args, res))
+        self.begin()
+        return res
+
+
 class StepGraph:
     """Capture / replay state of one Environment (see the module docstring)."""
 
@@ -267,6 +310,9 @@ class StepGraph:
         self._bk_dst: List[Tensor] = []
         self._bk_u: Optional[Tensor] = None
         self._raw_exec: Optional[ctypes.c_void_p] = None
+        self._segments: List[torch.cuda.CUDAGraph] = []  # one graph per stretch between host holes
+        self._holes: List[Tuple[Any, tuple, Tensor]] = []  # (fn, args, output) run after segment i
+        self._executed = None  # outputs of a capture step that already ran (segmented capture)
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -314,6 +360,10 @@ class StepGraph:
             if self.status in ("warming", "dropped"):
                 if self.eager_steps >= WARM_STEPS:
                     if self._capture():
+                        if self._executed is not None:  # a segmented capture ran the step already
+                            out, self._executed = self._clone_outputs(), None
+                            self._asserts.after_replay(self.env.device)
+                            return out
                         return self._replay()
                 elif self.eager_steps == WARM_STEPS - 1:
                     self.eager_steps += 1
@@ -339,18 +389,32 @@ class StepGraph:
             warnings.simplefilter("always")
             torch.cuda.set_sync_debug_mode(1)
             self.env.world._assert_sink = _assert_unwatched
+            hole_waits = [0]
+
+            def hole(fn, args):  # a host hole runs eagerly in a captured step: its waits are allowed
+                m = torch.cuda.get_sync_debug_mode()
+                torch.cuda.set_sync_debug_mode(0)
+                h0 = lib.vmas_host_waits()
+                try:
+                    return fn(*args)
+                finally:
+                    hole_waits[0] += (lib.vmas_host_waits() - h0) & 0xFFFFFFFF
+                    torch.cuda.set_sync_debug_mode(m)
+
+            self.env.world._hole_sink = hole
             try:
                 with consts:
                     out = self.body()
             finally:
                 self.env.world._assert_sink = None
+                self.env.world._hole_sink = None
                 torch.cuda.set_sync_debug_mode(mode)
         self._trial_consts = consts  # the arena outlives the copies that read it
         # torch's warning: "called a synchronizing CUDA operation" (not the notice that the mode
         # is a prototype, which set_sync_debug_mode emits itself)
         syncs = [str(r.message).splitlines()[0] for r in rec
                  if "synchronizing" in str(r.message) and "prototype" not in str(r.message)]
-        native = (lib.vmas_host_waits() - w0) & 0xFFFFFFFF
+        native = ((lib.vmas_host_waits() - w0) & 0xFFFFFFFF) - hole_waits[0]
         if syncs or native:
             self.status = "eager"
             self.why = ("host sync in the step: " + (syncs[0] if syncs else f"{native} native host wait(s)"))[:300]
@@ -359,6 +423,7 @@ class StepGraph:
     def drop(self, why: str):
         self.graph = None
         self._raw_exec = None
+        self._segments, self._holes = [], []
         self.status = "dropped"
         self.why = why
         self.eager_steps = 0
@@ -381,7 +446,6 @@ class StepGraph:
                     versions[id(v)] = (v, v._version)
         dev = env.device
         rng = torch.cuda.get_rng_state(dev)
-        g = torch.cuda.CUDAGraph()
         consts = _CapturableConstants()
         side = torch.cuda.Stream(dev)
         prev_stream = torch.cuda.current_stream(dev)
@@ -396,10 +460,22 @@ class StepGraph:
         gc.collect()
         gc_was_on = gc.isenabled()
         gc.disable()
+        # contents of every tracked tensor: a capture that hits a host hole runs the segments
+        # before the hole for real, so a failure after that has state to restore
+        contents = [(t, t.clone()) for t, _ in versions.values()]
+        segs = _Segments(side)
         try:
             env.world._assert_sink = asserts.capture_sink
-            with torch.cuda.graph(g, stream=side), consts:
+            env.world._hole_sink = segs.hole
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(side), consts:
+                segs.begin()
                 out = self.body()
+                segs.end()
+                if segs.holes:  # the last segment too: the capture step has then run the step
+                    segs.graphs[-1].replay()
+            prev_stream.wait_stream(side)
+            g = segs.graphs[0]
             self._consts = consts
             self._asserts = asserts
             self._sig = eng.graph_token()
@@ -414,14 +490,18 @@ class StepGraph:
             # a capture invalidated by a forbidden call may be left open: end it, so that the
             # eager step that follows can launch
             N.load_library().vmas_stream_abort_capture(ctypes.c_void_p(side.cuda_stream))
-            # torch.cuda.graph's __exit__ leaves the capture stream current when capture_end
-            # raises: go back to the caller's stream
+            # capture_end may raise with the capture stream current: go back to the caller's
             torch.cuda.set_stream(prev_stream)
             torch.cuda.synchronize(dev)
             _reset_generator_capture_state(dev)
             for o, d in snap:
                 o.__dict__.clear()
                 o.__dict__.update(d)
+            if segs.ran:  # segments before a hole ran for real: put the tensors back
+                with torch.no_grad():
+                    for t, c in contents:
+                        t.copy_(c)
+                torch.cuda.synchronize(dev)
             torch.cuda.set_rng_state(rng, dev)
             self.status = "eager"
             self.why = f"{type(ex).__name__}: {str(ex).splitlines()[0] if str(ex) else ''}"[:300]
@@ -432,12 +512,16 @@ class StepGraph:
                 gc.enable()
             env._raw_outputs = False
             env.world._assert_sink = None
+            env.world._hole_sink = None
+        del contents
         self.graph = g
+        self._segments, self._holes = segs.graphs, segs.holes
         self._raw_exec = None
         self.replays = 0
         self.status = "graph"
         self.why = ""
-        self._first_replay = True
+        self._first_replay = not segs.holes
+        self._executed = out if segs.holes else None
         return True
 
     def _plan(self, objs, snap, out):
@@ -512,6 +596,13 @@ class StepGraph:
         that captured random ops read); if it did not advance the device generator, the graph
         draws no random numbers and later replays launch the instantiated graph directly
         (vmas_graph_launch), without the prologue's two fill kernels."""
+        if self._holes:  # segmented step: graph, host hole, graph, ... (torch replays)
+            for i, seg in enumerate(self._segments):
+                seg.replay()
+                if i < len(self._holes):
+                    fn, args, res = self._holes[i]
+                    fn(*args, out=res)
+            return
         if self._raw_exec is not None:
             from ... import _native as N
 

@@ -213,6 +213,19 @@ class ScenarioUtils:
         finds every env's first non-overlapping candidate (one sync per batch instead of one per
         try), and the generator is rewound to the state after exactly the reference's tries.
         """
+        sink = getattr(world, "_hole_sink", None)
+        if sink is not None:  # a graph-mode capture: this loop waits on the device, so it stays on the host
+            return sink(ScenarioUtils._find_random_pos_native,
+                        (occupied_positions, env_index, world, min_dist_between_entities, x_bounds, y_bounds,
+                         disable_warn))
+        return ScenarioUtils._find_random_pos_native(occupied_positions, env_index, world, min_dist_between_entities,
+                                                     x_bounds, y_bounds, disable_warn)
+
+    @staticmethod
+    def _find_random_pos_native(occupied_positions, env_index, world, min_dist_between_entities, x_bounds, y_bounds,
+                                disable_warn=False, out: Tensor = None):
+        """find_random_pos_for_entity's body; ``out`` (a replayed graph-mode step) receives the
+        positions in place of a new tensor."""
         batch_size = world.batch_dim if env_index is None else 1
         dev = torch.device(world.device)
 
@@ -223,6 +236,8 @@ class ScenarioUtils:
 
         if occupied_positions.shape[1] == 0:
             x, y = draw((batch_size, 1, 1))
+            if out is not None:
+                return torch.cat([x, y], dim=2, out=out)
             return torch.cat([x, y], dim=2)
 
         from .. import _native as N
@@ -237,7 +252,7 @@ class ScenarioUtils:
         occ = occupied_positions.detach()
         if occ.dtype != torch.float32:
             occ = occ.float()
-        pos = torch.empty((batch_size, 1, 2), device=dev, dtype=torch.float32)
+        pos = torch.empty((batch_size, 1, 2), device=dev, dtype=torch.float32) if out is None else out
         resolved = torch.full((batch_size,), -1, device=dev, dtype=torch.int32)
         states = []  # generator state after each try, to rewind to the reference's consumption
         # On a GPU the tries of a batch are drawn in one launch (vmas_uniform_columns: the same
