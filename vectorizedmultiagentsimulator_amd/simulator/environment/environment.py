@@ -418,7 +418,7 @@ class Environment(TorchVectorizedObject):
         time than the draws' launches)."""
         ur = agent.action.u_range
         key = (ur if type(ur) in (float, int) else tuple(ur), self.world.dim_c, agent.silent, agent.action_size,
-               agent.batch_dim)
+               agent.batch_dim, agent.device)
         c = self._draw_plans.get(agent)
         if c is None or c[0] != key:
             n_c = self.world.dim_c if (self.world.dim_c != 0 and not agent.silent) else 0
