@@ -411,17 +411,24 @@ struct Gen {
         }
     }
 
+    // Broadphase activity bits of a pair, gathered in wave-uniform words (fr<k> / fz<k>) over the
+    // wave's pair phase and ORed into the workgroup's LDS words once per substep (flag_flush).
     std::string flag_r(int p, const std::string& ind) const {  // R: some env within the broadphase radius
-        return ind + "if (a.blk) {\n" + ind + "    const unsigned long long bal = __ballot(inr && valid);\n" + ind +
-               "    if (lane == 0 && bal) atomicOr(&FL[s * " + it(W) + " + " + it(p >> 5) + "], " +
-               it(1u << (p & 31)) + "u);\n" + ind + "}\n";
+        return ind + "if (a.blk && __ballot(inr && valid)) fr" + it(p >> 5) + " |= " + it(1u << (p & 31)) + "u;\n";
     }
     std::string flag_z(int p, const std::string& ind) const {  // Z: an out-of-range env got a force
-        return ind + "if (a.blk) {\n" + ind +
-               "    const bool nz = valid && !inr && (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || o.tb != 0.f);\n" +
-               ind + "    const unsigned long long bal = __ballot(nz);\n" + ind +
-               "    if (lane == 0 && bal) atomicOr(&FL[(a.S + s) * " + it(W) + " + " + it(p >> 5) + "], " +
-               it(1u << (p & 31)) + "u);\n" + ind + "}\n";
+        return ind + "if (a.blk && __ballot(valid && !inr && (o.fa.x != 0.f || o.fa.y != 0.f || o.ta != 0.f || "
+                     "o.tb != 0.f))) fz" + it(p >> 5) + " |= " + it(1u << (p & 31)) + "u;\n";
+    }
+    std::string flag_flush(const std::vector<char>& words) const {
+        std::string o;
+        for (int k = 0; k < W; ++k)
+            if (words[k])
+                o += "        if (lane == 0) {\n"
+                     "            if (fr" + it(k) + ") atomicOr(&FL[s * " + it(W) + " + " + it(k) + "], fr" + it(k) + ");\n"
+                     "            if (fz" + it(k) + ") atomicOr(&FL[(a.S + s) * " + it(W) + " + " + it(k) + "], fz" +
+                     it(k) + ");\n        }\n";
+        return o;
     }
     // result rows a whole pair needs: no torque is ever read from a sphere-sphere result, and
     // none for the sphere side of a line/box-sphere result (the entity items' torque flags)
@@ -560,7 +567,12 @@ struct Gen {
             for (const Item& x : items[e]) word[x.pair >> 5] = 1;
         for (int k = 0; k < W; ++k)
             if (word[k]) o += "        const uint32_t m" + it(k) + " = MSK[s * " + it(W) + " + " + it(k) + "];\n";
+        std::vector<char> fword(W, 0);  // flag words this wave's tasks set
+        for (const Task& t : wave_tasks[w]) fword[t.pair >> 5] = 1;
+        for (int k = 0; k < W; ++k)
+            if (fword[k]) o += "        uint32_t fr" + it(k) + " = 0u, fz" + it(k) + " = 0u;\n";
         for (const Task& t : wave_tasks[w]) task_code(o, t, w);
+        o += flag_flush(fword);
         o += "        " + stamp(w, "s * 4");
         o += "        __syncthreads();\n";
         o += "        " + stamp(w, "s * 4 + 1");
