@@ -217,13 +217,24 @@ struct Gen {
         }
         // pair tasks: longest-processing-time over the waves.  Contact-case costs in units of a
         // sphere-sphere contact, measured per wave with tools/jit_phase_profile.py.
-        static const float kCost[7] = {1.5f, 1.0f, 2.0f, 1.8f, 2.2f, 7.4f, 30.f};
+        // A sphere-sphere pair mostly takes the exact early-out (out of contact in all 64 envs), so
+        // it is priced at half a contact; a split pair's finish is placed by the LPT with the
+        // other tasks (last in its wave), priced at 3.  Measured (profiles/r01/run27_schedule):
+        // k_world balance 66.3 -> 64.4 us, transport 10.2 -> 9.9 us against SS 1.0 and the
+        // finish placed after all other tasks.  VMAS_JIT_COST_SS / VMAS_JIT_COST_FINISH /
+        // VMAS_JIT_FINISH_LPT=0 override (A/B).
+        float kCost[7] = {1.5f, 0.5f, 2.0f, 1.8f, 2.2f, 7.4f, 30.f};
+        float finish_cost = 3.0f;
+        if (const char* c = getenv("VMAS_JIT_COST_SS")) kCost[VMAS_PAIR_SS] = (float)atof(c);
+        if (const char* c = getenv("VMAS_JIT_COST_FINISH")) finish_cost = (float)atof(c);
+        const char* fl_lpt = getenv("VMAS_JIT_FINISH_LPT");
+        const bool finish_in_lpt = !(fl_lpt && fl_lpt[0] == '0');
         std::vector<Task> all, finishes;
         for (int p = 0; p < P; ++p) {
             if (split[p]) {
                 for (int k = 0; k < parts(pd[p].cls); ++k)
                     all.push_back({p, k, pd[p].cls == VMAS_PAIR_BL ? 1.8f : 3.8f});
-                finishes.push_back({p, kFinish, 1.5f});
+                (finish_in_lpt ? all : finishes).push_back({p, kFinish, finish_cost});
             } else {
                 all.push_back({p, kWhole, kCost[pd[p].cls]});
             }
@@ -241,8 +252,9 @@ struct Gen {
         // a finish has run all of its parts
         for (auto& v : wave_tasks)
             std::stable_sort(v.begin(), v.end(), [](const Task& a, const Task& b) {
-                const bool pa = a.part >= 0, pb = b.part >= 0;
-                return pa != pb ? pa : a.pair < b.pair;
+                const int ra = a.part >= 0 ? 0 : a.part == kFinish ? 2 : 1;  // parts, wholes, finishes
+                const int rb = b.part >= 0 ? 0 : b.part == kFinish ? 2 : 1;
+                return ra != rb ? ra < rb : a.pair < b.pair;
             });
         for (const Task& t : finishes) place(t);
         // entity phase: dynamic entities over the waves by contribution count (LPT)
