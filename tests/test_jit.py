@@ -97,3 +97,23 @@ def test_oversized_world_runs_generic_kernel_gpu(gpu_device):
         assert rep["ok"], rep
     assert env.world.engine.kernel_name == "k_step"
     assert "LDS budget" in env.world.engine.jit_error
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps", [s for s in SPECIALISED if s[0] in ("balance", "flocking")],
+                         ids=["balance", "flocking"])
+def test_jit_nan_state_matches_oracle_gpu(gpu_device, name, kw, substeps):
+    """A NaN agent position in one env: NaN envs are never in broadphase range but get NaN
+    forces from pairs that other envs keep active -- the fixed point's Z bits (an out-of-range env
+    got a nonzero force) must still see them (k_world reduces a sphere pair's Z test to a NaN
+    test).  The step must match the oracle's, NaN pattern included."""
+    env = make(name, kw, substeps, gpu_device, num_envs=300, seed=6)
+    for _ in range(2):
+        env.step(env.get_random_actions())
+    assert env.world.engine.kernel_name == "k_world"
+    a = env.world.agents[1]
+    with torch.no_grad():
+        a.state.pos[5, 0] = float("nan")
+        a.state.pos[17, 1] = float("nan")
+    report = O.compare_one_step(env.world)
+    assert report["ok"], report

@@ -2,7 +2,7 @@
 # Interleaved A/B of two builds of the library (abtmp/libvmas_{new,old}.so, swapped into the package).
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/ab_flags
+OUT=gpurun_out/ab_two
 mkdir -p $OUT
 LIB=vectorizedmultiagentsimulator_amd/libvmas_mi355x.so
 for rep in 1 2 3; do

@@ -510,7 +510,16 @@ struct Gen {
             else
                 o += I + "    const PairOut o = " + pair_call(p, w) + ";\n";
             o += store_res(p, I + "    ");
-            if (q.cls != VMAS_PAIR_JOINT) o += flag_z(p, I + "    ");
+            // A sphere pair whose squared broadphase limit is at or beyond its contact limit: an env
+            // out of range gets exactly zero force (core.py:2832, dist > dist_min) unless its
+            // distance is NaN (then the force is NaN), so Z reduces to "some valid env has a NaN
+            // distance" -- no dependency on the force.
+            const bool z_nan_only = q.cls == VMAS_PAIR_SS && sq_limit(q.bp_radius) >= sq_limit(q.dmin);
+            if (z_nan_only)
+                o += I + "    if (a.blk && __ballot(valid && d2 != d2)) fz" + it(p >> 5) + " |= " + it(1u << (p & 31)) +
+                     "u;\n";
+            else if (q.cls != VMAS_PAIR_JOINT)
+                o += flag_z(p, I + "    ");
             o += I + "}\n        }\n";
             return;
         }
