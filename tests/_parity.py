@@ -14,6 +14,9 @@ SCENARIOS = [
     ("flocking", dict(n_agents=4), None),    # S-S, scripted agent, LIDAR on obstacles
     ("pollock", dict(n_agents=4, n_lines=3, n_boxes=3, lidar=True), None),  # all 6 classes + box/line rays
     ("waterfall", dict(n_agents=5), None),   # joints (rotate / fixed rotation), L-L, B-L, B-B
+    # friction (world + entity), force/torque clamps, max_speed / v_range, [B,2] entity gravity,
+    # hollow + solid boxes vs spheres / lines / boxes, dim_c > 0 (scenarios/debug/features.py)
+    ("features", dict(n_agents=4), None),
 ]
 
 
@@ -35,12 +38,19 @@ def step_parity(env, n_steps, broadphase="batch", max_bad_frac=0.0):
     return reports
 
 
+# ray perturbations that certify a LIDAR mismatch as a hit/miss boundary case: the engine's value
+# must equal the oracle's for a ray turned by a few 1e-7 rad (a last-bit difference of the
+# angle's sin/cos) -- a tangent ray, a slab edge of a box, a line end point
+_RAY_CERT_DELTAS = (-1e-6, -3e-7, 3e-7, 1e-6)
+
+
 def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0):
-    """Every agent sensor: engine measure() vs the oracle's cast_rays on the same state/angles."""
+    """Every agent sensor: engine measure() vs the oracle's cast_rays on the same state/angles.
+    A (env, ray) outside atol/rtol passes only when certified as a boundary case (see above)."""
     w = env.world
     snap = O.snapshot(w)
     ow = O.OracleWorld(w, snap)
-    worst, n_bad, n_tot = 0.0, 0, 0
+    worst, n_bad, n_unc, n_tot = 0.0, 0, 0, 0
     for agent in w.agents:
         ai = w.entities.index(agent)
         for sensor in agent.sensors:
@@ -51,8 +61,15 @@ def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0):
             bad = diff > atol + rtol * exp.abs()
             worst = max(worst, float(diff.max()))
             n_bad += int(bad.any(-1).sum())
+            if bad.any():
+                cert = torch.zeros_like(bad)
+                for d in _RAY_CERT_DELTAS:
+                    e2 = ow.cast_rays(ai, angles + d, sensor._max_range, sensor.entity_filter)
+                    cert |= (got - e2).abs() <= atol + rtol * e2.abs()
+                n_unc += int((bad & ~cert).any(-1).sum())
             n_tot += got.shape[0]
-    return {"ok": n_bad <= max_bad_frac * max(n_tot, 1), "max_abs": worst, "bad_rows": n_bad, "rows": n_tot}
+    return {"ok": n_unc <= max_bad_frac * max(n_tot, 1), "max_abs": worst, "bad_rows": n_bad,
+            "uncertified_rows": n_unc, "rows": n_tot}
 
 
 def distance_parity(env, atol=2e-5):

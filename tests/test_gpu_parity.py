@@ -2,8 +2,10 @@
 
 Sizes: every scenario at 200 envs (4 steps each), the C2 benchmark world (balance, 4 agents,
 10 substeps) at its full 32 768 envs, LIDAR and distance queries.  Tolerance: fp32 atol/rtol +
-4x the system's own 1-ulp sensitivity band (oracle.vmas_oracle.compare); at 32 768 envs at most
-0.1% of envs may sit on a discontinuous contact cut-off (dist == dist_min within an ulp).
+4x the system's own 1-ulp sensitivity band (oracle.vmas_oracle.compare).  An env outside it passes
+only when the oracle certifies it sits on a discontinuous contact cut-off (|dist - dist_min| <=
+oracle.CUTOFF_TOL at some contact evaluation of the step); a LIDAR row outside it only when turning
+the ray by at most 1e-6 rad moves the oracle onto the engine's value (a hit/miss boundary).  No unexplained env is allowed at any size.
 """
 import pytest
 import torch
@@ -34,7 +36,7 @@ def test_lidar_distance_parity_gpu(gpu_device, name, kw, substeps):
     env = make(name, kw, substeps, gpu_device, num_envs=256, seed=3)
     for _ in range(3):
         env.step(env.get_random_actions())
-    rep = lidar_parity(env, max_bad_frac=1e-3)
+    rep = lidar_parity(env)
     assert rep["ok"], rep
     rep = distance_parity(env)
     assert rep["ok"], rep
@@ -43,7 +45,7 @@ def test_lidar_distance_parity_gpu(gpu_device, name, kw, substeps):
 def test_balance_full_size_gpu(gpu_device):
     """C2 at full size: 32 768 envs, n_agents=4, 10 substeps."""
     env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=32768, seed=0)
-    for rep in step_parity(env, n_steps=2, max_bad_frac=1e-3):
+    for rep in step_parity(env, n_steps=2):
         assert rep["ok"], rep
 
 
@@ -71,8 +73,8 @@ def test_batch_broadphase_fixed_point_gpu(gpu_device):
 
 
 @pytest.mark.parametrize("split", ["0", "1"])
-@pytest.mark.parametrize("name,kw,substeps", [s for s in SCENARIOS if s[0] in ("balance", "pollock", "waterfall")],
-                         ids=["balance", "pollock", "waterfall"])
+@pytest.mark.parametrize("name,kw,substeps", [s for s in SCENARIOS if s[0] in ("balance", "pollock", "waterfall", "features")],
+                         ids=["balance", "pollock", "waterfall", "features"])
 def test_split_box_pairs_gpu(gpu_device, monkeypatch, split, name, kw, substeps):
     """Box-line / box-box pairs evaluated whole by one wave (split=0) or as per-side parts on
     several waves plus a finish phase (split=1) give the oracle's result either way."""
@@ -89,9 +91,9 @@ def test_split_box_pairs_gpu(gpu_device, monkeypatch, split, name, kw, substeps)
 ], ids=["C3_transport", "C4_discovery", "C5_flocking"])
 def test_baseline_configs_full_size_gpu(gpu_device, name, kw, envs):
     """BASELINE.json configs C3-C5 at their full per-GPU sizes: teacher-forced step parity and
-    LIDAR parity against the oracle (0.1 % of envs may sit on a contact cut-off)."""
+    LIDAR parity against the oracle (only certified cut-off envs may differ)."""
     env = make(name, kw, None, gpu_device, num_envs=envs, seed=0)
-    for rep in step_parity(env, n_steps=2, max_bad_frac=1e-3):
+    for rep in step_parity(env, n_steps=2):
         assert rep["ok"], rep
-    rep = lidar_parity(env, max_bad_frac=1e-3)
+    rep = lidar_parity(env)
     assert rep["ok"], rep

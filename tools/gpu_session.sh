@@ -19,7 +19,7 @@ rocm-smi --showproductname > gpurun_out/gpu_info.log 2>&1 || true
 lscpu > gpurun_out/lscpu.log 2>&1 || true
 for step in ${SESSION_STEPS:-tests bench prof}; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     bench) run bench 600 python bench.py --steps "$STEPS" --warmup 10 ;;
     benchenv) run bench_env 600 python bench.py --steps "$STEPS" --warmup 10 --broadphase env --cpu-steps 0 ;;

@@ -452,7 +452,7 @@ class PhysicsEngine:
         """What a captured step depends on besides tensor contents: the static tables (entity /
         joint / world parameters), the kernel object and the step parameters."""
         w = self.world
-        return (self._signature(), int(w._substeps), w._dt, w.broadphase, id(self._jit), id(self._handle))
+        return (self._signature(), int(w._substeps), w._sub_dt, w.broadphase, id(self._jit), id(self._handle))
 
     def get_timing(self, reset: bool = True):
         """(milliseconds, launches) of the step kernel (k_world or k_step) since the last reset."""
@@ -585,10 +585,13 @@ class PhysicsEngine:
         io = self._io
         io.out_pos, io.out_vel, io.out_rot = base + 4 * o_pos, base + 4 * o_vel, base + 4 * o_rot
         io.out_ang_vel, io.out_force, io.out_torque = base + 4 * o_ang, base + 4 * o_force, base + 4 * o_torque
-        params = (w._substeps, w._dt, w.broadphase)
+        # the substep loop runs w._substeps times with the world's own w._sub_dt attribute, as
+        # ref core.py:1977 / 2068 / 2870 / 2879 / 2905 / 2907 read them (two independent
+        # attributes: setting one does not update the other)
+        params = (w._substeps, w._sub_dt, w.broadphase)
         if params != self._step_params:
             io.substeps = int(w._substeps)
-            io.sub_dt = _f32(w._dt / w._substeps)
+            io.sub_dt = _f32(w._sub_dt)
             io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
             self._step_params = params
         iters = ctypes.c_int32(0)
