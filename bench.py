@@ -17,8 +17,11 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus:
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -41,8 +44,11 @@ def parse():
     p.add_argument("--n-agents", type=int, default=4)
     p.add_argument("--substeps", type=int, default=10)
     p.add_argument("--broadphase", default="batch", choices=["batch", "env"])
-    p.add_argument("--cpu-steps", type=int, default=6, help="timed CPU-oracle steps (0 = skip)")
+    p.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-oracle steps per repeat (0 = skip)")
+    p.add_argument("--cpu-repeats", type=int, default=5, help="CPU-oracle repeats (the median is reported)")
     p.add_argument("--cpu-envs", type=int, default=32768)
+    p.add_argument("--event-launches", type=int, default=20,
+                   help="extra eager step launches timed with HIP events after the timed region")
     p.add_argument("--device", default=None, help="override device (e.g. cpu for plumbing tests)")
     p.add_argument("--graph", default="on", choices=["on", "off"],
                    help="on: make_env(graph_step=True) -- each step replayed as one HIP graph once warm "
@@ -68,26 +74,48 @@ def make_world_env(args, device, seed):
 
 def alg_bytes_per_env_step(world) -> int:
     """read pos/vel/rot/ang_vel of every entity (24 B), write them for every
-    movable-or-rotatable entity (24 B), read every agent's force + torque (12 B)."""
+    movable-or-rotatable entity (24 B), read every agent's force + torque (12 B), write every
+    LIDAR ray distance (4 B per ray of every agent sensor)."""
     ents = world.entities
     e_dyn = sum(1 for e in ents if e.movable or e.rotatable)
     n_agents = len(world.agents)
-    return 24 * len(ents) + 24 * e_dyn + 12 * n_agents
+    rays = sum(s._angles.shape[-1] for a in world.agents for s in a.sensors if hasattr(s, "_angles"))
+    return 24 * len(ents) + 24 * e_dyn + 12 * n_agents + 4 * rays
 
 
-def load_pmc(workload: str, kernel: str) -> dict:
+def kernel_source_hash(world) -> str:
+    """sha256 of the generated step kernel's source (k_world) -- what a PMC record must match."""
+    src = world.engine.jit_source()
+    return hashlib.sha256(src.encode()).hexdigest() if src else ""
+
+
+def load_pmc(workload: str, kernel: str, src_hash: str) -> dict:
     """Per-launch PMC record of the step kernel (profiles/pmc_traffic.json, written by
-    tools/pmc_traffic.py), if it was measured on this workload and this kernel."""
+    tools/pmc_traffic.py from rocprofv3 CSVs kept under profiles/), only if it was measured on
+    this workload AND on this exact kernel (the generated source's sha256)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return {}
     try:
         d = json.loads(f.read_text())
-        if d.get("workload") == workload and d.get("kernel") == kernel:
-            return d
     except Exception:
         return {}
-    return {}
+    if d.get("workload") != workload or d.get("kernel") != kernel:
+        return {"stale": "record is for another workload / kernel"}
+    if not src_hash or d.get("kernel_source_sha256") != src_hash:
+        return {"stale": "record was measured on another k_world source (sha256 mismatch)"}
+    return d
+
+
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
 
 
 # VALU issue peak of the MI355X (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU
@@ -97,25 +125,42 @@ VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
 
 
 def cpu_baseline(args):
-    """Oracle physics (torch CPU, reference op sequence) under the same host layer."""
+    """Oracle physics (torch CPU, reference op sequence) under the same host layer: the median of
+    ``--cpu-repeats`` timings of ``--cpu-steps`` steps, at the bench's substeps and at substeps=1
+    (BASELINE.md's reference number is quoted at substeps=1)."""
     from oracle import vmas_oracle
 
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-    env = make_world_env(args, "cpu-baseline", seed=0)
-    vmas_oracle.install(env.world)
-    env.step(env.get_random_actions())  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        env.step(env.get_random_actions())
-    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+
+    def timed(substeps):
+        a = argparse.Namespace(**vars(args))
+        a.substeps = substeps
+        env = make_world_env(a, "cpu-baseline", seed=0)
+        vmas_oracle.install(env.world)
+        env.step(env.get_random_actions())  # warm-up
+        rates = []
+        for _ in range(args.cpu_repeats):
+            t0 = time.perf_counter()
+            for _ in range(args.cpu_steps):
+                env.step(env.get_random_actions())
+            rates.append(args.cpu_envs * args.cpu_steps / (time.perf_counter() - t0))
+        return statistics.median(rates), rates
+
+    med, rates = timed(args.substeps)
+    med1, rates1 = timed(1)
     return {
-        "value": args.cpu_envs * args.cpu_steps / dt,
+        "value": med,
         "unit": "env-steps/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": f"{args.scenario} {args.cpu_envs} envs x {args.cpu_steps} steps (after 1 warm-up), "
-                  f"substeps={args.substeps}, PyTorch-CPU oracle physics",
-        "ms_per_step": 1e3 * dt / args.cpu_steps,
+        "cpu_model": cpu_model(),
+        "sample": f"{args.scenario} {args.cpu_envs} envs, median of {args.cpu_repeats} x {args.cpu_steps} steps "
+                  f"(after 1 warm-up), substeps={args.substeps}, PyTorch-CPU oracle physics, "
+                  f"{torch.get_num_threads()} threads",
+        "repeats": [round(r, 1) for r in rates],
+        "substeps1": {"value": med1, "repeats": [round(r, 1) for r in rates1],
+                      "note": "same sample at substeps=1 (the configuration of BASELINE.md's reference CPU number)"},
     }
 
 
@@ -172,6 +217,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     kernel_ms, launches, timer, clock_ghz = 0.0, 0, None, 0.0
+    event_us = None
     if on_gpu:
         dev_ms, dev_n, clock_ghz = world.engine.device_timing(reset=True, with_clock=True)
         if env.graph_status == "graph":
@@ -182,6 +228,15 @@ def main():
         else:
             kernel_ms, launches = world.engine.get_timing(reset=True)
             timer = "HIP events on the launch's dispatch packet (hipExtModuleLaunchKernel)"
+        if args.event_launches > 0:
+            # after the timed region: eager launches of the same step kernel on the same state
+            # chain, timed by HIP events on their own dispatch packets (what rocprofv3's kernel
+            # trace measures; the in-kernel timer misses the launch ramp and the exit tail)
+            world.engine.get_timing(reset=True)
+            for _ in range(args.event_launches):
+                world.step()
+            ev_ms, ev_n = world.engine.get_timing(reset=True)
+            event_us = 1e3 * ev_ms / ev_n if ev_n else None
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -199,7 +254,8 @@ def main():
     if on_gpu and launches:
         per_launch_ms = kernel_ms / launches
         achieved = b_env * args.envs / (per_launch_ms * 1e-3) / 1e9
-        pmc = load_pmc(workload, world.engine.kernel_name)
+        src_hash = kernel_source_hash(world)
+        pmc = load_pmc(workload, world.engine.kernel_name, src_hash)
         traffic = pmc.get("hbm_bytes_per_launch")
         roofline = {
             "bound": "hbm",
@@ -213,6 +269,10 @@ def main():
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,
             "timer": timer,
+            "kernel_us_event": round(event_us, 3) if event_us else None,
+            "frac_event": round(b_env * args.envs / (event_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5) if event_us else None,
+            "kernel_source_sha256": src_hash,
+            "pmc_record": ("profiles/pmc_traffic.json" if traffic else pmc.get("stale", "none")),
         }
         if pmc.get("valu_insts_per_launch"):
             # the bound the kernel actually meets: VALU issue, from PMC SQ_INSTS_VALU

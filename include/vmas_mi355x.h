@@ -215,6 +215,11 @@ int32_t vmas_graph_launch(void* graph_exec, void* stream);
  * tell whether the step can be captured (no reference counterpart). */
 int32_t vmas_host_waits(void);
 
+/* Test utility (no reference counterpart): launches `blocks` workgroups of 256 threads on
+ * `stream` that each occupy their CU for `microseconds` (<= 5 s) -- a kernel of another stream
+ * holding CUs while a step runs (tests/test_jit.py). */
+int32_t vmas_test_hold(int32_t device, int32_t blocks, int64_t microseconds, void* stream);
+
 int32_t vmas_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
                           const VmasPairDesc* pairs, const VmasJointDesc* joints,
                           VmasWorld** out_world);
@@ -347,6 +352,43 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
                            int32_t* resolved, int32_t* max_accepted, int32_t* n_unresolved,
                            void* stream);
 
+/* ---- fused scenario programs (csrc/vmas_scenarios.hip) -------------------
+ * One launch computes a benchmark scenario's per-step observation / reward / done tensor program
+ * (one thread per env, the reference's fp32 operations in its order).  Error reporting as the
+ * other auxiliary entry points (vmas_aux_last_error). */
+typedef struct VmasVec { /* a [B, 2] or [B, 1] fp32 tensor: element (b, k) at p[b * s0 + k * s1] */
+    const float* p;
+    int32_t s0, s1;
+} VmasVec;
+
+#define VMAS_SCN_MAX_AGENTS 32
+#define VMAS_SCN_REWARD 1 /* the first agent's reward call and every agent's reward */
+#define VMAS_SCN_OBS 2    /* every agent's observation */
+#define VMAS_SCN_DONE 4   /* done() */
+
+/* balance (reference vmas/scenarios/balance.py:205-262): replaces, for all agents at once,
+ * Scenario.reward (compute_on_the_ground, the package-goal norm, ground / position rewards, the
+ * global shaping update, ground_rew + pos_rew per agent), Scenario.observation (torch.cat of 9
+ * pieces, 16 entries) and Scenario.done. */
+typedef struct VmasBalanceIO {
+    int32_t batch, n_agents, what, pad0;
+    float shaping_factor, fall_reward, pi, pad1; /* pi: f32(math.pi), the `% torch.pi` divisor */
+    VmasShapeRef package, goal, line, floor;     /* shapes + pos / rot, as for vmas_distance */
+    VmasVec package_vel, line_vel, line_ang_vel;
+    VmasVec agent_pos[VMAS_SCN_MAX_AGENTS], agent_vel[VMAS_SCN_MAX_AGENTS];
+    const float* global_shaping; /* [B] (stride gs_s0) in: the previous shaping */
+    int32_t gs_s0, pad2;
+    float* global_shaping_out;   /* [B] REWARD outputs (fresh tensors) */
+    float* package_dist;
+    float* pos_rew;
+    float* ground_rew;           /* [B] written in place (the reference's [:] = 0 + masked_fill_) */
+    uint8_t* on_the_ground;      /* [B] torch.bool: REWARD output, DONE input */
+    float* rewards[VMAS_SCN_MAX_AGENTS]; /* [B] per agent (REWARD) */
+    float* obs[VMAS_SCN_MAX_AGENTS];     /* [B, 16] contiguous per agent (OBS) */
+    uint8_t* done;                       /* [B] torch.bool (DONE) */
+} VmasBalanceIO;
+int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream);
+
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);
 
@@ -361,9 +403,11 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
                               const VmasPairDesc* pairs, const VmasJointDesc* joints,
                               VmasJitWorld** out_world);
 int32_t vmas_jit_world_destroy(VmasJitWorld* world);
-/* With the batch broadphase the step is one persistent launch that runs every fixed-point pass
- * on the device (no host wait): *iterations is then 0 and vmas_jit_world_passes reports the
- * count.  A device-side failure (no convergence, a wait timeout) is returned by
+/* With the batch broadphase the step is a relay of launches on `stream` that runs every
+ * fixed-point pass on the device (no host wait, no workgroup waiting for another): pass 0, then
+ * substeps + 1 rerun launches that exit at once unless the previous pass found the mask violated.
+ * *iterations is then 0 and vmas_jit_world_passes reports the count.  A fixed point that did not
+ * converge writes NaN over the step's outputs and is returned by
  * vmas_jit_world_passes and by the next vmas_jit_world_step. */
 int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
                             int32_t* iterations);
@@ -372,15 +416,15 @@ int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* str
 int32_t vmas_jit_world_check(VmasJitWorld* world);
 /* Fixed-point passes of the last step (waits for it on its stream). */
 int32_t vmas_jit_world_passes(VmasJitWorld* world, int32_t* passes);
-/* Persistent grid size: > 0 cooperative launch, < 0 plain launch, 0 host-driven passes
- * (VMAS_JIT_GRID=coop|plain|host at create). */
+/* Relay grid size, returned negative (plain launches); 0: host-driven passes
+ * (VMAS_JIT_GRID=relay|host at create). */
 int32_t vmas_jit_world_grid(const VmasJitWorld* world);
 int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
 int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
                                   int64_t* launches);
-/* Device timer (timing on; persistent batch-broadphase launches): the kernel itself accumulates,
- * per launch, the span from workgroup 0's start to the final fixed-point reduction, after which
- * every workgroup exits (s_memrealtime, converted with the device's wall-clock rate);
+/* Device timer (timing on; batch-broadphase relay launches): the kernel itself accumulates,
+ * per step, the span from pass 0 workgroup 0's start to the final fixed-point reduction (the
+ * rerun launches that exit at once after it are not counted) (s_memrealtime, converted with the device's wall-clock rate);
  * *clock_ghz (may be NULL) is the in-kernel shader clock (s_memtime / s_memrealtime spans).  It also times launches replayed from a HIP graph, where HIP records
  * no events.  Waits for the device.  (bench.py's roofline timer; no reference counterpart.) */
 int32_t vmas_jit_world_device_timing(VmasJitWorld* world, int32_t reset, double* total_ms,

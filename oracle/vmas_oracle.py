@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """ORACLE -- test infrastructure only (never imported by the product package).
 
 A PyTorch-CPU restatement of the reference's tensor programs for the hot path:

@@ -305,3 +305,32 @@ def test_trial_step_detects_host_waits():
 
     lib = N.load_library()
     assert isinstance(lib.vmas_host_waits(), int)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["python_counter", "numpy_rng", "torch_cpu_rng"])
+def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
+    """A step that keeps Python-side state (a Python-int counter) or draws from a host RNG would
+    be frozen by a replay: graph mode must detect it in the trial step and stay eager."""
+    import numpy as np
+
+    env = make_env("balance", num_envs=64, device=gpu_device, seed=0, graph_step=True, n_agents=2)
+    sc = env.scenario
+    orig = sc.post_step
+    sc.count = 0
+
+    def post_step():
+        orig()
+        if kind == "python_counter":
+            sc.count += 1
+        elif kind == "numpy_rng":
+            np.random.rand()
+        else:
+            torch.rand(1)
+
+    sc.post_step = post_step
+    for _ in range(5):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "eager", env.graph_reason
+    expect = "Python-side state" if kind == "python_counter" else "host RNG"
+    assert expect in env.graph_reason, env.graph_reason

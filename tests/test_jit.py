@@ -1,6 +1,8 @@
 """World-specialised step kernels (csrc/vmas_jit.hip, hipRTC): every benchmark/parity world's
 kernel is generated and compiles for gfx950 (CPU check); on the GPU it runs (kernel_name
 'k_world'), matches the oracle, and is bit-identical to the generic k_step on the same state."""
+import ctypes
+
 import pytest
 import torch
 
@@ -36,6 +38,9 @@ def test_jit_parity_and_bit_identity_gpu(gpu_device, monkeypatch, name, kw, subs
     ref = make(name, kw, substeps, gpu_device, num_envs=300, seed=4)
     snap = O.snapshot(env.world)
     O.load_snapshot(ref.world, snap)
+    for a, ra in zip(env.world.agents, ref.world.agents):  # (dim_c > 0: the comm update reads it)
+        if a.action.c is not None:
+            ra.action.c = a.action.c.clone()
     for bp in ("batch", "env"):
         O.load_snapshot(env.world, snap)
         O.load_snapshot(ref.world, snap)
@@ -64,11 +69,16 @@ def test_jit_balance_full_size_gpu(gpu_device):
     ("waterfall", dict(), None, 700),
 ], ids=["balance100k", "flocking", "waterfall"])
 def test_device_fixed_point_matches_host_loop_gpu(gpu_device, monkeypatch, name, kw, substeps, num_envs):
-    """The persistent launch (fixed-point passes on the device, cooperative or plain launch)
-    is bit-identical to the host-driven pass loop and runs the same number of passes."""
+    """The relay (fixed-point passes on the device, one launch per pass, no cross-workgroup
+    wait; also with a grid far below the group count) is bit-identical to the host-driven pass
+    loop and runs the same number of passes."""
     envs = {}
-    for mode in ("host", "coop", "plain"):
-        monkeypatch.setenv("VMAS_JIT_GRID", mode)
+    for mode, cap in (("host", None), ("relay", None), ("relay37", "37")):
+        monkeypatch.setenv("VMAS_JIT_GRID", mode[:5])
+        if cap:
+            monkeypatch.setenv("VMAS_JIT_GRID_CAP", cap)
+        else:
+            monkeypatch.delenv("VMAS_JIT_GRID_CAP", raising=False)
         envs[mode] = make(name, kw, substeps, gpu_device, num_envs=num_envs, seed=2)
         envs[mode].world.engine._ensure()  # the mode is read when the kernel is built
     snap = O.snapshot(envs["host"].world)
@@ -79,15 +89,78 @@ def test_device_fixed_point_matches_host_loop_gpu(gpu_device, monkeypatch, name,
             env.world.step()
         eng = {m: e.world.engine for m, e in envs.items()}
         assert eng["host"].kernel_name == "k_world" and eng["host"].jit_grid == 0
-        assert eng["coop"].jit_grid > 0 and eng["plain"].jit_grid < 0
+        assert eng["relay"].jit_grid < 0 and eng["relay37"].jit_grid == -min(37, (num_envs + 63) // 64)
         passes = {m: e.last_iterations for m, e in eng.items()}
-        assert passes["coop"] == passes["plain"] == passes["host"] >= 1, passes
+        assert passes["relay"] == passes["relay37"] == passes["host"] >= 1, passes
         a = O.snapshot(envs["host"].world)
-        for mode in ("coop", "plain"):
+        for mode in ("relay", "relay37"):
             b = O.snapshot(envs[mode].world)
             for i in a:
                 for k in a[i]:
                     assert torch.equal(a[i][k], b[i][k]), (mode, i, k)
+
+
+def _violating_pollock(device):
+    """A 2-env world whose all-active first pass violates the batch broadphase: a line/sphere
+    pair just outside the circumscribed radius in both envs, inside the thin contact shell."""
+    env = make("pollock", dict(n_agents=1, n_lines=1, n_boxes=0), None, device, num_envs=2, seed=0)
+    w = env.world
+    line, agent = w.landmarks[0], w.agents[0]
+    d = line.shape.length / 2 + agent.shape.radius + 0.002
+    agent.set_pos(torch.tensor([[d, 0.0], [d, 0.0]], device=w.device), batch_index=None)
+    agent.set_vel(torch.zeros(2, 2, device=w.device), batch_index=None)
+    line.set_pos(torch.zeros(2, 2, device=w.device), batch_index=None)
+    line.set_rot(torch.zeros(2, 1, device=w.device), batch_index=None)
+    return env
+
+
+@pytest.mark.gpu
+def test_relay_rerun_pass_gpu(gpu_device):
+    """The violating world needs the rerun launch (2 passes) and then equals the oracle."""
+    env = _violating_pollock(gpu_device)
+    rep = O.compare_one_step(env.world)
+    assert env.world.engine.kernel_name == "k_world"
+    assert rep["ok"], rep
+    assert rep["iterations"] == 2, rep
+
+
+@pytest.mark.gpu
+def test_relay_no_convergence_poisons_outputs_gpu(gpu_device, monkeypatch):
+    """A relay capped at one pass cannot converge on the violating world: the step's outputs are
+    NaN (visible in the step itself) and the sticky error is raised by the next check."""
+    monkeypatch.setenv("VMAS_JIT_RELAY", "1")
+    env = _violating_pollock(gpu_device)
+    env.world.engine._ensure()
+    env.world.step()
+    torch.cuda.synchronize()
+    agent = env.world.agents[0]
+    assert torch.isnan(agent.state.pos).all() and torch.isnan(agent.state.vel).all()
+    with pytest.raises(Exception, match="fixed point"):
+        env.world.engine.check_device_errors()
+
+
+@pytest.mark.gpu
+def test_relay_with_cus_held_by_another_stream_gpu(gpu_device):
+    """A kernel on a second stream holds half of the chip's wave slots for 0.5 s while the step
+    launches: part of the step's grid cannot become resident until it ends.  The relay has no
+    cross-workgroup wait, so the step completes exactly (oracle parity, no error bit)."""
+    from vectorizedmultiagentsimulator_amd import _native as N
+
+    env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=32768, seed=0)
+    env.step(env.get_random_actions())
+    w = env.world
+    snap = O.snapshot(w)
+    expected, ow = O.oracle_step(w, snap)
+    band = O.sensitivity_band(w, snap, expected)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    N.check_aux(N.load_library().vmas_test_hold(0, 1024, 500_000, ctypes.c_void_p(side.cuda_stream)),
+                "vmas_test_hold")
+    w.step()
+    torch.cuda.synchronize()
+    w.engine.check_device_errors()
+    rep = O.compare(O.snapshot(w), expected, w, band=band, cutoff=ow.cutoff_margin)
+    assert rep["ok"], rep
 
 
 @pytest.mark.gpu

@@ -18,7 +18,7 @@ for counters in "${GROUPS_[@]}"; do
   i=$((i+1))
   echo "=== $TAG pass $i: $counters"
   # shellcheck disable=SC2086
-  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "k_step|k_world" -d "$OUT/p$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/p$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "^(k_step|k_world)$" -d "$OUT/p$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -n 2 "$OUT/p$i.log"
   case $rc in 0|1|2) ;; *) echo "stopping"; exit $rc;; esac

@@ -1,53 +1,86 @@
-"""Turn a FETCH_SIZE / WRITE_SIZE rocprofv3 PMC pair (tools/pmc_session.sh) into
-profiles/pmc_traffic.json, the HBM bytes per k_step launch that bench.py reports as
-roofline.traffic.
+"""Turn the rocprofv3 PMC passes of tools/pmc_session.sh into profiles/pmc_traffic.json, the
+per-launch HBM bytes (and VALU instructions) of the step kernel that bench.py reports as
+roofline.traffic -- only for the kernel source it was measured on.
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports 1/2 of the bytes of
 wide coalesced reads -> doubled; WRITE_SIZE is taken as reported.  Both counters are KiB.
-usage: python tools/pmc_traffic.py <pmc dir with p1 (FETCH_SIZE) and p2 (WRITE_SIZE)> <workload> [kernel]
-       <alg bytes per launch>
+
+The bench JSON line that each pass's log holds gives the workload and the generated kernel's
+source sha256 (roofline.kernel_source_sha256); every pass must agree.  The counter CSVs are
+copied under profiles/<dest>/ so that the record's evidence is tracked.
+
+usage: python tools/pmc_traffic.py <pmc dir: p1/, p1.log, p2/, ...> <profiles dest dir> [kernel]
 """
 import csv
 import glob
 import json
+import shutil
 import sys
 from pathlib import Path
 
+ROOT = Path(__file__).resolve().parent.parent
 
-def per_launch(d, counter):
+
+def per_launch(d, counter, kernel):
     vals = {}
     for f in glob.glob(f"{d}/**/pmc_counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if ("k_step" in row["Kernel_Name"] or "k_world" in row["Kernel_Name"]) and row["Counter_Name"] == counter:
+            name = row["Kernel_Name"].split("(")[0].strip()
+            if name == kernel and row["Counter_Name"] == counter:
                 vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
     if not vals:
-        raise SystemExit(f"no {counter} rows for k_step under {d}")
+        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
     return sum(vals.values()) / len(vals), len(vals)
 
 
+def bench_line(log):
+    for line in reversed(Path(log).read_text().splitlines()):
+        if line.startswith("{") and '"roofline"' in line:
+            return json.loads(line)
+    raise SystemExit(f"no bench JSON line in {log}")
+
+
 def main():
-    d, workload, alg = sys.argv[1], sys.argv[2], float(sys.argv[3])
-    fetch_kib, n1 = per_launch(d, "FETCH_SIZE")
-    write_kib, n2 = per_launch(d, "WRITE_SIZE")
-    try:  # wave-level VALU instructions per launch (VALU-issue roofline in bench.py)
-        valu, _ = per_launch(d, "SQ_INSTS_VALU")
-    except SystemExit:
-        valu = None
+    d, dest = Path(sys.argv[1]), ROOT / sys.argv[2]
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "k_world"
+    lines = [bench_line(f) for f in sorted(glob.glob(f"{d}/p*.log"))]
+    hashes = {b["roofline"]["kernel_source_sha256"] for b in lines}
+    workloads = {b["config"]["workload"] for b in lines}
+    if len(hashes) != 1 or len(workloads) != 1:
+        raise SystemExit(f"passes disagree: {hashes} {workloads}")
+    b = lines[0]
+    alg = b["roofline"]["alg_bytes_per_env_step"] * b["config"]["num_envs_per_gpu"]
+    fetch_kib, n1 = per_launch(d, "FETCH_SIZE", kernel)
+    write_kib, n2 = per_launch(d, "WRITE_SIZE", kernel)
+    extra = {}
+    for c in ("SQ_INSTS_VALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+        try:
+            extra[c.lower() + "_per_launch"] = per_launch(d, c, kernel)[0]
+        except SystemExit:
+            pass
     hbm = 2 * fetch_kib * 1024 + write_kib * 1024
+    dest.mkdir(parents=True, exist_ok=True)
+    for f in glob.glob(f"{d}/**/pmc_counter_collection.csv", recursive=True):
+        rel = Path(f).relative_to(d)
+        shutil.copy(f, dest / ("_".join(rel.parts)))
+    for f in glob.glob(f"{d}/p*.log"):
+        shutil.copy(f, dest / Path(f).name)
     out = {
-        "workload": workload,
-        "kernel": sys.argv[4] if len(sys.argv) > 4 else "k_world",
+        "workload": b["config"]["workload"],
+        "kernel": kernel,
+        "kernel_source_sha256": hashes.pop(),
         "launches_sampled": [n1, n2],
         "fetch_size_kib_per_launch": round(fetch_kib, 1),
         "write_size_kib_per_launch": round(write_kib, 1),
         "hbm_bytes_per_launch": round(hbm),
         "alg_bytes_per_launch": round(alg),
         "traffic_over_alg": round(hbm / alg, 3),
-        "valu_insts_per_launch": valu,
+        "valu_insts_per_launch": extra.get("sq_insts_valu_per_launch"),
+        **{k: v for k, v in extra.items() if k != "sq_insts_valu_per_launch"},
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads), WRITE_SIZE x1; KiB -> B",
-        "source": d,
+        "source": str(dest.relative_to(ROOT)),
     }
-    p = Path(__file__).resolve().parent.parent / "profiles" / "pmc_traffic.json"
+    p = ROOT / "profiles" / "pmc_traffic.json"
     p.write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out, indent=1))
 

@@ -54,6 +54,8 @@ EXPORTED_SYMBOLS = (
     "vmas_stream_abort_capture",
     "vmas_graph_launch",
     "vmas_host_waits",
+    "vmas_test_hold",
+    "vmas_balance_outputs",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -205,6 +207,29 @@ class VmasShapeRef(ctypes.Structure):
     ]
 
 
+class VmasVec(ctypes.Structure):
+    _fields_ = [("p", _vp), ("s0", _i32), ("s1", _i32)]
+
+
+VMAS_SCN_MAX_AGENTS = 32
+VMAS_SCN_REWARD, VMAS_SCN_OBS, VMAS_SCN_DONE = 1, 2, 4
+
+
+class VmasBalanceIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", _i32), ("n_agents", _i32), ("what", _i32), ("pad0", _i32),
+        ("shaping_factor", _f32), ("fall_reward", _f32), ("pi", _f32), ("pad1", _f32),
+        ("package", VmasShapeRef), ("goal", VmasShapeRef), ("line", VmasShapeRef), ("floor", VmasShapeRef),
+        ("package_vel", VmasVec), ("line_vel", VmasVec), ("line_ang_vel", VmasVec),
+        ("agent_pos", VmasVec * VMAS_SCN_MAX_AGENTS), ("agent_vel", VmasVec * VMAS_SCN_MAX_AGENTS),
+        ("global_shaping", _vp), ("gs_s0", _i32), ("pad2", _i32),
+        ("global_shaping_out", _vp), ("package_dist", _vp), ("pos_rew", _vp), ("ground_rew", _vp),
+        ("on_the_ground", _vp),
+        ("rewards", _vp * VMAS_SCN_MAX_AGENTS), ("obs", _vp * VMAS_SCN_MAX_AGENTS),
+        ("done", _vp),
+    ]
+
+
 # Per-call pointer tables are built as numpy structured arrays (one row per entity/agent/joint);
 # their layouts must match VmasEntityIO / VmasAgentIO / VmasJointIO / VmasRayTarget.
 ENTITY_IO_DTYPE = np.dtype(
@@ -311,6 +336,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_last_error.restype = ctypes.c_char_p
     lib.vmas_host_waits.restype = _i32
     lib.vmas_host_waits.argtypes = []
+    lib.vmas_test_hold.restype = _i32
+    lib.vmas_test_hold.argtypes = [_i32, _i32, ctypes.c_int64, _vp]
+    lib.vmas_balance_outputs.restype = _i32
+    lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_graph_launch.restype = _i32

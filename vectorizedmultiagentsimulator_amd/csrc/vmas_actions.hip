@@ -381,4 +381,26 @@ int32_t vmas_assert_wait(VmasDeviceAssert* ch, int32_t slot, uint32_t seq, int32
     return VMAS_OK;
 }
 
+// Test utility: occupy CUs for `ticks` s_memrealtime ticks.  Every wave polls the wall clock and
+// leaves once the span has passed (or after a poll bound), so the grid always drains.
+__global__ void __launch_bounds__(256) k_hold(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t i = 0; i < (1u << 28); ++i) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+int32_t vmas_test_hold(int32_t device, int32_t blocks, int64_t microseconds, void* stream) {
+    if (device < 0 || blocks <= 0 || microseconds <= 0 || microseconds > 5000000)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_test_hold: bad arguments");
+    VMAS_AUX_HIP(hipSetDevice(device));
+    int khz = 0;
+    VMAS_AUX_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+    const unsigned long long ticks = (unsigned long long)microseconds * (unsigned long long)(khz > 0 ? khz : 100000) / 1000ull;
+    hipLaunchKernelGGL(k_hold, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ticks);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
 }  // extern "C"

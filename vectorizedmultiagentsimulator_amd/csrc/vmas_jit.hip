@@ -30,11 +30,12 @@
 // vmas_jit_world_create and the caller uses vmas_world_step.
 //
 // Batch-global broadphase (core.py:2796): the fixed-point scheme of vmas_world_step (R/Z flags
-// per block, a reduction that checks the mask, a re-run on violation), run on the device: the
-// grid is persistent (at most the resident workgroup count, each striding over 64-env groups)
-// and workgroup 0 reduces the flags between passes while the others wait on a published state
-// word (vmas_jit_ops.hpp grid_fixed_point), so the host only launches.  VMAS_JIT_GRID=host keeps
-// the host-driven loop (one launch + reduction + host read per pass).
+// per block, a reduction that checks the mask, a re-run on violation), run on the device as a
+// relay of launches: pass 0 (k_world), then rerun launches (k_world_rerun) that exit at once
+// unless the previous pass asked for them.  The last workgroup to arrive in a pass reduces the
+// flags and publishes the decision; no workgroup waits for another (vmas_jit_ops.hpp
+// relay_arrive), so the host only launches.  VMAS_JIT_GRID=host keeps the host-driven loop (one
+// launch + reduction + host read per pass).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <hip/hip_ext.h>
@@ -332,7 +333,9 @@ struct Gen {
     }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        return 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        // (+5 ints: B, S, sdt, max_pass, pass; the struct is padded to its 8-byte alignment)
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 5);
+        return (n + 7) & ~(size_t)7;
     }
 
     // expressions for entity e as seen by wave w (registers when w owns it)
@@ -660,7 +663,7 @@ struct Gen {
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
-             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
+             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n    int pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
              "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
@@ -679,6 +682,19 @@ struct Gen {
         for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
         const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
+        // NaN over every output field of the step (one workgroup; only after a fixed point that
+        // did not converge within the relay): the bad step is visible in its own results
+        {
+            const int n_lin = cfg.n_out_lin, n_rot = cfg.n_out_rot, n_f = cfg.n_out_force, n_t = cfg.n_out_torque;
+            const int per_env[6] = {2 * n_lin, 2 * n_lin, n_rot, n_rot, 2 * n_f, n_t};
+            o += "__device__ __forceinline__ void poison_outputs(const Args& a) {\n"
+                 "    const float nan = __builtin_nanf(\"\");\n";
+            for (int k = 0; k < 6; ++k)
+                if (per_env[k] > 0)
+                    o += "    for (size_t i = threadIdx.x; i < (size_t)" + it(per_env[k]) +
+                         " * a.B; i += blockDim.x) a.out[" + it(k) + "][i] = nan;\n";
+            o += "}\n\n";
+        }
         o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
         o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
@@ -694,37 +710,39 @@ struct Gen {
         o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n";
         o += "    const int nfl = 2 * a.S * " + it(W) + ", ngrp = (a.B + 63) >> 6;\n"
              "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
-        // Persistent launch (a.ctl set, every workgroup resident): workgroups stride over the
-        // 64-env groups and run the passes of the broadphase fixed point without the host.
-        // Otherwise one group per workgroup and one pass per launch.  DONE is back to zero at
-        // the end of every substep's pair phase, so it carries over between groups.
+        // Relay launch (a.ctl set): workgroups stride over the 64-env groups and run pass a.pass
+        // of the broadphase fixed point; a rerun launch (a.pass > 0) exits at once unless the
+        // previous pass asked for it (vmas_jit_ops.hpp relay_arrive).  Otherwise (a.ctl null) one
+        // group per workgroup and one pass per launch (host-driven loop).  DONE is back to zero
+        // at the end of every substep's pair phase, so it carries over between groups.
         o += "    const uint32_t epoch = a.ctl ? ld_agent(&a.ctl[3]) : 0u;\n";
-        o += "    const TimerStart t0s = device_timer_start(a.ctl ? a.tm : nullptr);\n";
-        o += "    for (int pass = 0;; ++pass) {\n"
-             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
-             "        for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
-             "            MSK[i] = ~__hip_atomic_load(&a.mask[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-             "        for (int g = blockIdx.x; g < ngrp; g += gridDim.x) {\n"
-             "            const int b = g * 64 + lane;\n"
-             "            const bool valid = b < a.B;\n"
-             "            const int bb = valid ? b : (a.B - 1);\n"
-             "            switch (wave) {\n";
+        o += "    if (a.ctl && a.pass > 0 && !relay_requested(a.ctl, epoch, a.pass)) return;\n";
+        o += "    const TimerStart t0s = device_timer_start(a.ctl ? a.tm : nullptr, a.pass == 0);\n";
+        o += "    const int pass = a.pass;\n"
+             "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+             "    for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
+             "        MSK[i] = ~__hip_atomic_load(&a.mask[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+             "    for (int g = blockIdx.x; g < ngrp; g += gridDim.x) {\n"
+             "        const int b = g * 64 + lane;\n"
+             "        const bool valid = b < a.B;\n"
+             "        const int bb = valid ? b : (a.B - 1);\n"
+             "        switch (wave) {\n";
         for (int w = 0; w < nw; ++w)
-            o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
-        o += "                default: break;\n            }\n        }\n";
-        o += "        if (!a.blk) return;\n"
-             "        __syncthreads();\n"
-             "        uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
-             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x)\n"
-             "            __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-             "        if (!a.ctl) return;\n"
-             "        if (!grid_fixed_point(a.blk, a.mask, a.ctl, a.err, a.herr, a.S * " + it(W) +
-             ", pass, a.max_pass, RED, epoch, a.tm, t0s)) return;\n"
-             "    }\n}\n\n";
-        o += "extern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) +
-             ") k_world(Args a) {\n"
-             "    world_body(a);\n"
-             "}\n";
+            o += "            case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
+        o += "            default: break;\n        }\n    }\n";
+        o += "    if (!a.blk) return;\n"
+             "    __syncthreads();\n"
+             "    uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
+             "    for (int i = threadIdx.x; i < nfl; i += blockDim.x)\n"
+             "        __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+             "    if (!a.ctl) return;\n"
+             "    if (relay_arrive(a.blk, a.mask, a.ctl, a.err, a.herr, a.S * " + it(W) +
+             ", pass, a.max_pass, RED, epoch, a.tm, t0s))\n"
+             "        poison_outputs(a);\n"
+             "}\n\n";
+        const std::string bounds = "__launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) + ")";
+        o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
+        o += "extern \"C\" __global__ void " + bounds + " k_world_rerun(Args a) {\n    world_body(a);\n}\n";
     }
 };
 
@@ -858,16 +876,16 @@ struct VmasJitWorld {
     size_t arg_bytes = 0;
     int W = 1, nblk = 0, nw = kNW;
     hipModule_t mod = nullptr;
-    hipFunction_t fn = nullptr;
+    hipFunction_t fn = nullptr, fn_rerun = nullptr;  // k_world (pass 0), k_world_rerun (passes >= 1)
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
-    // persistent launch: d_ctl = [kGridCtlWords control words | inverted mask words], zeroed by
+    // relay launches: d_ctl = [kGridCtlWords control words | inverted mask words], zeroed at create;
     // d_err: sticky error bits; h_err: mapped host word the kernel stores them into (dh_err: its
     // device address)
     uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr, *dh_err = nullptr;
-    int grid = 0;          // persistent workgroups (0: one pass per launch, host-driven loop)
-    bool coop = false;     // cooperative launch (VMAS_JIT_GRID=coop)
+    int grid = 0;          // workgroups of a relay launch (0: host-driven loop, one pass per launch)
+    int relay = 0;         // launches per step (0: substeps + 2, the fixed point's bound; VMAS_JIT_RELAY)
     hipStream_t last_stream = nullptr;
-    int last_passes = 0;   // passes of the last host-driven step (persistent: read on demand)
+    int last_passes = 0;   // passes of the last host-driven step (relay: read on demand)
     bool last_persistent = false;
     unsigned long long* d_prof = nullptr;  // phase timestamps of one workgroup (VMAS_JIT_PROFILE)
     size_t n_prof = 0;
@@ -875,7 +893,7 @@ struct VmasJitWorld {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
     double timed_ms = 0.0;
     long timed_launches = 0;
-    // device timer (timing on, persistent launches): [0] workgroup 0's start, [2] accumulated
+    // device timer (timing on, relay launches): [0] pass 0 workgroup 0's start, [2] accumulated
     // ticks, [4] launches -- s_memrealtime, kept by the kernel itself so that launches replayed
     // from a HIP graph are timed too (HIP records no events inside a graph; vmas_jit_ops.hpp)
     unsigned long long* d_tm = nullptr;
@@ -950,7 +968,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
         if (hipModuleLoadData(&W->mod, code.data()) != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
-        if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
+        if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess ||
+            hipModuleGetFunction(&W->fn_rerun, W->mod, "k_world_rerun") != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
         int scratch = 0;
         (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
@@ -981,15 +1000,14 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipDeviceGetAttribute(&W->wall_khz, hipDeviceAttributeWallClockRate, cfg->device) != hipSuccess ||
         W->wall_khz <= 0)
         return cleanup(jfail(VMAS_E_HIP, "device timer (hipMalloc / wall clock rate)"));
-    // Persistent grid: as many workgroups as can be resident at once (occupancy x CUs), capped
-    // by the number of 64-env groups, launched as a plain launch: the workgroups of one launch on
-    // an in-order stream all become resident (any other kernel holding CUs finishes without
-    // waiting on this one), and every wait is bounded anyway.  VMAS_JIT_GRID=coop uses the
-    // cooperative API instead (residency guaranteed by the runtime; measured +18 us per launch),
-    // =host the host-driven loop (one launch + reduction + host read per pass).
+    // Relay grid (vmas_jit_ops.hpp relay_arrive): as many workgroups as can be resident at once
+    // (occupancy x CUs), capped by the number of 64-env groups; each strides over the groups.
+    // Nothing waits across workgroups, so residency is a performance choice, not a requirement.
+    // VMAS_JIT_GRID=host keeps the host-driven loop (one launch + reduction + host read per pass);
+    // VMAS_JIT_RELAY=<n> caps the launches per step (default substeps + 2: the fixed point's bound).
     {
         const char* gm = getenv("VMAS_JIT_GRID");
-        const std::string mode = gm ? gm : "plain";
+        const std::string mode = gm ? gm : "relay";
         int per_cu = 0, cus = 0;
         if (mode != "host" &&
             hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, W->fn, W->nw * 64, 0) == hipSuccess &&
@@ -997,7 +1015,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             per_cu > 0 && cus > 0) {
             W->grid = std::min(W->nblk, per_cu * cus);
             if (const char* cap = getenv("VMAS_JIT_GRID_CAP")) W->grid = std::max(1, std::min(W->grid, atoi(cap)));
-            W->coop = mode == "coop";
+            if (const char* r = getenv("VMAS_JIT_RELAY")) W->relay = std::max(1, atoi(r));
         }
     }
     if (g.prof_block >= 0) {
@@ -1135,12 +1153,17 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     memcpy(p, &io->sub_dt, 4);
     p += 4;
     const int max_it = batch_bp ? io->substeps + 2 : 1;
-    put_i32(max_it);
-    size_t size = (size_t)(p - buf.data());
+    const int relay_len = W->relay > 0 ? std::min(W->relay, max_it) : max_it;
+    int32_t* arg_pass = nullptr;
+    put_i32(persistent ? relay_len : max_it);
+    arg_pass = reinterpret_cast<int32_t*>(p);
+    put_i32(0);
+    size_t size = ((size_t)(p - buf.data()) + 7) & ~(size_t)7;
+    if (size > buf.size()) return jfail(VMAS_E_INVALID, "kernel argument block overflow");
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
 
-    // a fixed-point failure of an earlier persistent step (sticky error bits, which the kernel
+    // a fixed-point failure of an earlier relay step (sticky error bits, which the kernel
     // stores into mapped host memory) surfaces here
     if (uint32_t e = *(volatile uint32_t*)W->h_err)
         return jfail(e & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
@@ -1148,7 +1171,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     W->last_stream = stream;
     W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
-    // (the persistent kernel resets its own control words: see grid_fixed_point)
+    // (the relay resets its own control words: see relay_arrive)
     if (!persistent) JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
     // Timing (vmas_jit_world_set_timing): the events ride on the kernel's own dispatch packet
     // (hipExtModuleLaunchKernel), so they bracket its execution alone, as rocprofv3's kernel
@@ -1166,42 +1189,32 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     JHIP(hipStreamIsCapturing(stream, &cap));
     const bool capturing = cap == hipStreamCaptureStatusActive;
-    auto launch_plain = [&](int blocks) -> int32_t {
+    // (timed: only k_world, pass 0; a rerun is counted by the device timer of the relay)
+    auto launch_plain = [&](int blocks, hipFunction_t fn, bool timed) -> int32_t {
         const uint32_t threads = (uint32_t)W->nw * 64;
-        if (!W->timing || capturing) {  // (a captured launch is timed by the device timer)
-            JHIP(hipModuleLaunchKernel(W->fn, blocks, 1, 1, threads, 1, 1, 0, stream, nullptr, extra));
+        if (!W->timing || capturing || !timed) {  // (a captured launch is timed by the device timer)
+            JHIP(hipModuleLaunchKernel(fn, blocks, 1, 1, threads, 1, 1, 0, stream, nullptr, extra));
             return VMAS_OK;
         }
         std::pair<hipEvent_t, hipEvent_t> ev{};
         if (int32_t rc = ev_pair(&ev)) return rc;
-        JHIP(hipExtModuleLaunchKernel(W->fn, (uint32_t)blocks * threads, 1, 1, threads, 1, 1, 0, stream, nullptr,
+        JHIP(hipExtModuleLaunchKernel(fn, (uint32_t)blocks * threads, 1, 1, threads, 1, 1, 0, stream, nullptr,
                                       extra, ev.first, ev.second, 0));
         W->ev_pending.push_back(ev);
         return VMAS_OK;
     };
     if (persistent) {
-        // one launch runs every pass; nothing waits on the host
-        if (W->coop && capturing) return jfail(VMAS_E_INVALID, "cooperative launches are not captured into graphs");
-        if (W->coop) {
-            void* params[] = {buf.data()};
-            std::pair<hipEvent_t, hipEvent_t> ev{};
-            if (W->timing) {
-                if (int32_t rc = ev_pair(&ev)) return rc;
-                JHIP(hipEventRecord(ev.first, stream));
-            }
-            JHIP(hipModuleLaunchCooperativeKernel(W->fn, W->grid, 1, 1, W->nw * 64, 1, 1, 0, stream, params));
-            if (W->timing) {
-                JHIP(hipEventRecord(ev.second, stream));
-                W->ev_pending.push_back(ev);
-            }
-        } else if (int32_t rc = launch_plain(W->grid)) {
-            return rc;
+        // the relay: pass 0, then relay_len - 1 rerun launches that exit at once unless the
+        // previous pass asked for them; nothing waits on the host or across workgroups
+        for (int pass = 0; pass < relay_len; ++pass) {
+            *arg_pass = pass;  // (the launch copies the argument block)
+            if (int32_t rc = launch_plain(W->grid, pass ? W->fn_rerun : W->fn, pass == 0)) return rc;
         }
         if (iterations) *iterations = 0;  // not known without a sync: vmas_jit_world_passes
         return VMAS_OK;
     }
     for (int it = 0; it < max_it; ++it) {
-        if (int32_t rc = launch_plain(W->nblk)) return rc;
+        if (int32_t rc = launch_plain(W->nblk, W->fn, true)) return rc;
         W->last_passes = it + 1;
         if (iterations) *iterations = it + 1;
         if (!batch_bp) return VMAS_OK;
@@ -1245,10 +1258,10 @@ int32_t vmas_jit_world_check(VmasJitWorld* W) {
     return VMAS_OK;
 }
 
-// 0: host-driven passes; otherwise the persistent grid size (negative: plain, non-cooperative launch)
+// 0: host-driven passes; otherwise the relay's grid size (returned negative: plain launches)
 int32_t vmas_jit_world_grid(const VmasJitWorld* W) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
-    return W->coop ? W->grid : -W->grid;
+    return -W->grid;
 }
 
 int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
@@ -1257,7 +1270,7 @@ int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
     return VMAS_OK;
 }
 
-// Device timer totals (timing on, persistent launches): every launch -- eager or replayed from a
+// Device timer totals (timing on, relay launches): every launch -- eager or replayed from a
 // HIP graph -- adds (final reduction - workgroup 0 start) in s_memrealtime ticks; *clock_ghz is
 // the in-kernel shader clock of the reducing workgroups.  Waits for the device.
 int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches,

@@ -78,34 +78,41 @@ __device__ __forceinline__ void integrate(const VmasEntityDesc& d, int substep, 
 #define __HIP_MEMORY_SCOPE_AGENT 4
 #endif
 
-// Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily)
+// Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily).
+// (kGridErrStateTimeout belonged to the former spin-waiting persistent launch; no code sets it.)
 constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
-// spin bound of a waiting workgroup (~2^22 polls of >= 64 clocks: seconds, far above any pass)
-constexpr uint32_t kGridSpinLimit = 1u << 22;
 
-// Device-side fixed point of the batch-global broadphase for a persistent launch (every
-// workgroup resident).  Each workgroup has stored the OR of its R/Z activity words in
-// blk[blockIdx.x] ([2][nwords]) and arrives on a two-level counter; the LAST workgroup to
-// arrive ORs every row, applies the k_jit_flags_reduce test (was the mask a fixed point?),
-// publishes the next mask (stored inverted, so a zero memset means "all pairs active") and a
-// continue bit; the others wait for that bit.
-// ctl: [0] top arrival counter, [1] published (epoch << 8 | (pass+1) << 1 | continue), [2] passes
-// run, [3] launch epoch, [32 * (1 + k)] arrival counter of the workgroups with blockIdx % 8 == k
-// (one 128-byte line each: 512 arrivals on one address serialise at the memory side).  No host
-// memset: the final pass's reducer, which runs after every workgroup has arrived, clears the
-// counters and the mask words for the next launch, and the epoch (read by every workgroup at its
-// start, advanced by that reducer) keeps the previous launch's published word from being read as
-// this launch's.  It also removes the memset node in front of the kernel: with one there, replays
-// of a captured HIP graph timed out in these waits on ROCm 7.2 (cause not isolated).
-// RED: workgroup LDS of 2 * nwords + 2 words.  Returns whether another pass is needed.  Every
-// wait is bounded: a timeout stops the passes and sets an error bit instead of hanging.
+// Device-side fixed point of the batch-global broadphase as a RELAY of launches, with no
+// workgroup ever waiting for another (so nothing assumes that the workgroups of a launch are
+// co-resident).  The step enqueues L launches on one stream: pass 0 (k_world) and passes
+// 1..L-1 (k_world_rerun).  Every launch is an ordinary grid over the 64-env groups:
+//   * each workgroup stores the OR of its R/Z activity words in blk[blockIdx.x] ([2][nwords])
+//     and arrives on a two-level counter;
+//   * the LAST workgroup to arrive ORs every row, applies the k_jit_flags_reduce test (was the
+//     mask a fixed point?) and publishes the decision in ctl[1] = (epoch << 8 | (pass+1) << 1 |
+//     continue), with the next mask (stored inverted, so zero means "all pairs active");
+//   * a rerun launch reads ctl[1] first and exits at once unless the previous pass asked for it.
+// Stream order between the launches is the only synchronisation: a launch starts after the
+// previous one has completed, with its memory visible (kernel-boundary release / acquire).
+// ctl: [0] top arrival counter, [1] published word, [2] passes run, [3] launch epoch, [32 * (1 +
+// k)] arrival counter of the workgroups with blockIdx % 8 == k (one 128-byte line each: 512
+// arrivals on one address serialise at the memory side).  No host memset: the final pass's
+// reducer, which runs after every workgroup of the step has arrived, clears the counters and the
+// mask words for the next step and advances the epoch, which keeps the previous step's
+// published word from being read as this step's.
 //
-// Everything exchanged between workgroups (blk rows, mask words, ctl) is accessed only with
-// agent-scope atomics, which are coherent across the XCDs' L2s by themselves; a writer waits
-// for its stores (s_waitcnt) before the workgroup barrier that precedes the arrival/publish
-// atomic.  Agent-scope fences are avoided: a release writes back the whole XCD L2 and an
-// acquire invalidates it (measured: per-wave fences cost 120 us per launch, one fence per
-// workgroup still 40-60 us, on a 10-70 us kernel).
+// Why no spin-wait any more (the former single persistent launch): its waiting workgroups needed
+// every workgroup of the grid resident at once, which a plain launch does not guarantee (a kernel
+// of another stream or process holding CUs delays some workgroups; the resident ones then spun
+// until their bound and the step completed with a non-fixed-point mask).  The relay has no such
+// assumption.  The graph-replay timeouts seen with a memset node in front of the persistent
+// kernel are consistent with the same cause: the waits could only time out if an arrival never
+// came, i.e. a workgroup of the grid was not running (or its counter increment was zeroed by a
+// memset that had not completed when the first workgroups arrived).  Neither can stall a relay.
+//
+// RED: workgroup LDS of 2 * nwords + 2 words.  Returns true in the reducer of a final pass that
+// did NOT converge (the caller then poisons the step's outputs with NaN, so that the bad step is
+// visible in its own results; the sticky error bit also fails the next step).
 constexpr int kGridCtlWords = 32 * 9;
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
@@ -128,14 +135,20 @@ __device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
 struct TimerStart {
     unsigned long long rt, sc;
 };
-__device__ __forceinline__ TimerStart device_timer_start(unsigned long long* tm) {
+__device__ __forceinline__ TimerStart device_timer_start(unsigned long long* tm, bool stamp_start) {
     TimerStart t{0ull, 0ull};
     if (tm && threadIdx.x == 0) {
         t.rt = __builtin_amdgcn_s_memrealtime();
         t.sc = __builtin_amdgcn_s_memtime();
-        if (blockIdx.x == 0) __hip_atomic_store(&tm[0], t.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (stamp_start && blockIdx.x == 0)
+            __hip_atomic_store(&tm[0], t.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return t;
+}
+
+// Whether a rerun launch of pass `pass` (>= 1) was requested by the previous pass of this step.
+__device__ __forceinline__ bool relay_requested(const uint32_t* ctl, uint32_t epoch, int pass) {
+    return ld_agent(&ctl[1]) == (((epoch & 0xFFFFFFu) << 8) | ((uint32_t)pass << 1) | 1u);
 }
 
 // Sticky error bits: OR-ed into the device word, and the OR so far stored into the mapped host
@@ -146,9 +159,9 @@ __device__ __forceinline__ void report_err(uint32_t* err, uint32_t* herr, uint32
     if (herr) __hip_atomic_store(herr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
-                                        int nwords, int pass, int max_pass, uint32_t* RED, uint32_t epoch,
-                                        unsigned long long* tm, TimerStart t0s) {
+__device__ inline bool relay_arrive(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
+                                    int nwords, int pass, int max_pass, uint32_t* RED, uint32_t epoch,
+                                    unsigned long long* tm, TimerStart t0s) {
     const uint32_t tag = ((epoch & 0xFFFFFFu) << 8) | ((uint32_t)(pass + 1) << 1);
     const uint32_t G = gridDim.x, k = blockIdx.x & 7u;
     const uint32_t n_k = (G + 7u - k) / 8u, n_sub = G < 8u ? G : 8u;  // workgroups in sub-counter k
@@ -164,24 +177,7 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
     __syncthreads();
     const bool reducer = RED[nw2] != 0u;
     __syncthreads();
-    if (!reducer) {
-        if (threadIdx.x == 0) {
-            uint32_t st = 0u, spins = 0u;
-            while (((st = ld_agent(&ctl[1])) & ~1u) != tag) {
-                if (++spins > kGridSpinLimit) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (spins > kGridSpinLimit) {
-                report_err(err, herr, kGridErrStateTimeout);
-                st = 0u;
-            }
-            RED[0] = st & 1u;
-        }
-        __syncthreads();
-        const bool more = RED[0] != 0u;
-        __syncthreads();
-        return more;
-    }
+    if (!reducer) return false;  // nothing to wait for: the next launch reads the decision
     // the reducer: every row has arrived
     for (int w = threadIdx.x; w < nw2 + 2; w += blockDim.x) RED[w] = 0u;
     __syncthreads();
@@ -227,7 +223,7 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
         st_agent(&ctl[2], (uint32_t)(pass + 1));
         st_agent(&ctl[1], tag | (more ? 1u : 0u));
     }
-    if (!more) {  // the final pass: every workgroup has arrived; reset for the next launch
+    if (!more) {  // the final pass: every workgroup of the step has arrived; reset for the next step
         for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
         if (threadIdx.x == 0) st_agent(&ctl[0], 0u);
         if (threadIdx.x >= 1 && threadIdx.x <= 8) st_agent(&ctl[32 * threadIdx.x], 0u);
@@ -245,7 +241,7 @@ __device__ inline bool grid_fixed_point(const uint32_t* blk, uint32_t* nmask, ui
         }
     }
     __syncthreads();
-    return more;
+    return viol && !more;
 }
 
 }  // namespace vmas

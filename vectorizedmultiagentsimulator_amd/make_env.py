@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """make_env (restates vmas/make_env.py:13-100)."""
 from __future__ import annotations
 

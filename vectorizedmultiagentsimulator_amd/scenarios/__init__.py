@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Scenario loader: ``load(name)`` finds ``name`` (a file name) under this folder and imports it
 (restates vmas/scenarios/__init__.py:10-23)."""
 import importlib.util

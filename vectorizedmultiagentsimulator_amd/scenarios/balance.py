@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Balance: agents carry a line with a package on it towards a goal, under gravity.
 
 Workload of BASELINE configs C1/C2.  Restates vmas/scenarios/balance.py:15-262 (world layout,

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Pollock: many movable + rotatable spheres, lines and boxes -- every narrowphase class.
 
 Parity fixture (restates vmas/scenarios/debug/pollock.py:15-97): all six pair classes with real

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Waterfall: a chain of agents joined by collidable line joints, boxes and a floor.
 
 Parity fixture for joints (restates vmas/scenarios/debug/waterfall.py).

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Discovery: agents must cover targets (``agents_per_target`` at a time); covered targets respawn.
 
 Workload of BASELINE config C4 (LIDAR-heavy).  Restates vmas/scenarios/discovery.py:23-265.

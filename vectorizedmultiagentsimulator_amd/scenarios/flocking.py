@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Flocking: agents flock around a scripted target agent among static obstacles.
 
 Workload of BASELINE config C5.  Restates vmas/scenarios/flocking.py:18-206.  The target is an

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Transport: agents push heavy box packages onto a goal.
 
 Workload of BASELINE config C3.  Restates vmas/scenarios/transport.py:15-190 (layout, reset,

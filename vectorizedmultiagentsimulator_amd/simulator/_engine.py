@@ -112,7 +112,7 @@ class PhysicsEngine:
 
     @property
     def jit_grid(self) -> int:
-        """Persistent grid of the specialised kernel (>0 cooperative, <0 plain launch, 0 host loop)."""
+        """Relay grid of the specialised kernel (negative: plain launches; 0: host-driven loop)."""
         return self.lib.vmas_jit_world_grid(self._jit) if self._jit is not None else 0
 
     def __del__(self):

@@ -1,0 +1,81 @@
+"""Host side of the fused scenario programs (csrc/vmas_scenarios.hip).
+
+A benchmark scenario restated in ``scenarios/`` computes its per-step rewards / observations /
+dones with one native launch on GPU worlds instead of the reference's eager tensor program
+(~37 kernels per balance step).  The scenario keeps the reference's attributes and return
+values; this module holds what every fused scenario needs:
+
+* ``enabled(world)``: GPU world and ``VMAS_FUSED_SCENARIOS`` not "0" (the torch program
+  otherwise -- CPU worlds always run it);
+* ``vec`` / ``ref``: tensors and entities as the ABI's ``VmasVec`` / ``VmasShapeRef``;
+* ``state_key``: identity + version counters of the tensors a cached result was computed from.
+  A program computes the outputs of every agent in one launch at the first agent's call; the
+  other agents' calls return the cached tensors only while every input is the same tensor
+  object with the same version counter (the reference recomputes per call, so any change
+  between the calls -- a user's in-place edit, a re-bound state -- recomputes here too).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from .. import _native as N
+
+_ON = os.environ.get("VMAS_FUSED_SCENARIOS", "1") != "0"
+
+
+def enabled(world) -> bool:
+    return _ON and torch.device(world.device).type == "cuda"
+
+
+def device_index(world) -> int:
+    dev = torch.device(world.device)
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def stream(world):
+    return ctypes.c_void_p(torch.cuda.current_stream(device_index(world)).cuda_stream)
+
+
+def f32(t: torch.Tensor, dev) -> torch.Tensor:
+    if t.dtype is not torch.float32 or t.device != dev:
+        t = t.to(device=dev, dtype=torch.float32)
+    return t
+
+
+def vec(t: torch.Tensor, keep: list) -> "N.VmasVec":
+    """A [B, 2] / [B, 1] / [B] fp32 device tensor as a VmasVec (kept alive in ``keep``)."""
+    keep.append(t)
+    v = N.VmasVec()
+    v.p = t.data_ptr()
+    v.s0 = t.stride(0)
+    v.s1 = t.stride(1) if t.dim() > 1 else 0
+    return v
+
+
+def ref(world, entity, keep: list, slot: int = 0) -> "N.VmasShapeRef":
+    """Shape + pos/rot of an entity (the distance queries' VmasShapeRef)."""
+    dev = torch.device(world.device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return world.engine._ref(entity, dev, keep, slot)
+
+
+def state_key(tensors) -> tuple:
+    return tuple((id(t), t.data_ptr(), t._version) for t in tensors)
+
+
+def bump_version(t: torch.Tensor) -> None:
+    """A kernel wrote ``t`` in place through a raw pointer: advance its version counter as the
+    reference's in-place torch op would (graph mode finds in-place writes by version)."""
+    torch.autograd.graph.increment_version(t)
+
+
+def check(rc: int, what: str) -> None:
+    N.check_aux(rc, what)
+
+
+def lib():
+    return N.load_library()

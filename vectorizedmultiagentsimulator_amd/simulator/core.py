@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Entity / World surface of the simulator (restates vmas/simulator/core.py's public API).
 
 The classes keep the reference's names, constructor arguments, properties and side effects so

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Forward-only dynamics (dynamics/forward.py:9-20): a thrust along the agent's heading."""
 import torch
 

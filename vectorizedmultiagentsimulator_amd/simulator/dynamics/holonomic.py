@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Holonomic dynamics (dynamics/holonomic.py:13-14): the force is the first two action entries."""
 from .common import Dynamics
 

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Holonomic dynamics with a torque input (dynamics/holonomic_with_rot.py:8-15): the action is
 (fx, fy, torque); force and torque go to the physics step as the agent's action inputs."""
 from .common import Dynamics

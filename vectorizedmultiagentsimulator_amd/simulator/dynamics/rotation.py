@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Rotation-only dynamics (dynamics/roatation.py:8-15): the action is a torque."""
 from .common import Dynamics
 

@@ -37,18 +37,24 @@ What a replay must honour, and how:
     of pageable memory, discrete or communication actions -- makes the capture fail; the
     simulator's objects are rolled back (nothing ran: capture only records) and the env stays
     eager.  ``env.graph_status`` says which.
-  * Not detectable, so a documented requirement of graph mode: per-step Python state that feeds
-    kernel arguments (a Python-int step counter multiplied into a tensor, numpy random numbers
-    drawn inside the step) is frozen at its capture-time value.  The benchmark scenarios keep
-    all per-step state in device tensors; tests/test_graph.py checks replay == eager bit for bit.
+  * Per-step host state.  A replay runs no Python, so host state the step changes would be
+    frozen at its capture-time value.  The last eager step before the capture is watched: if it
+    draws from a host RNG (torch CPU, numpy or Python ``random``, outside the host holes, which
+    run eagerly in a replay too) or changes a plain Python number / string attribute of the
+    tracked objects (a Python-int step counter), the env stays eager (``graph_reason`` says
+    why).  Host state kept elsewhere (module globals, objects the tracker does not visit) stays
+    a documented requirement: the benchmark scenarios keep all per-step state in device
+    tensors; tests/test_graph.py checks replay == eager bit for bit.
 """
 from __future__ import annotations
 
 import ctypes
 import gc
 import os
+import random
 from typing import Any, Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 from torch import Tensor
 
@@ -72,6 +78,33 @@ def _tracked_objects(env) -> List[Any]:
         if id(o) not in seen and hasattr(o, "__dict__"):
             seen.add(id(o))
             out.append(o)
+    return out
+
+
+def _host_rng_states():
+    return torch.random.get_rng_state(), np.random.get_state(), random.getstate()
+
+
+def _host_rng_changed(a, b) -> Optional[str]:
+    if not torch.equal(a[0], b[0]):
+        return "torch CPU generator"
+    if a[1][0] != b[1][0] or not np.array_equal(a[1][1], b[1][1]) or tuple(a[1][2:]) != tuple(b[1][2:]):
+        return "numpy global generator"
+    if a[2] != b[2]:
+        return "python random"
+    return None
+
+
+_PLAIN = (bool, int, float, str)
+
+
+def _plain_attrs(objs) -> Dict[Tuple[int, str], Any]:
+    """Plain Python number / string attributes of the tracked objects (Python-side step state)."""
+    out = {}
+    for o in objs:
+        for k, v in o.__dict__.items():
+            if type(v) in _PLAIN:
+                out[(id(o), k)] = v
     return out
 
 
@@ -401,7 +434,20 @@ class StepGraph:
                     hole_waits[0] += (lib.vmas_host_waits() - h0) & 0xFFFFFFFF
                     torch.cuda.set_sync_debug_mode(m)
 
+            rng_cur = [_host_rng_states()]
+            rng_used = [None]
+
+            def hole(fn, args, _inner=hole):  # host RNG use inside a hole is replayed eagerly too
+                if rng_used[0] is None:
+                    rng_used[0] = _host_rng_changed(rng_cur[0], _host_rng_states())
+                try:
+                    return _inner(fn, args)
+                finally:
+                    rng_cur[0] = _host_rng_states()
+
             self.env.world._hole_sink = hole
+            objs = _tracked_objects(self.env)
+            plain0 = _plain_attrs(objs)
             try:
                 with consts:
                     out = self.body()
@@ -409,6 +455,10 @@ class StepGraph:
                 self.env.world._assert_sink = None
                 self.env.world._hole_sink = None
                 torch.cuda.set_sync_debug_mode(mode)
+            if rng_used[0] is None:
+                rng_used[0] = _host_rng_changed(rng_cur[0], _host_rng_states())
+            plain1 = _plain_attrs(objs)
+            changed = sorted(k for k in set(plain0) | set(plain1) if plain0.get(k) != plain1.get(k))
         self._trial_consts = consts  # the arena outlives the copies that read it
         # torch's warning: "called a synchronizing CUDA operation" (not the notice that the mode
         # is a prototype, which set_sync_debug_mode emits itself)
@@ -418,6 +468,14 @@ class StepGraph:
         if syncs or native:
             self.status = "eager"
             self.why = ("host sync in the step: " + (syncs[0] if syncs else f"{native} native host wait(s)"))[:300]
+        elif rng_used[0] is not None:
+            self.status = "eager"
+            self.why = f"the step draws from a host RNG ({rng_used[0]}): a replay would repeat its numbers"
+        elif changed:
+            names = {id(o): type(o).__name__ for o in objs}
+            self.status = "eager"
+            self.why = ("the step changes Python-side state a replay would freeze: "
+                        + ", ".join(f"{names.get(i, '?')}.{k}" for i, k in changed[:4]))[:300]
         return out
 
     def drop(self, why: str):

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """The vectorized Environment (restates vmas/simulator/environment/environment.py:49-1070).
 
 Differences from the reference are limited to host-synchronisation placement (§8f row 1 of
@@ -60,6 +62,16 @@ def _f32(x) -> float:
 _storage_use_count = getattr(torch._C, "_storage_Use_Count", None)
 
 
+def _refs_of_fresh_argument(value) -> int:
+    return sys.getrefcount(value)
+
+
+# sys.getrefcount of a temporary passed straight into a function, measured on THIS interpreter
+# (3.10 counts the caller's stack slot and the parameter; 3.11+ moves arguments into the callee
+# frame, one reference fewer): a tensor that something else also holds counts more than this
+_FRESH_REFS = _refs_of_fresh_argument(object())
+
+
 def _owned_or_clone(value):
     """The reference clones every reward / observation / info it returns (environment.py:
     149-196) so that callers never alias tensors the scenario keeps.  A tensor that nothing else
@@ -69,7 +81,7 @@ def _owned_or_clone(value):
     kernel less.  Anything else (scenario attributes, views, dicts) is cloned as the reference
     does."""
     if (isinstance(value, Tensor) and _storage_use_count is not None
-            and sys.getrefcount(value) <= 3  # the caller's stack slot, this parameter, the argument
+            and sys.getrefcount(value) <= _FRESH_REFS  # no reference but the call's own
             and _storage_use_count(value.untyped_storage()._cdata) <= 2):
         return value
     return TorchUtils.recursive_clone(value)

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Minimal action/observation spaces.
 
 The reference builds its spaces with ``gym.spaces`` (environment.py:13).  Neither gym nor

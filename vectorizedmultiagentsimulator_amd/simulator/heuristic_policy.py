@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Heuristic policy base classes (restates vmas/simulator/heuristic_policy.py)."""
 from abc import ABC, abstractmethod
 

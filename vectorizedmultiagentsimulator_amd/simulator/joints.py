@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Joints (restates vmas/simulator/joints.py).
 
 ``Joint`` is an observer that owns an optional "joint landmark" (a Line or Box of length

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """The Scenario plugin API (restates vmas/simulator/scenario.py:24-451).
 
 Scenarios subclass ``BaseScenario`` and implement ``make_world``, ``reset_world_at``,

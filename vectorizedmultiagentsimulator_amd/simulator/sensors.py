@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Sensors (restates vmas/simulator/sensors.py).  ``Lidar.measure`` runs one ray-cast kernel."""
 from __future__ import annotations
 

@@ -1,3 +1,5 @@
+# Derived from VMAS, Copyright (c) 2022-2024 ProrokLab (https://www.proroklab.org/), licensed under
+# GPL-3.0; modified for this MI355X build.  See NOTICE.md.
 """Constants and helpers of the simulator surface (restates vmas/simulator/utils.py).
 
 Physical constants are the reference's (utils.py:27-34).  ``TorchUtils`` keeps the reference's
