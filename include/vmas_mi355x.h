@@ -403,12 +403,12 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
                               const VmasPairDesc* pairs, const VmasJointDesc* joints,
                               VmasJitWorld** out_world);
 int32_t vmas_jit_world_destroy(VmasJitWorld* world);
-/* With the batch broadphase the step is a relay of launches on `stream` that runs every
- * fixed-point pass on the device (no host wait, no workgroup waiting for another): pass 0, then
- * substeps + 1 rerun launches that exit at once unless the previous pass found the mask violated.
- * *iterations is then 0 and vmas_jit_world_passes reports the count.  A fixed point that did not
- * converge writes NaN over the step's outputs and is returned by
- * vmas_jit_world_passes and by the next vmas_jit_world_step. */
+/* With the batch broadphase the step is ONE persistent launch on `stream` that runs every
+ * fixed-point pass on the device (no host wait; workgroups claim the 64-env groups per pass and
+ * only ever wait for groups that running workgroups have claimed, so co-residency of the grid is
+ * not assumed).  *iterations is then 0 and vmas_jit_world_passes reports the count.  A fixed
+ * point that did not converge within substeps + 2 passes writes NaN over the step's outputs and
+ * is returned by vmas_jit_world_passes and by the next vmas_jit_world_step. */
 int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
                             int32_t* iterations);
 /* Error bits the kernel has reported so far, without waiting (VMAS_OK if none): how a launch
@@ -416,15 +416,15 @@ int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* str
 int32_t vmas_jit_world_check(VmasJitWorld* world);
 /* Fixed-point passes of the last step (waits for it on its stream). */
 int32_t vmas_jit_world_passes(VmasJitWorld* world, int32_t* passes);
-/* Relay grid size, returned negative (plain launches); 0: host-driven passes
- * (VMAS_JIT_GRID=relay|host at create). */
+/* Persistent grid size, returned negative (plain launches); 0: host-driven passes
+ * (VMAS_JIT_GRID=persistent|host at create). */
 int32_t vmas_jit_world_grid(const VmasJitWorld* world);
 int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
 int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
                                   int64_t* launches);
-/* Device timer (timing on; batch-broadphase relay launches): the kernel itself accumulates,
- * per step, the span from pass 0 workgroup 0's start to the final fixed-point reduction (the
- * rerun launches that exit at once after it are not counted) (s_memrealtime, converted with the device's wall-clock rate);
+/* Device timer (timing on; batch-broadphase persistent launches): the kernel itself accumulates,
+ * per step, the span from workgroup 0's start to the final fixed-point decision
+ * (s_memrealtime, converted with the device's wall-clock rate);
  * *clock_ghz (may be NULL) is the in-kernel shader clock (s_memtime / s_memrealtime spans).  It also times launches replayed from a HIP graph, where HIP records
  * no events.  Waits for the device.  (bench.py's roofline timer; no reference counterpart.) */
 int32_t vmas_jit_world_device_timing(VmasJitWorld* world, int32_t reset, double* total_ms,

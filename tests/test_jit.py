@@ -69,12 +69,12 @@ def test_jit_balance_full_size_gpu(gpu_device):
     ("waterfall", dict(), None, 700),
 ], ids=["balance100k", "flocking", "waterfall"])
 def test_device_fixed_point_matches_host_loop_gpu(gpu_device, monkeypatch, name, kw, substeps, num_envs):
-    """The relay (fixed-point passes on the device, one launch per pass, no cross-workgroup
-    wait; also with a grid far below the group count) is bit-identical to the host-driven pass
-    loop and runs the same number of passes."""
+    """The persistent fixed point (every pass in one launch, groups claimed per pass; also with
+    a grid far below the group count, where workgroups claim several groups and steal) is
+    bit-identical to the host-driven pass loop and runs the same number of passes."""
     envs = {}
-    for mode, cap in (("host", None), ("relay", None), ("relay37", "37")):
-        monkeypatch.setenv("VMAS_JIT_GRID", mode[:5])
+    for mode, cap in (("host", None), ("persistent", None), ("persistent37", "37")):
+        monkeypatch.setenv("VMAS_JIT_GRID", mode.rstrip("0123456789"))
         if cap:
             monkeypatch.setenv("VMAS_JIT_GRID_CAP", cap)
         else:
@@ -89,11 +89,12 @@ def test_device_fixed_point_matches_host_loop_gpu(gpu_device, monkeypatch, name,
             env.world.step()
         eng = {m: e.world.engine for m, e in envs.items()}
         assert eng["host"].kernel_name == "k_world" and eng["host"].jit_grid == 0
-        assert eng["relay"].jit_grid < 0 and eng["relay37"].jit_grid == -min(37, (num_envs + 63) // 64)
+        assert eng["persistent"].jit_grid < 0
+        assert eng["persistent37"].jit_grid == -min(37, (num_envs + 63) // 64)
         passes = {m: e.last_iterations for m, e in eng.items()}
-        assert passes["relay"] == passes["relay37"] == passes["host"] >= 1, passes
+        assert passes["persistent"] == passes["persistent37"] == passes["host"] >= 1, passes
         a = O.snapshot(envs["host"].world)
-        for mode in ("relay", "relay37"):
+        for mode in ("persistent", "persistent37"):
             b = O.snapshot(envs[mode].world)
             for i in a:
                 for k in a[i]:
@@ -115,8 +116,8 @@ def _violating_pollock(device):
 
 
 @pytest.mark.gpu
-def test_relay_rerun_pass_gpu(gpu_device):
-    """The violating world needs the rerun launch (2 passes) and then equals the oracle."""
+def test_fixed_point_second_pass_gpu(gpu_device):
+    """The violating world needs a second pass (inside the one launch) and then equals the oracle."""
     env = _violating_pollock(gpu_device)
     rep = O.compare_one_step(env.world)
     assert env.world.engine.kernel_name == "k_world"
@@ -125,10 +126,10 @@ def test_relay_rerun_pass_gpu(gpu_device):
 
 
 @pytest.mark.gpu
-def test_relay_no_convergence_poisons_outputs_gpu(gpu_device, monkeypatch):
-    """A relay capped at one pass cannot converge on the violating world: the step's outputs are
-    NaN (visible in the step itself) and the sticky error is raised by the next check."""
-    monkeypatch.setenv("VMAS_JIT_RELAY", "1")
+def test_fixed_point_no_convergence_poisons_outputs_gpu(gpu_device, monkeypatch):
+    """A fixed point capped at one pass cannot converge on the violating world: the step's outputs
+    are NaN (visible in the step itself) and the sticky error is raised by the next check."""
+    monkeypatch.setenv("VMAS_JIT_MAX_PASSES", "1")
     env = _violating_pollock(gpu_device)
     env.world.engine._ensure()
     env.world.step()
@@ -140,10 +141,11 @@ def test_relay_no_convergence_poisons_outputs_gpu(gpu_device, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_relay_with_cus_held_by_another_stream_gpu(gpu_device):
-    """A kernel on a second stream holds half of the chip's wave slots for 0.5 s while the step
-    launches: part of the step's grid cannot become resident until it ends.  The relay has no
-    cross-workgroup wait, so the step completes exactly (oracle parity, no error bit)."""
+def test_fixed_point_with_cus_held_by_another_stream_gpu(gpu_device):
+    """A kernel on a second stream holds most of the chip's wave slots for 0.5 s while the step
+    launches: part of the step's grid cannot become resident until it ends.  Workgroups only wait
+    for groups that running workgroups have claimed, so the step completes exactly (oracle parity,
+    no error bit; the resident workgroups steal the groups of the absent ones)."""
     from vectorizedmultiagentsimulator_amd import _native as N
 
     env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=32768, seed=0)
@@ -154,7 +156,7 @@ def test_relay_with_cus_held_by_another_stream_gpu(gpu_device):
     band = O.sensitivity_band(w, snap, expected)
     side = torch.cuda.Stream()
     torch.cuda.synchronize()
-    N.check_aux(N.load_library().vmas_test_hold(0, 1024, 500_000, ctypes.c_void_p(side.cuda_stream)),
+    N.check_aux(N.load_library().vmas_test_hold(0, 224, 500_000, ctypes.c_void_p(side.cuda_stream)),
                 "vmas_test_hold")
     w.step()
     torch.cuda.synchronize()

@@ -381,14 +381,21 @@ int32_t vmas_assert_wait(VmasDeviceAssert* ch, int32_t slot, uint32_t seq, int32
     return VMAS_OK;
 }
 
-// Test utility: occupy CUs for `ticks` s_memrealtime ticks.  Every wave polls the wall clock and
-// leaves once the span has passed (or after a poll bound), so the grid always drains.
-__global__ void __launch_bounds__(256) k_hold(unsigned long long ticks) {
+// Test utility: occupy CUs for `ticks` s_memrealtime ticks.  Every workgroup holds 144 KiB of
+// the CU's 160 KiB LDS, so at most one fits per CU and no step workgroup (whose LDS is larger
+// than the 16 KiB left) fits beside it: `blocks` CUs are closed to other kernels for the span.
+// Every wave polls the wall clock and leaves once the span has passed (or after a poll bound),
+// so the grid always drains.
+__global__ void __launch_bounds__(256) k_hold(unsigned long long ticks, int* sink) {
+    __shared__ int hog[144 * 1024 / 4];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    hog[threadIdx.x] = (int)threadIdx.x;
     for (uint32_t i = 0; i < (1u << 28); ++i) {
         if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
         __builtin_amdgcn_s_sleep(8);
     }
+    __syncthreads();
+    if (sink && hog[(threadIdx.x * 7u) & 255u] < 0) sink[0] = 1;  // (never true: keeps the LDS)
 }
 
 int32_t vmas_test_hold(int32_t device, int32_t blocks, int64_t microseconds, void* stream) {
@@ -398,7 +405,7 @@ int32_t vmas_test_hold(int32_t device, int32_t blocks, int64_t microseconds, voi
     int khz = 0;
     VMAS_AUX_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
     const unsigned long long ticks = (unsigned long long)microseconds * (unsigned long long)(khz > 0 ? khz : 100000) / 1000ull;
-    hipLaunchKernelGGL(k_hold, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ticks);
+    hipLaunchKernelGGL(k_hold, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ticks, (int*)nullptr);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

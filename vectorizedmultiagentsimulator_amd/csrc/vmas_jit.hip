@@ -30,12 +30,12 @@
 // vmas_jit_world_create and the caller uses vmas_world_step.
 //
 // Batch-global broadphase (core.py:2796): the fixed-point scheme of vmas_world_step (R/Z flags
-// per block, a reduction that checks the mask, a re-run on violation), run on the device as a
-// relay of launches: pass 0 (k_world), then rerun launches (k_world_rerun) that exit at once
-// unless the previous pass asked for them.  The last workgroup to arrive in a pass reduces the
-// flags and publishes the decision; no workgroup waits for another (vmas_jit_ops.hpp
-// relay_arrive), so the host only launches.  VMAS_JIT_GRID=host keeps the host-driven loop (one
-// launch + reduction + host read per pass).
+// per group, a reduction that checks the mask, a re-run on violation), run on the device inside
+// ONE persistent launch: the 64-env groups are claimed per pass, the last completion of a pass
+// reduces the flags and publishes the decision, and a workgroup only ever waits for groups that
+// running workgroups have claimed -- never for another workgroup to become resident
+// (vmas_jit_ops.hpp grid_*).  The host only launches.  VMAS_JIT_GRID=host keeps the host-driven
+// loop (one launch + reduction + host read per pass).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <hip/hip_ext.h>
@@ -333,8 +333,8 @@ struct Gen {
     }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        // (+5 ints: B, S, sdt, max_pass, pass; the struct is padded to its 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 5);
+        // (+4 ints: B, S, sdt, max_pass; the struct is padded to its 8-byte alignment)
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
         return (n + 7) & ~(size_t)7;
     }
 
@@ -637,19 +637,20 @@ struct Gen {
             for (int e : wave_ents[w]) {
                 const VmasEntityDesc& d = ed[e];
                 const std::string s = it(e);
+                // sc1 (write-through) stores: a group re-run in a later fixed-point pass by a
+                // workgroup on another XCD must not race a dirty line of the earlier pass
+                // (vmas_jit_ops.hpp, memory order of the persistent launch)
                 if (d.out_lin >= 0)
-                    o += "        reinterpret_cast<float2*>(a.out[0])[(size_t)" + it(d.out_lin) + " * a.B + b] = make_float2(p" +
-                         s + ".x, p" + s + ".y);\n        reinterpret_cast<float2*>(a.out[1])[(size_t)" + it(d.out_lin) +
-                         " * a.B + b] = make_float2(v" + s + ".x, v" + s + ".y);\n";
+                    o += "        st_out2(a.out[0], (size_t)" + it(d.out_lin) + " * a.B + b, p" + s + ");\n        st_out2(a.out[1], (size_t)" +
+                         it(d.out_lin) + " * a.B + b, v" + s + ");\n";
                 if (d.out_rot >= 0)
-                    o += "        a.out[2][(size_t)" + it(d.out_rot) + " * a.B + b] = r" + s + ";\n        a.out[3][(size_t)" +
-                         it(d.out_rot) + " * a.B + b] = w" + s + ";\n";
+                    o += "        st_out1(a.out[2], (size_t)" + it(d.out_rot) + " * a.B + b, r" + s + ");\n        st_out1(a.out[3], (size_t)" +
+                         it(d.out_rot) + " * a.B + b, w" + s + ");\n";
                 if (d.agent_index >= 0) {
                     if (d.out_force >= 0)
-                        o += "        reinterpret_cast<float2*>(a.out[4])[(size_t)" + it(d.out_force) +
-                             " * a.B + b] = make_float2(af" + s + ".x, af" + s + ".y);\n";
+                        o += "        st_out2(a.out[4], (size_t)" + it(d.out_force) + " * a.B + b, af" + s + ");\n";
                     if (d.out_torque >= 0)
-                        o += "        a.out[5][(size_t)" + it(d.out_torque) + " * a.B + b] = at" + s + ";\n";
+                        o += "        st_out1(a.out[5], (size_t)" + it(d.out_torque) + " * a.B + b, at" + s + ");\n";
                 }
             }
             o += "    }\n";
@@ -663,7 +664,7 @@ struct Gen {
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
-             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n    int pass;\n};\n\n";
+             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
              "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
@@ -683,7 +684,7 @@ struct Gen {
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
         const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
         // NaN over every output field of the step (one workgroup; only after a fixed point that
-        // did not converge within the relay): the bad step is visible in its own results
+        // did not converge within max_pass passes): the bad step is visible in its own results
         {
             const int n_lin = cfg.n_out_lin, n_rot = cfg.n_out_rot, n_f = cfg.n_out_force, n_t = cfg.n_out_torque;
             const int per_env[6] = {2 * n_lin, 2 * n_lin, n_rot, n_rot, 2 * n_f, n_t};
@@ -700,49 +701,62 @@ struct Gen {
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
-        // idle between passes), else its own array
+        // idle between groups), else its own array; QL: steal list + broadcast word
         const int red_words = nfl + 2;
         o += "    __shared__ uint32_t MSK[" + it(std::max(nfl / 2, 1)) + "];\n";
+        o += "    __shared__ uint32_t QL[66];\n";
         if ((long)std::max(n_rows, 1) * 64 >= red_words)
             o += "    uint32_t* RED = reinterpret_cast<uint32_t*>(L);\n";
         else
             o += "    __shared__ uint32_t RED[" + it(red_words) + "];\n";
         o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n";
-        o += "    const int nfl = 2 * a.S * " + it(W) + ", ngrp = (a.B + 63) >> 6;\n"
+        o += "    const int nfl = 2 * a.S * " + it(W) + ", nwords = a.S * " + it(W) + ", ngrp = (a.B + 63) >> 6;\n"
              "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
-        // Relay launch (a.ctl set): workgroups stride over the 64-env groups and run pass a.pass
-        // of the broadphase fixed point; a rerun launch (a.pass > 0) exits at once unless the
-        // previous pass asked for it (vmas_jit_ops.hpp relay_arrive).  Otherwise (a.ctl null) one
-        // group per workgroup and one pass per launch (host-driven loop).  DONE is back to zero
-        // at the end of every substep's pair phase, so it carries over between groups.
-        o += "    const uint32_t epoch = a.ctl ? ld_agent(&a.ctl[3]) : 0u;\n";
-        o += "    if (a.ctl && a.pass > 0 && !relay_requested(a.ctl, epoch, a.pass)) return;\n";
-        o += "    const TimerStart t0s = device_timer_start(a.ctl ? a.tm : nullptr, a.pass == 0);\n";
-        o += "    const int pass = a.pass;\n"
+        // Host-driven loop (a.ctl null): one pass per launch, each workgroup strides over the
+        // 64-env groups and ORs their activity words into its own blk row (read by
+        // k_jit_flags_reduce).  Persistent launch (a.ctl set): the broadphase fixed point on the
+        // device; groups are claimed per pass (own groups, then steals), each completion stores
+        // the group's row, the last completion of a pass decides, waits are only for claimed
+        // work (vmas_jit_ops.hpp grid_*).  One call site of the group body (a second one would
+        // duplicate the per-wave code).  DONE is back to zero at the end of every substep's pair
+        // phase, so it carries over between groups.
+        o += "    const bool persistent = a.ctl != nullptr;\n"
+             "    uint32_t* claim = a.mask + " + it((long)cfg.max_substeps * W) + ";\n"
+             "    const TimerStart t0s = device_timer_start(persistent ? a.tm : nullptr, true);\n"
+             "    __shared__ GridCursor CUR;\n"
+             "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
-             "    for (int i = threadIdx.x; i < nfl / 2; i += blockDim.x)\n"
-             "        MSK[i] = ~__hip_atomic_load(&a.mask[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-             "    for (int g = blockIdx.x; g < ngrp; g += gridDim.x) {\n"
-             "        const int b = g * 64 + lane;\n"
-             "        const bool valid = b < a.B;\n"
-             "        const int bb = valid ? b : (a.B - 1);\n"
-             "        switch (wave) {\n";
-        for (int w = 0; w < nw; ++w)
-            o += "            case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
-        o += "            default: break;\n        }\n    }\n";
-        o += "    if (!a.blk) return;\n"
+             "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n"
              "    __syncthreads();\n"
-             "    uint32_t* dst = a.blk + (size_t)blockIdx.x * nfl;\n"
-             "    for (int i = threadIdx.x; i < nfl; i += blockDim.x)\n"
-             "        __hip_atomic_store(&dst[i], FL[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-             "    if (!a.ctl) return;\n"
-             "    if (relay_arrive(a.blk, a.mask, a.ctl, a.err, a.herr, a.S * " + it(W) +
-             ", pass, a.max_pass, RED, epoch, a.tm, t0s))\n"
-             "        poison_outputs(a);\n"
+             "    for (;;) {\n"
+             "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, &CUR, QL);\n"
+             "        if (g < 0) break;\n"
+             "        if (persistent) {\n"
+             "            for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+             "            __syncthreads();\n"
+             "        }\n"
+             "        {\n"
+             "            const int b = g * 64 + lane;\n"
+             "            const bool valid = b < a.B;\n"
+             "            const int bb = valid ? b : (a.B - 1);\n"
+             "            switch (wave) {\n";
+        for (int w = 0; w < nw; ++w)
+            o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
+        o += "                default: break;\n            }\n        }\n";
+        o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, a.ctl, a.err, a.herr, nwords, ngrp, CUR.pass,\n"
+             "                                      a.max_pass, RED, &QL[65], a.tm, t0s))\n"
+             "            poison_outputs(a);\n"
+             "    }\n"
+             "    if (!persistent) {\n"
+             "        if (!a.blk) return;\n"
+             "        __syncthreads();\n"
+             "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) st_agent(&a.blk[(size_t)blockIdx.x * nfl + i], FL[i]);\n"
+             "        return;\n"
+             "    }\n"
+             "    grid_exit(a.ctl, a.mask, claim, nwords, ngrp, a.max_pass, &QL[65]);\n"
              "}\n\n";
         const std::string bounds = "__launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) + ")";
         o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
-        o += "extern \"C\" __global__ void " + bounds + " k_world_rerun(Args a) {\n    world_body(a);\n}\n";
     }
 };
 
@@ -876,16 +890,17 @@ struct VmasJitWorld {
     size_t arg_bytes = 0;
     int W = 1, nblk = 0, nw = kNW;
     hipModule_t mod = nullptr;
-    hipFunction_t fn = nullptr, fn_rerun = nullptr;  // k_world (pass 0), k_world_rerun (passes >= 1)
+    hipFunction_t fn = nullptr;  // k_world
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
-    // relay launches: d_ctl = [kGridCtlWords control words | inverted mask words], zeroed at create;
+    // persistent launches: d_ctl = [kGridCtlWords control words | inverted mask words | claim word
+    // per group], zeroed at create and reset by the kernel's last workgroup;
     // d_err: sticky error bits; h_err: mapped host word the kernel stores them into (dh_err: its
     // device address)
     uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr, *dh_err = nullptr;
-    int grid = 0;          // workgroups of a relay launch (0: host-driven loop, one pass per launch)
-    int relay = 0;         // launches per step (0: substeps + 2, the fixed point's bound; VMAS_JIT_RELAY)
+    int grid = 0;          // workgroups of a persistent launch (0: host-driven loop, one pass per launch)
+    int max_passes = 0;    // fixed-point passes per step (0: substeps + 2, the bound; VMAS_JIT_MAX_PASSES)
     hipStream_t last_stream = nullptr;
-    int last_passes = 0;   // passes of the last host-driven step (relay: read on demand)
+    int last_passes = 0;   // passes of the last host-driven step (persistent: read on demand)
     bool last_persistent = false;
     unsigned long long* d_prof = nullptr;  // phase timestamps of one workgroup (VMAS_JIT_PROFILE)
     size_t n_prof = 0;
@@ -893,7 +908,7 @@ struct VmasJitWorld {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
     double timed_ms = 0.0;
     long timed_launches = 0;
-    // device timer (timing on, relay launches): [0] pass 0 workgroup 0's start, [2] accumulated
+    // device timer (timing on, persistent launches): [0] workgroup 0's start, [2] accumulated
     // ticks, [4] launches -- s_memrealtime, kept by the kernel itself so that launches replayed
     // from a HIP graph are timed too (HIP records no events inside a graph; vmas_jit_ops.hpp)
     unsigned long long* d_tm = nullptr;
@@ -968,8 +983,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
         if (hipModuleLoadData(&W->mod, code.data()) != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
-        if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess ||
-            hipModuleGetFunction(&W->fn_rerun, W->mod, "k_world_rerun") != hipSuccess)
+        if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
         int scratch = 0;
         (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
@@ -989,25 +1003,27 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
-    if (hipMalloc((void**)&W->d_ctl, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
+    const size_t ctl_words = vmas::kGridCtlWords + nwords + (size_t)W->nblk;
+    if (hipMalloc((void**)&W->d_ctl, ctl_words * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_err, 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W->dh_err, W->h_err, 0) != hipSuccess ||
         hipMemset(W->d_err, 0, 4) != hipSuccess ||
-        hipMemset(W->d_ctl, 0, (vmas::kGridCtlWords + nwords) * 4) != hipSuccess)
+        hipMemset(W->d_ctl, 0, ctl_words * 4) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc fixed-point control words"));
     *W->h_err = 0u;
     if (hipMalloc((void**)&W->d_tm, 8 * 8) != hipSuccess || hipMemset(W->d_tm, 0, 8 * 8) != hipSuccess ||
         hipDeviceGetAttribute(&W->wall_khz, hipDeviceAttributeWallClockRate, cfg->device) != hipSuccess ||
         W->wall_khz <= 0)
         return cleanup(jfail(VMAS_E_HIP, "device timer (hipMalloc / wall clock rate)"));
-    // Relay grid (vmas_jit_ops.hpp relay_arrive): as many workgroups as can be resident at once
-    // (occupancy x CUs), capped by the number of 64-env groups; each strides over the groups.
-    // Nothing waits across workgroups, so residency is a performance choice, not a requirement.
-    // VMAS_JIT_GRID=host keeps the host-driven loop (one launch + reduction + host read per pass);
-    // VMAS_JIT_RELAY=<n> caps the launches per step (default substeps + 2: the fixed point's bound).
+    // Persistent grid (vmas_jit_ops.hpp grid_*): as many workgroups as can be resident at once
+    // (occupancy x CUs), capped by the number of 64-env groups; each claims its own groups, then
+    // steals.  Waits are only for claimed work, so residency is a performance choice, not a
+    // requirement.  VMAS_JIT_GRID=host keeps the host-driven loop (one launch + reduction + host
+    // read per pass); VMAS_JIT_MAX_PASSES=<n> caps the passes per step (default substeps + 2, the
+    // fixed point's bound; at most kGridMaxPasses).
     {
         const char* gm = getenv("VMAS_JIT_GRID");
-        const std::string mode = gm ? gm : "relay";
+        const std::string mode = gm ? gm : "persistent";
         int per_cu = 0, cus = 0;
         if (mode != "host" &&
             hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, W->fn, W->nw * 64, 0) == hipSuccess &&
@@ -1015,7 +1031,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             per_cu > 0 && cus > 0) {
             W->grid = std::min(W->nblk, per_cu * cus);
             if (const char* cap = getenv("VMAS_JIT_GRID_CAP")) W->grid = std::max(1, std::min(W->grid, atoi(cap)));
-            if (const char* r = getenv("VMAS_JIT_RELAY")) W->relay = std::max(1, atoi(r));
+            if (const char* r = getenv("VMAS_JIT_MAX_PASSES")) W->max_passes = std::max(1, atoi(r));
         }
     }
     if (g.prof_block >= 0) {
@@ -1153,17 +1169,14 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     memcpy(p, &io->sub_dt, 4);
     p += 4;
     const int max_it = batch_bp ? io->substeps + 2 : 1;
-    const int relay_len = W->relay > 0 ? std::min(W->relay, max_it) : max_it;
-    int32_t* arg_pass = nullptr;
-    put_i32(persistent ? relay_len : max_it);
-    arg_pass = reinterpret_cast<int32_t*>(p);
-    put_i32(0);
+    const int max_pass = std::min(W->max_passes > 0 ? std::min(W->max_passes, max_it) : max_it, vmas::kGridMaxPasses);
+    put_i32(persistent ? max_pass : max_it);
     size_t size = ((size_t)(p - buf.data()) + 7) & ~(size_t)7;
     if (size > buf.size()) return jfail(VMAS_E_INVALID, "kernel argument block overflow");
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
 
-    // a fixed-point failure of an earlier relay step (sticky error bits, which the kernel
+    // a fixed-point failure of an earlier step (sticky error bits, which the kernel
     // stores into mapped host memory) surfaces here
     if (uint32_t e = *(volatile uint32_t*)W->h_err)
         return jfail(e & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
@@ -1171,7 +1184,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     W->last_stream = stream;
     W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
-    // (the relay resets its own control words: see relay_arrive)
+    // (the persistent kernel resets its own control words: see grid_exit)
     if (!persistent) JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
     // Timing (vmas_jit_world_set_timing): the events ride on the kernel's own dispatch packet
     // (hipExtModuleLaunchKernel), so they bracket its execution alone, as rocprofv3's kernel
@@ -1189,7 +1202,6 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     JHIP(hipStreamIsCapturing(stream, &cap));
     const bool capturing = cap == hipStreamCaptureStatusActive;
-    // (timed: only k_world, pass 0; a rerun is counted by the device timer of the relay)
     auto launch_plain = [&](int blocks, hipFunction_t fn, bool timed) -> int32_t {
         const uint32_t threads = (uint32_t)W->nw * 64;
         if (!W->timing || capturing || !timed) {  // (a captured launch is timed by the device timer)
@@ -1204,12 +1216,8 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
         return VMAS_OK;
     };
     if (persistent) {
-        // the relay: pass 0, then relay_len - 1 rerun launches that exit at once unless the
-        // previous pass asked for them; nothing waits on the host or across workgroups
-        for (int pass = 0; pass < relay_len; ++pass) {
-            *arg_pass = pass;  // (the launch copies the argument block)
-            if (int32_t rc = launch_plain(W->grid, pass ? W->fn_rerun : W->fn, pass == 0)) return rc;
-        }
+        // one launch runs every pass of the fixed point; nothing waits on the host
+        if (int32_t rc = launch_plain(W->grid, W->fn, true)) return rc;
         if (iterations) *iterations = 0;  // not known without a sync: vmas_jit_world_passes
         return VMAS_OK;
     }
@@ -1258,7 +1266,7 @@ int32_t vmas_jit_world_check(VmasJitWorld* W) {
     return VMAS_OK;
 }
 
-// 0: host-driven passes; otherwise the relay's grid size (returned negative: plain launches)
+// 0: host-driven passes; otherwise the persistent grid size (returned negative: plain launches)
 int32_t vmas_jit_world_grid(const VmasJitWorld* W) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
     return -W->grid;
@@ -1270,7 +1278,7 @@ int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
     return VMAS_OK;
 }
 
-// Device timer totals (timing on, relay launches): every launch -- eager or replayed from a
+// Device timer totals (timing on, persistent launches): every launch -- eager or replayed from a
 // HIP graph -- adds (final reduction - workgroup 0 start) in s_memrealtime ticks; *clock_ghz is
 // the in-kernel shader clock of the reducing workgroups.  Waits for the device.
 int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches,

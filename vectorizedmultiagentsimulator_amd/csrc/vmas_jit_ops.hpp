@@ -79,41 +79,51 @@ __device__ __forceinline__ void integrate(const VmasEntityDesc& d, int substep, 
 #endif
 
 // Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily).
-// (kGridErrStateTimeout belonged to the former spin-waiting persistent launch; no code sets it.)
+// (kGridErrStateTimeout belonged to an earlier spin-waiting launch; no code sets it.)
 constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 
-// Device-side fixed point of the batch-global broadphase as a RELAY of launches, with no
-// workgroup ever waiting for another (so nothing assumes that the workgroups of a launch are
-// co-resident).  The step enqueues L launches on one stream: pass 0 (k_world) and passes
-// 1..L-1 (k_world_rerun).  Every launch is an ordinary grid over the 64-env groups:
-//   * each workgroup stores the OR of its R/Z activity words in blk[blockIdx.x] ([2][nwords])
-//     and arrives on a two-level counter;
-//   * the LAST workgroup to arrive ORs every row, applies the k_jit_flags_reduce test (was the
-//     mask a fixed point?) and publishes the decision in ctl[1] = (epoch << 8 | (pass+1) << 1 |
-//     continue), with the next mask (stored inverted, so zero means "all pairs active");
-//   * a rerun launch reads ctl[1] first and exits at once unless the previous pass asked for it.
-// Stream order between the launches is the only synchronisation: a launch starts after the
-// previous one has completed, with its memory visible (kernel-boundary release / acquire).
-// ctl: [0] top arrival counter, [1] published word, [2] passes run, [3] launch epoch, [32 * (1 +
-// k)] arrival counter of the workgroups with blockIdx % 8 == k (one 128-byte line each: 512
-// arrivals on one address serialise at the memory side).  No host memset: the final pass's
-// reducer, which runs after every workgroup of the step has arrived, clears the counters and the
-// mask words for the next step and advances the epoch, which keeps the previous step's
-// published word from being read as this step's.
+// Device-side fixed point of the batch-global broadphase (core.py:2796) in ONE persistent launch
+// whose only cross-workgroup wait is for work that a RUNNING workgroup has claimed -- so nothing
+// assumes that the workgroups of the launch are co-resident.
 //
-// Why no spin-wait any more (the former single persistent launch): its waiting workgroups needed
-// every workgroup of the grid resident at once, which a plain launch does not guarantee (a kernel
-// of another stream or process holding CUs delays some workgroups; the resident ones then spun
-// until their bound and the step completed with a non-fixed-point mask).  The relay has no such
-// assumption.  The graph-replay timeouts seen with a memset node in front of the persistent
-// kernel are consistent with the same cause: the waits could only time out if an arrival never
-// came, i.e. a workgroup of the grid was not running (or its counter increment was zeroed by a
-// memset that had not completed when the first workgroups arrived).  Neither can stall a relay.
+//   * Work items are the 64-env groups.  Group g is claimed for pass p by a compare-and-swap of
+//     claim[g] from p to p + 1 (one word per group: no contended counter).  A workgroup first
+//     claims its own groups (g = blockIdx.x + k * gridDim.x), then, unless the claim counters
+//     (sharded g % 8) say every group is taken, scans for groups still unclaimed in this pass
+//     and steals them (normally none: every workgroup has started long before the first one
+//     finishes).
+//   * Processing a group ends with its R/Z activity row stored in blk[g] and one completion on a
+//     two-level counter (sub-counter g % 8, one 128-byte line each, then the top counter;
+//     cumulative over the passes of a step).  The workgroup whose completion is the last of the
+//     pass is the DECIDER: it ORs the rows, applies the k_jit_flags_reduce test (was the mask a
+//     fixed point?), stores the next mask (inverted: zero means "all pairs active") and publishes
+//     dec[p] = 2 | continue.
+//   * A workgroup that finds nothing left to claim in pass p waits for dec[p].  Every group of
+//     pass p is then claimed, and a group is claimed only by a workgroup that is executing, which
+//     finishes it without waiting for anyone: the decision always comes, whichever workgroups
+//     are resident (a workgroup that only becomes resident later finds every group claimed and
+//     the decisions published, and follows them to the exit).
+//   * The last workgroup to exit (exit counter == gridDim.x: nobody reads the control words any
+//     more) resets claims, counters, decisions and the mask for the next step: no host memset,
+//     so the step stays one capturable kernel node.
+// Memory order (MI355X_MICROARCH.md, the sc1 hand-off forms): every byte handed between
+// workgroups inside the launch -- activity rows, mask words, claims, counters, decisions -- is
+// stored and loaded with agent-scope atomics (sc1: L1 bypassed, L2 dropped / written through);
+// every storing wave waits for its stores (s_waitcnt 0) and the workgroup synchronises before
+// lane 0 signals (a completion add, a decision store); a consumer loads only after its add
+// returned last or its poll matched, and its other waves after a barrier.  No agent fences
+// (1.7-6.5 us each on the critical path).  The step outputs are stored sc1 as well, so a group
+// re-run in a later pass by a workgroup on another XCD never races a dirty line of the earlier
+// pass: the earlier stores have completed (s_waitcnt) before the completion that precedes the
+// decision that precedes the re-run.
 //
-// RED: workgroup LDS of 2 * nwords + 2 words.  Returns true in the reducer of a final pass that
-// did NOT converge (the caller then poisons the step's outputs with NaN, so that the bad step is
-// visible in its own results; the sticky error bit also fails the next step).
-constexpr int kGridCtlWords = 32 * 9;
+// ctl (uint32): [0] top completion counter, [2] passes run by the last step, [32 * (1 + k)]
+// completion sub-counter k, [32 * 9] exit counter, [32 * (10 + k)] claim sub-counter k,
+// [32 * 18 + p] dec[p] (p < kGridMaxPasses); then the mask words (nwords) and the claim words
+// (one per group).
+constexpr int kGridMaxPasses = 64;
+constexpr int kGridExit = 32 * 9, kGridClaimed = 32 * 10, kGridDec = 32 * 18;
+constexpr int kGridCtlWords = kGridDec + kGridMaxPasses;
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -124,12 +134,23 @@ __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
     return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ bool cas_agent(uint32_t* p, uint32_t expect, uint32_t v) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+// step outputs, stored sc1 (write-through: no dirty copy stays in the XCD's L2)
+__device__ __forceinline__ void st_out1(float* p, size_t i, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p) + i, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_out2(float* p, size_t i, V2 v) {
+    const unsigned long long bits = (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p) + i, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Device timer (timing on, persistent launches): workgroup 0 stamps s_memrealtime into tm[0] at
-// its start; the final pass's reducer -- the last workgroup to arrive, after which every
-// workgroup only reads the published word and exits -- adds (now - tm[0]) to tm[2] and counts
-// the launch in tm[4].  Two stores per launch instead of per-workgroup atomics (measured: ~10 us
-// on a 512-workgroup launch).  The reducer also adds its own s_memtime (shader clock) and
+// its start; the decider of the final pass adds (now - tm[0]) to tm[2] and counts the launch in
+// tm[4].  Two stores per launch instead of per-workgroup atomics (measured: ~10 us on a
+// 512-workgroup launch).  The decider also adds its own s_memtime (shader clock) and
 // s_memrealtime (100 MHz-class wall clock) spans to tm[5] / tm[6]: their ratio is the in-kernel
 // shader clock (MI355X_MICROARCH.md, DVFS give-back item 6).
 struct TimerStart {
@@ -146,11 +167,6 @@ __device__ __forceinline__ TimerStart device_timer_start(unsigned long long* tm,
     return t;
 }
 
-// Whether a rerun launch of pass `pass` (>= 1) was requested by the previous pass of this step.
-__device__ __forceinline__ bool relay_requested(const uint32_t* ctl, uint32_t epoch, int pass) {
-    return ld_agent(&ctl[1]) == (((epoch & 0xFFFFFFu) << 8) | ((uint32_t)pass << 1) | 1u);
-}
-
 // Sticky error bits: OR-ed into the device word, and the OR so far stored into the mapped host
 // word (system scope, no fence: any nonzero value means failure), so the host sees a failure
 // without a copy in the stream.
@@ -159,30 +175,80 @@ __device__ __forceinline__ void report_err(uint32_t* err, uint32_t* herr, uint32
     if (herr) __hip_atomic_store(herr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ inline bool relay_arrive(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
-                                    int nwords, int pass, int max_pass, uint32_t* RED, uint32_t epoch,
-                                    unsigned long long* tm, TimerStart t0s) {
-    const uint32_t tag = ((epoch & 0xFFFFFFu) << 8) | ((uint32_t)(pass + 1) << 1);
-    const uint32_t G = gridDim.x, k = blockIdx.x & 7u;
-    const uint32_t n_k = (G + 7u - k) / 8u, n_sub = G < 8u ? G : 8u;  // workgroups in sub-counter k
-    const int nw2 = 2 * nwords;
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's blk stores have completed
+// Claim group g for pass `pass` (one thread): claim[g] p -> p + 1, counted on the claim
+// sub-counter g % 8 (cumulative over the passes of a step).
+__device__ __forceinline__ bool grid_claim(uint32_t* ctl, uint32_t* claim, int g, int pass) {
+    if (ld_agent(&claim[g]) != (uint32_t)pass || !cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) return false;
+    (void)add_agent(&ctl[kGridClaimed + 32 * (g & 7)], 1u);
+    return true;
+}
+
+// Whether every group of `pass` is claimed (all threads; 8 loads).
+__device__ __forceinline__ bool grid_all_claimed(uint32_t* ctl, int ngrp, int pass, uint32_t* FLAG) {
+    if (threadIdx.x == 0) *FLAG = 0u;
+    __syncthreads();
+    if ((int)threadIdx.x < 8 && (int)threadIdx.x < ngrp) {
+        const uint32_t k = threadIdx.x, n_k = ((uint32_t)ngrp + 7u - k) / 8u;
+        if (ld_agent(&ctl[kGridClaimed + 32 * k]) != n_k * (uint32_t)(pass + 1)) atomicOr(FLAG, 1u);
+    }
+    __syncthreads();
+    const bool all = *FLAG == 0u;
+    __syncthreads();
+    return all;
+}
+
+// Steal round (all threads): claim up to 64 groups still unclaimed in `pass`; returns the count,
+// groups in LIST[0..count).  LIST: 65 words of LDS.  A claim beyond the list is put back.
+__device__ __forceinline__ int grid_steal(uint32_t* ctl, uint32_t* claim, int ngrp, int pass, uint32_t* LIST) {
+    if (threadIdx.x == 0) LIST[64] = 0u;
+    __syncthreads();
+    for (int g = (int)threadIdx.x; g < ngrp; g += (int)blockDim.x)
+        if (ld_agent(&claim[g]) == (uint32_t)pass && cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) {
+            const uint32_t i = atomicAdd(&LIST[64], 1u);
+            if (i < 64u) {
+                LIST[i] = (uint32_t)g;
+                (void)add_agent(&ctl[kGridClaimed + 32 * (g & 7)], 1u);
+            } else {
+                st_agent(&claim[g], (uint32_t)pass);
+            }
+        }
+    __syncthreads();
+    const int n = LIST[64] < 64u ? (int)LIST[64] : 64;
+    __syncthreads();
+    return n;
+}
+
+// Completion of group g in `pass` (all threads; the group's row and outputs are stored).
+// Returns true in the workgroup that completed the pass (the decider).
+__device__ __forceinline__ bool grid_complete(uint32_t* ctl, int g, int ngrp, int pass, uint32_t* FLAG) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
+        const uint32_t k = (uint32_t)g & 7u, n_k = ((uint32_t)ngrp + 7u - k) / 8u;
+        const uint32_t n_sub = ngrp < 8 ? (uint32_t)ngrp : 8u;
         bool last = false;
         if (add_agent(&ctl[32 * (1 + k)], 1u) == n_k * (uint32_t)(pass + 1) - 1u)
             last = add_agent(&ctl[0], 1u) == n_sub * (uint32_t)(pass + 1) - 1u;
-        RED[nw2] = last ? 1u : 0u;
+        *FLAG = last ? 1u : 0u;
     }
     __syncthreads();
-    const bool reducer = RED[nw2] != 0u;
+    const bool last = *FLAG != 0u;
     __syncthreads();
-    if (!reducer) return false;  // nothing to wait for: the next launch reads the decision
-    // the reducer: every row has arrived
+    return last;
+}
+
+// The decider of pass `pass` (all threads): every group's row is in blk.  RED: 2 * nwords + 2
+// words of LDS.  Returns true when the final pass did NOT converge (the caller then poisons the
+// step's outputs with NaN, so that the bad step is visible in its own results; the sticky error
+// bit also fails the next step).
+__device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
+                                   int nwords, int ngrp, int pass, int max_pass, uint32_t* RED,
+                                   unsigned long long* tm, TimerStart t0s) {
+    const int nw2 = 2 * nwords;
     for (int w = threadIdx.x; w < nw2 + 2; w += blockDim.x) RED[w] = 0u;
     __syncthreads();
     {
-        const int rows = (int)G, t = (int)threadIdx.x;
+        const int rows = ngrp, t = (int)threadIdx.x;
         if (nw2 <= (int)blockDim.x) {  // rows split over blockDim / nw2 thread groups per word
             const int per = (int)blockDim.x / nw2, w = t % nw2, g0 = t / nw2;
             if (g0 < per) {
@@ -221,14 +287,8 @@ __device__ inline bool relay_arrive(const uint32_t* blk, uint32_t* nmask, uint32
     if (threadIdx.x == 0) {
         if (viol && !more) report_err(err, herr, kGridErrNoConverge);
         st_agent(&ctl[2], (uint32_t)(pass + 1));
-        st_agent(&ctl[1], tag | (more ? 1u : 0u));
-    }
-    if (!more) {  // the final pass: every workgroup of the step has arrived; reset for the next step
-        for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
-        if (threadIdx.x == 0) st_agent(&ctl[0], 0u);
-        if (threadIdx.x >= 1 && threadIdx.x <= 8) st_agent(&ctl[32 * threadIdx.x], 0u);
-        if (threadIdx.x == 9) st_agent(&ctl[3], epoch + 1u);
-        if (tm && threadIdx.x == 0) {  // (thread 0 holds this workgroup's start stamps)
+        st_agent(&ctl[kGridDec + pass], more ? 3u : 2u);
+        if (!more && tm) {  // (thread 0 holds this workgroup's start stamps)
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             const unsigned long long c1 = __builtin_amdgcn_s_memtime();
             const unsigned long long t0 = __hip_atomic_load(&tm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -242,6 +302,106 @@ __device__ inline bool relay_arrive(const uint32_t* blk, uint32_t* nmask, uint32
     }
     __syncthreads();
     return viol && !more;
+}
+
+// Wait for the decision of `pass` (all threads): true when another pass follows.
+__device__ __forceinline__ bool grid_wait(const uint32_t* ctl, int pass, uint32_t* FLAG) {
+    if (threadIdx.x == 0) {
+        uint32_t d;
+        while ((d = ld_agent(&ctl[kGridDec + pass])) == 0u) __builtin_amdgcn_s_sleep(4);
+        *FLAG = d;
+    }
+    __syncthreads();
+    const bool more = (*FLAG & 1u) != 0u;
+    __syncthreads();
+    return more;
+}
+
+// Per-workgroup cursor of the persistent launch (LDS; thread 0 writes it, behind barriers).
+struct GridCursor {
+    int pass, own, nl, il;
+};
+
+// The next group this workgroup processes, or -1 once the step is done (all threads).  Host-driven
+// launches (persistent false): the workgroup's own groups.  Persistent launches: own groups
+// claimed for the current pass, then the steal list, then steal rounds while the claim counters
+// say a group is unclaimed, then the pass decision -- another pass restarts the cursor and
+// reloads MSK from the (inverted) mask words.  Not inlined: its loop-invariant addresses would be
+// hoisted around the group body and spill its registers (measured: +125 SGPR spills on balance).
+__device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ctl, uint32_t* claim, const uint32_t* mask,
+                                                   uint32_t* MSK, int nwords, int ngrp, GridCursor* CUR, uint32_t* QL) {
+    GridCursor c = *CUR;
+    int g = -1;
+    for (;;) {
+        if (c.own < ngrp) {
+            const int own = c.own;
+            c.own += (int)gridDim.x;
+            if (!persistent) {
+                g = own;
+                break;
+            }
+            if (threadIdx.x == 0) QL[65] = grid_claim(ctl, claim, own, c.pass) ? 1u : 0u;
+            __syncthreads();
+            const bool mine = QL[65] != 0u;
+            __syncthreads();
+            if (mine) {
+                g = own;
+                break;
+            }
+        } else if (!persistent) {
+            break;
+        } else if (c.il < c.nl) {
+            g = (int)QL[c.il++];
+            break;
+        } else if (!grid_all_claimed(ctl, ngrp, c.pass, &QL[65])) {
+            c.nl = grid_steal(ctl, claim, ngrp, c.pass, QL);
+            c.il = 0;
+            if (c.nl == 0) __builtin_amdgcn_s_sleep(2);
+        } else if (grid_wait(ctl, c.pass, &QL[65])) {
+            ++c.pass;
+            c.own = (int)blockIdx.x;
+            c.nl = c.il = 0;
+            for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&mask[i]);
+        } else {
+            break;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *CUR = c;
+    __syncthreads();
+    return g;
+}
+
+// End of group g (all threads; persistent launches): its activity row FL into blk[g], the
+// completion, and -- in the decider -- the pass decision.  Returns true when the step's final
+// pass did not converge (the caller poisons the outputs).  Not inlined (see grid_next).
+__device__ __attribute__((noinline)) bool grid_finish(int g, const uint32_t* FL, int nfl, uint32_t* blk, uint32_t* nmask,
+                                                      uint32_t* ctl, uint32_t* err, uint32_t* herr, int nwords, int ngrp,
+                                                      int pass, int max_pass, uint32_t* RED, uint32_t* FLAG,
+                                                      unsigned long long* tm, TimerStart t0s) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nfl; i += blockDim.x) st_agent(&blk[(size_t)g * nfl + i], FL[i]);
+    return grid_complete(ctl, g, ngrp, pass, FLAG) &&
+           grid_decide(blk, nmask, ctl, err, herr, nwords, ngrp, pass, max_pass, RED, tm, t0s);
+}
+
+// Exit (all threads): the last workgroup out resets the control words for the next step.
+__device__ __forceinline__ void grid_exit(uint32_t* ctl, uint32_t* nmask, uint32_t* claim, int nwords, int ngrp,
+                                          int max_pass, uint32_t* FLAG) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const bool last = add_agent(&ctl[kGridExit], 1u) == gridDim.x - 1u;
+        *FLAG = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (*FLAG == 0u) return;
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
+    for (int g = threadIdx.x; g < ngrp; g += blockDim.x) st_agent(&claim[g], 0u);
+    for (int p = threadIdx.x; p < max_pass; p += blockDim.x) st_agent(&ctl[kGridDec + p], 0u);
+    if (threadIdx.x == 0) st_agent(&ctl[0], 0u);
+    if (threadIdx.x >= 1 && threadIdx.x <= 8) st_agent(&ctl[32 * threadIdx.x], 0u);
+    if (threadIdx.x >= 16 && threadIdx.x < 24) st_agent(&ctl[kGridClaimed + 32 * (threadIdx.x - 16)], 0u);
+    if (threadIdx.x == 9) st_agent(&ctl[kGridExit], 0u);
 }
 
 }  // namespace vmas
