@@ -386,8 +386,22 @@ typedef struct VmasBalanceIO {
     float* rewards[VMAS_SCN_MAX_AGENTS]; /* [B] per agent (REWARD) */
     float* obs[VMAS_SCN_MAX_AGENTS];     /* [B, 16] contiguous per agent (OBS) */
     uint8_t* done;                       /* [B] torch.bool (DONE) */
+    float* pos_rew_prev; /* [B] the previous pos_rew, zeroed in place (REWARD; the reference's
+                            `pos_rew[:] = 0` before re-binding it); may be NULL */
 } VmasBalanceIO;
 int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream);
+
+/* Device-to-device byte copies, all spans in one launch (csrc/vmas_copy.hip): graph mode's carried
+ * state, output clones and per-step backups (simulator/environment/_graph.py; no reference
+ * counterpart -- the reference returns fresh tensors from its eager ops).  Spans must not
+ * overlap one another's destinations; more than VMAS_COPY_MAX_SPANS spans take several launches. */
+#define VMAS_COPY_MAX_SPANS 48
+typedef struct VmasCopySpan {
+    const void* src;
+    void* dst;
+    int64_t nbytes;
+} VmasCopySpan;
+int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, void* stream);
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);

@@ -1,0 +1,103 @@
+"""Fused scenario programs (csrc/vmas_scenarios.hip, simulator/_fused.py):
+on a GPU world a benchmark scenario's per-step reward / observation / done tensor program runs as
+one native launch.  Its oracle is the scenario's own torch program (the reference's, restated in
+scenarios/): the same env stepped with the program forced to torch must give bit-identical
+outputs, scenario attributes and world state, eagerly and replayed from a HIP graph, across
+reset_at / reset."""
+
+import pytest
+import torch
+
+from vectorizedmultiagentsimulator_amd import make_env
+from vectorizedmultiagentsimulator_amd.simulator import _fused
+from vectorizedmultiagentsimulator_amd.simulator.environment import Environment
+
+from test_graph import _assert_same, _flat, _rng_load, _rng_save, _state
+
+
+def test_fused_programs_off_on_cpu_worlds():
+    env = make_env("balance", num_envs=4, device="cpu", seed=0, n_agents=3)
+    assert not _fused.enabled(env.world)
+
+
+# (scenario, kwargs, substeps, scenario attributes the program leaves behind)
+FUSED = [
+    ("balance", dict(n_agents=4), 10, ["on_the_ground", "package_dist", "ground_rew", "pos_rew", "global_shaping"]),
+]
+
+
+class _Torch:
+    """Context: the scenario programs run as torch ops (the reference's program)."""
+
+    def __enter__(self):
+        self.prev = _fused._ON
+        _fused._ON = False
+
+    def __exit__(self, *exc):
+        _fused._ON = self.prev
+
+
+def _attrs(env, names):
+    return [getattr(env.scenario, n) for n in names]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps,attrs", FUSED, ids=[c[0] for c in FUSED])
+def test_fused_program_matches_torch_program_gpu(gpu_device, name, kw, substeps, attrs):
+    envs = {}
+    for mode in ("torch", "fused", "graph"):
+        saved = _rng_save()
+        with _Torch() if mode == "torch" else _NullCtx():
+            env = make_env(name, num_envs=777, device=gpu_device, seed=3, graph_step=mode == "graph", **kw)
+        if substeps:
+            env.world._substeps = substeps
+            env.world._sub_dt = env.world._dt / substeps
+        envs[mode] = env
+        if mode != "graph":
+            _rng_load(saved)
+    ref = envs["torch"]
+    for t in range(12):
+        actions = ref.get_random_actions()
+        outs = {}
+        for mode, env in envs.items():
+            s = _rng_save()
+            with _Torch() if mode == "torch" else _NullCtx():
+                if t == 5:
+                    env.reset_at(7)
+                if t == 9:
+                    env.reset()
+                outs[mode] = env.step([a.clone() for a in actions])
+            if mode != "graph":
+                _rng_load(s)
+        for mode in ("fused", "graph"):
+            _assert_same(outs["torch"], outs[mode], f"{name} {mode} outputs step {t}")
+            _assert_same(_state(ref), _state(envs[mode]), f"{name} {mode} state step {t}")
+            _assert_same(_attrs(ref, attrs), _attrs(envs[mode], attrs), f"{name} {mode} attributes step {t}")
+    assert envs["graph"].graph_status == "graph", envs["graph"].graph_reason
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+@pytest.mark.gpu
+def test_fused_balance_cache_follows_state_changes_gpu(gpu_device):
+    """A call whose inputs changed since the launch recomputes (the reference recomputes on every
+    call): an observation after an in-place position edit, and a second reward call."""
+    env = make_env("balance", num_envs=64, device=gpu_device, seed=0, n_agents=3)
+    env.step(env.get_random_actions())
+    sc, w = env.scenario, env.world
+    r0 = sc.reward(w.agents[0])
+    with torch.no_grad():
+        w.agents[1].state.pos[3, 0] += 0.25
+    obs1 = sc.observation(w.agents[1])
+    with _Torch():
+        expect = sc.observation(w.agents[1])
+    assert torch.equal(obs1, expect)
+    r0b = sc.reward(w.agents[2])
+    assert torch.equal(r0, r0b) and r0.data_ptr() != r0b.data_ptr()
+    assert torch.equal(sc.done(), sc.on_the_ground + w.is_overlapping(sc.package, sc.package.goal))

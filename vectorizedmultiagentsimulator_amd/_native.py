@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = (
     "vmas_host_waits",
     "vmas_test_hold",
     "vmas_balance_outputs",
+    "vmas_copy_spans",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -207,6 +208,30 @@ class VmasShapeRef(ctypes.Structure):
     ]
 
 
+VMAS_COPY_MAX_SPANS = 48
+
+
+class VmasCopySpan(ctypes.Structure):
+    _fields_ = [("src", _vp), ("dst", _vp), ("nbytes", ctypes.c_int64)]
+
+
+def copy_raw(device_index: int, spans, stream) -> None:
+    """One native launch (vmas_copy_spans) for every (src_ptr, dst_ptr, nbytes) span."""
+    n = len(spans)
+    if not n:
+        return
+    arr = (VmasCopySpan * n)()
+    for i, (src, dst, nb) in enumerate(spans):
+        arr[i].src, arr[i].dst, arr[i].nbytes = src, dst, nb
+    check_aux(load_library().vmas_copy_spans(device_index, arr, n, stream), "vmas_copy_spans")
+
+
+def copy_spans(device_index: int, pairs, stream) -> None:
+    """dst.copy_(src) for every (dst, src) pair of same-size contiguous device tensors, all in one
+    native launch (vmas_copy_spans; any dtype: bytes are copied)."""
+    copy_raw(device_index, [(s.data_ptr(), d.data_ptr(), d.numel() * d.element_size()) for d, s in pairs], stream)
+
+
 class VmasVec(ctypes.Structure):
     _fields_ = [("p", _vp), ("s0", _i32), ("s1", _i32)]
 
@@ -226,7 +251,7 @@ class VmasBalanceIO(ctypes.Structure):
         ("global_shaping_out", _vp), ("package_dist", _vp), ("pos_rew", _vp), ("ground_rew", _vp),
         ("on_the_ground", _vp),
         ("rewards", _vp * VMAS_SCN_MAX_AGENTS), ("obs", _vp * VMAS_SCN_MAX_AGENTS),
-        ("done", _vp),
+        ("done", _vp), ("pos_rew_prev", _vp),
     ]
 
 
@@ -340,6 +365,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_test_hold.argtypes = [_i32, _i32, ctypes.c_int64, _vp]
     lib.vmas_balance_outputs.restype = _i32
     lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_copy_spans.restype = _i32
+    lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_graph_launch.restype = _i32

@@ -27,7 +27,9 @@
 namespace {
 
 constexpr int kMaxRefsPerLaunch = 8;  // refs travel in the kernel arguments (16 flag bits)
-constexpr int kThreads = 256, kPerThread = 8, kMaxBlocksPerRef = 64;
+// (kPerThread 2 / up to 256 workgroups per ref: 8 per thread and 64 per ref left most CUs idle
+// and took 9.8 us per balance step in the kernel alone)
+constexpr int kThreads = 256, kPerThread = 2, kMaxBlocksPerRef = 256;
 
 struct ApplyArgs {
     VmasActionApplyRef r[kMaxRefsPerLaunch];
@@ -54,11 +56,11 @@ __host__ __device__ inline void apply_one(const VmasActionApplyRef& r, float* ou
 __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
     const int ref = blockIdx.y;
     const VmasActionApplyRef& r = a.r[ref];
-    const long n = (long)a.B * r.n_cols;
+    const int n = a.B * r.n_cols;  // (< 2^31: checked by the host)
     bool nan_seen = false, oor = false;
-    const long stride = (long)gridDim.x * kThreads;
-    for (long idx = (long)blockIdx.x * kThreads + threadIdx.x; idx < n; idx += stride) {
-        const int b = (int)(idx / r.n_cols), c = (int)(idx - (long)b * r.n_cols);
+    const int stride = (int)gridDim.x * kThreads;
+    for (int idx = (int)blockIdx.x * kThreads + (int)threadIdx.x; idx < n; idx += stride) {
+        const int b = idx / r.n_cols, c = idx - b * r.n_cols;
         apply_one(r, a.out, b, c, nan_seen, oor);
     }
     __shared__ uint32_t bits;
@@ -229,7 +231,7 @@ int32_t vmas_apply_actions_launch(int32_t device, int32_t batch, const VmasActio
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_launch: bad arguments");
     for (int i = 0; i < n_refs; ++i)
         if (!refs[i].u || !refs[i].u_range || !refs[i].u_mult || refs[i].n_phys > refs[i].n_cols ||
-            refs[i].n_phys < 0 || refs[i].out_offset < 0)
+            refs[i].n_phys < 0 || refs[i].out_offset < 0 || (long)batch * refs[i].n_cols > INT32_MAX)
             return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions_launch: bad ref %d", i);
     std::lock_guard<std::mutex> lk(g_mu);
     int cur = -1;
@@ -262,7 +264,7 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
     if (!refs || !out || !flags) return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions: null argument");
     for (int i = 0; i < n_refs; ++i)
         if (!refs[i].u || !refs[i].u_range || !refs[i].u_mult || refs[i].n_phys > refs[i].n_cols ||
-            refs[i].n_phys < 0 || refs[i].out_offset < 0)
+            refs[i].n_phys < 0 || refs[i].out_offset < 0 || (long)batch * refs[i].n_cols > INT32_MAX)
             return vmas_aux::fail(VMAS_E_INVALID, "vmas_apply_actions: bad ref %d", i);
     if (device < 0) {
         for (int i = 0; i < n_refs; ++i) {

@@ -58,6 +58,8 @@ import numpy as np
 import torch
 from torch import Tensor
 
+from ... import _native as N
+
 WARM_STEPS = 2  # eager steps before the capture (JIT compile, engine tables, allocator warm)
 
 
@@ -346,6 +348,8 @@ class StepGraph:
         self._segments: List[torch.cuda.CUDAGraph] = []  # one graph per stretch between host holes
         self._holes: List[Tuple[Any, tuple, Tensor]] = []  # (fn, args, output) run after segment i
         self._executed = None  # outputs of a capture step that already ran (segmented capture)
+        self._carry_ys: List[Tensor] = []  # the Y tensors as bound (version counters)
+        self._post: Optional[dict] = None  # what the last post-replay launch covered (_post_replay)
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -379,10 +383,11 @@ class StepGraph:
                 with torch.no_grad():
                     t.copy_(cur)
                 d[k] = t
-        if not self._first_replay:
+        if not self._first_replay and not self._carry_current():
+            self._post = None
             with torch.no_grad():
                 if self._carry_dst:
-                    torch._foreach_copy_(self._carry_dst, self._carry_src)
+                    N.copy_spans(self._dev_index(), list(zip(self._carry_dst, self._carry_src)), self._stream())
                 for x, y in self._carry_other:
                     x.copy_(y)
 
@@ -488,6 +493,7 @@ class StepGraph:
         self._out_tree = None
         self._out_tensors = []
         self._carry_dst, self._carry_src, self._watch = [], [], []
+        self._carry_ys, self._post = [], None
 
     # ---- capture --------------------------------------------------------------------------------
     def _capture(self) -> bool:
@@ -580,6 +586,7 @@ class StepGraph:
         self.why = ""
         self._first_replay = not segs.holes
         self._executed = out if segs.holes else None
+        self._post = None
         return True
 
     def _plan(self, objs, snap, out):
@@ -601,6 +608,7 @@ class StepGraph:
                     continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
                 carry.append((v0, v1))
                 names.append(f"{type(o).__name__}.{k}")
+        self._carry_ys = [y for _, y in carry]
         x_keys = {_storage_key(x): n for (x, _), n in zip(carry, names)}
         for (_, y), n in zip(carry, names):
             if _storage_key(y) in x_keys:
@@ -685,14 +693,13 @@ class StepGraph:
         self._first_replay = False
         self._launch()
         self.replays += 1
-        out = self._clone_outputs()
-        if asserts:
+        if asserts:  # (the post-replay carry overwrites X, which a rollback restores Y from)
             try:
                 self._asserts.after_replay(self.env.device)
             except AssertionError:
                 self._rollback(rng, restore_actions=False)
                 raise
-        return out
+        return self._post_replay()
 
     # ---- speculative replay ---------------------------------------------------------------------
     def backup(self, u_buf: Optional[Tensor]):
@@ -703,10 +710,15 @@ class StepGraph:
             self._bk_src = [*self._inplace] + ([u_buf] if u_buf is not None else [])
             self._bk_dst = [torch.empty_like(t) for t in self._bk_src]
             self._bk_u = u_buf
+            self._post = None
         n = len(self._bk_src) if u_buf is not None else len(self._inplace)
-        if n:
+        if n and not self._backup_current(n):
             with torch.no_grad():
-                torch._foreach_copy_(self._bk_dst[:n], self._bk_src[:n])
+                pairs = list(zip(self._bk_dst[:n], self._bk_src[:n]))
+                if all(d.is_contiguous() and s.is_contiguous() for d, s in pairs):
+                    N.copy_spans(self._dev_index(), pairs, self._stream())
+                else:
+                    torch._foreach_copy_(self._bk_dst[:n], self._bk_src[:n])
 
     def replay_speculative(self, flags_ok):
         """Replays the step while the action kernel's flags are still in flight, then waits for
@@ -722,7 +734,6 @@ class StepGraph:
         self._first_replay = False
         self._launch()
         self.replays += 1
-        out = self._clone_outputs()
         if not flags_ok():
             self._asserts.after_replay(dev, raise_=False)
             self._rollback(rng, restore_actions=True)
@@ -732,9 +743,11 @@ class StepGraph:
         except AssertionError:
             self._rollback(rng, restore_actions=False)
             raise
-        return out
+        # only now: the post-replay carry overwrites X, which a rollback restores Y from
+        return self._post_replay()
 
     def _rollback(self, rng: Tensor, restore_actions: bool):
+        self._post = None
         n = len(self._bk_src) if restore_actions else len(self._inplace)
         with torch.no_grad():
             if n:
@@ -744,6 +757,74 @@ class StepGraph:
             for x, y in self._carry_other:
                 y.copy_(x)
         torch.cuda.set_rng_state(rng, self.env.device)
+
+    # ---- copies after a replay -----------------------------------------------------------------
+    def _dev_index(self) -> int:
+        dev = torch.device(self.env.device)
+        return dev.index if dev.index is not None else torch.cuda.current_device()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self._dev_index()).cuda_stream)
+
+    def _carry_current(self) -> bool:
+        """The last post-replay launch carried Y -> X and no Y was modified since (version
+        counters: a native replay bumps none, a caller's in-place edit or the re-bind copy of
+        before_actions bumps them)."""
+        p = self._post
+        return p is not None and p["carry_ver"] == tuple(y._version for y in self._carry_ys)
+
+    def _backup_current(self, n: int) -> bool:
+        p = self._post
+        return (p is not None and p["bk_n"] >= n and self._carry_current()
+                and p["bk_ver"] == tuple(t._version for t in self._inplace))
+
+    def _post_spans(self):
+        """Per capture: the carry spans (Y -> X, contiguous byte views) and the backup spans of
+        the next step (in-place tensors and the action buffer -> their backups; a backup whose
+        tensor lies inside a carry destination X is taken from the matching bytes of Y, which
+        is what X holds once the carry has run).  None if a backup straddles a carry destination
+        or is not contiguous (then the backups stay in backup())."""
+        carry = [(y.data_ptr(), x.data_ptr(), x.numel()) for x, y in zip(self._carry_dst, self._carry_src)]
+        bk = []
+        n = len(self._bk_src) if self._bk_dst else 0
+        for t, d in zip(self._bk_src[:n], self._bk_dst[:n]):
+            if not (t.is_contiguous() and d.is_contiguous()):
+                return carry, None, 0
+            lo, nb = t.data_ptr(), t.numel() * t.element_size()
+            src = lo
+            for y, x, cn in carry:
+                if lo < x + cn and x < lo + nb:  # overlaps carry destination X
+                    if not (x <= lo and lo + nb <= x + cn):
+                        return carry, None, 0
+                    src = y + (lo - x)
+            bk.append((src, d.data_ptr(), nb))
+        return carry, bk, n
+
+    def _post_replay(self):
+        """After a replay, in ONE native launch (vmas_copy_spans): the fresh copies of the
+        outputs, the carry of the re-bound state to the next step (Y -> X, which before_actions
+        then skips while no Y changes) and the next step's backups (which backup() then skips
+        while no in-place tensor changes).  The outputs are copied before the carry when one
+        of them lies in a carry destination (two launches)."""
+        views, spans, rest = self._clone_prepare()
+        carry, bk, n_bk = self._post_spans()
+        out_ranges = [(s, nb) for s, _, nb in spans]
+        clash = any(lo < x + cn and x < lo + nb for lo, nb in out_ranges for _, x, cn in carry)
+        if self._carry_other or bk is None:  # non-contiguous carries / backups: the old order
+            N.copy_raw(self._dev_index(), spans, self._stream())
+            self._clone_finish(rest)
+            self._post = None
+        else:
+            if clash:
+                N.copy_raw(self._dev_index(), spans, self._stream())
+                N.copy_raw(self._dev_index(), carry + bk, self._stream())
+            else:
+                N.copy_raw(self._dev_index(), spans + carry + bk, self._stream())
+            self._clone_finish(rest)
+            self._post = {"carry_ver": tuple(y._version for y in self._carry_ys),
+                          "bk_ver": tuple(t._version for t in self._inplace), "bk_n": n_bk}
+        fn, consts = self._clone_build
+        return fn(views, consts)
 
     def _clone_plan(self):
         """Outputs grouped by (dtype, shape): per group one allocation [n, *shape] whose unbind
@@ -790,8 +871,9 @@ class StepGraph:
         fn = eval("lambda v, c: " + body)  # noqa: S307 -- generated from the output tree's structure only
         self._clone_build = (fn, consts)
 
-    def _clone_outputs(self):
-        """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
+    def _clone_prepare(self):
+        """Fresh output tensors and the spans that fill them: (views, contiguous spans as
+        (src_ptr, dst_ptr, nbytes), the non-contiguous (dst, src) rest)."""
         ts = self._out_tensors
         if getattr(self, "_clone_src_of", None) is not ts:
             self._clone_plan()
@@ -800,7 +882,24 @@ class StepGraph:
         views = ()
         for dt, shape, n in self._clone_groups:
             views += torch.empty((n,) + shape, dtype=dt, device=dev).unbind(0)
+        spans, rest = [], []
         for lo, hi, srcs in self._clone_spans:
-            torch._foreach_copy_(views[lo:hi], srcs)
+            for v, t in zip(views[lo:hi], srcs):
+                if t.is_contiguous():
+                    spans.append((t.data_ptr(), v.data_ptr(), t.numel() * t.element_size()))
+                else:
+                    rest.append((v, t))
+        return views, spans, rest
+
+    @staticmethod
+    def _clone_finish(rest):
+        for v, t in rest:
+            v.copy_(t)
+
+    def _clone_outputs(self):
+        """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
+        views, spans, rest = self._clone_prepare()
+        N.copy_raw(self._dev_index(), spans, self._stream())
+        self._clone_finish(rest)
         fn, consts = self._clone_build
         return fn(views, consts)
