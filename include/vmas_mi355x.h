@@ -437,7 +437,7 @@ int32_t vmas_jit_world_set_timing(VmasJitWorld* world, int32_t enable);
 int32_t vmas_jit_world_get_timing(VmasJitWorld* world, int32_t reset, double* total_ms,
                                   int64_t* launches);
 /* Device timer (timing on; batch-broadphase persistent launches): the kernel itself accumulates,
- * per step, the span from workgroup 0's start to the final fixed-point decision
+ * per step, the span from workgroup 0's start to the last workgroup's exit
  * (s_memrealtime, converted with the device's wall-clock rate);
  * *clock_ghz (may be NULL) is the in-kernel shader clock (s_memtime / s_memrealtime spans).  It also times launches replayed from a HIP graph, where HIP records
  * no events.  Waits for the device.  (bench.py's roofline timer; no reference counterpart.) */

@@ -33,7 +33,13 @@ def test_jit_parity_and_bit_identity_gpu(gpu_device, monkeypatch, name, kw, subs
     for rep in step_parity(env, n_steps=3):
         assert rep["ok"], rep
     assert env.world.engine.kernel_name == "k_world", env.world.engine.jit_error
-    # same state through the generic kernel: bit-identical
+    # same state through the generic kernel: bit-identical with exact math (the default relaxed
+    # math of jointless worlds is checked against the oracle above, at its tolerance)
+    monkeypatch.setenv("VMAS_JIT_MATH", "exact")
+    env = make(name, kw, substeps, gpu_device, num_envs=300, seed=4)
+    for _ in range(2):
+        env.step(env.get_random_actions())
+    assert env.world.engine.kernel_name == "k_world", env.world.engine.jit_error
     monkeypatch.setenv("VMAS_JIT", "0")
     ref = make(name, kw, substeps, gpu_device, num_envs=300, seed=4)
     snap = O.snapshot(env.world)

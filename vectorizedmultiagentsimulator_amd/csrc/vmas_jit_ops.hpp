@@ -93,8 +93,8 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 //     and steals them (normally none: every workgroup has started long before the first one
 //     finishes).
 //   * Processing a group ends with its R/Z activity row stored in blk[g] and one completion on a
-//     two-level counter (sub-counter g % 8, one 128-byte line each, then the top counter;
-//     cumulative over the passes of a step).  The workgroup whose completion is the last of the
+//     two-level counter (shard g % 32, one 128-byte line each, then the top counter; cumulative
+//     over the passes of a step).  The workgroup whose completion is the last of the
 //     pass is the DECIDER: it ORs the rows, applies the k_jit_flags_reduce test (was the mask a
 //     fixed point?), stores the next mask (inverted: zero means "all pairs active") and publishes
 //     dec[p] = 2 | continue.
@@ -117,13 +117,27 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 // pass: the earlier stores have completed (s_waitcnt) before the completion that precedes the
 // decision that precedes the re-run.
 //
-// ctl (uint32): [0] top completion counter, [2] passes run by the last step, [32 * (1 + k)]
-// completion sub-counter k, [32 * 9] exit counter, [32 * (10 + k)] claim sub-counter k,
-// [32 * 18 + p] dec[p] (p < kGridMaxPasses); then the mask words (nwords) and the claim words
-// (one per group).
-constexpr int kGridMaxPasses = 64;
-constexpr int kGridExit = 32 * 9, kGridClaimed = 32 * 10, kGridDec = 32 * 18;
+// ctl (uint32), every counter shard on a 128-byte line of its own (the adds of hundreds of
+// workgroups arriving together on one address serialise at the memory side: 32 shards):
+// [0] top completion counter, [1] top exit counter, [2] passes run by the last step,
+// [32 * (1 + k)] completion shard k (groups g % 32 == k, cumulative over the passes of a step),
+// [32 * (33 + k)] exit shard k (workgroups blockIdx % 32 == k), [32 * (65 + k)] claim shard k
+// (groups g % 8 == k), [32 * 73 + p] dec[p] (p < kGridMaxPasses); then the mask words (nwords)
+// and the claim words (one per group).
+constexpr int kGridMaxPasses = 64, kGridShards = 32;
+constexpr int kGridDone = 32, kGridExit = 32 * 33, kGridClaimed = 32 * 65, kGridDec = 32 * 73;
 constexpr int kGridCtlWords = kGridDec + kGridMaxPasses;
+
+// Two-level sharded arrival: add one to shard (i % kGridShards) of `base`; the arrival that
+// completes its shard adds one to the top counter; true for the arrival that completes the top
+// (n arrivals per round, `round` rounds so far including this one).  One thread.
+__device__ __forceinline__ bool sharded_arrive(uint32_t* shard0, uint32_t* top, uint32_t i, uint32_t n, uint32_t round) {
+    const uint32_t k = i % kGridShards, n_k = (n + kGridShards - 1u - k) / kGridShards;
+    const uint32_t n_top = n < (uint32_t)kGridShards ? n : (uint32_t)kGridShards;
+    if (__hip_atomic_fetch_add(&shard0[32 * k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != n_k * round - 1u)
+        return false;
+    return __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_top * round - 1u;
+}
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -148,11 +162,12 @@ __device__ __forceinline__ void st_out2(float* p, size_t i, V2 v) {
 }
 
 // Device timer (timing on, persistent launches): workgroup 0 stamps s_memrealtime into tm[0] at
-// its start; the decider of the final pass adds (now - tm[0]) to tm[2] and counts the launch in
-// tm[4].  Two stores per launch instead of per-workgroup atomics (measured: ~10 us on a
-// 512-workgroup launch).  The decider also adds its own s_memtime (shader clock) and
-// s_memrealtime (100 MHz-class wall clock) spans to tm[5] / tm[6]: their ratio is the in-kernel
-// shader clock (MI355X_MICROARCH.md, DVFS give-back item 6).
+// its start; the last workgroup to exit (grid_exit) adds (now - tm[0]) to tm[2] and counts the
+// launch in tm[4] -- the launch's span bar the dispatch of workgroup 0 and the completion signal.
+// Two stores per launch instead of per-workgroup atomics (measured: ~10 us on a 512-workgroup
+// launch).  The last workgroup also adds its own s_memtime (shader clock) and s_memrealtime
+// (100 MHz-class wall clock) spans to tm[5] / tm[6]: their ratio is the in-kernel shader clock
+// (MI355X_MICROARCH.md, DVFS give-back item 6).
 struct TimerStart {
     unsigned long long rt, sc;
 };
@@ -176,9 +191,10 @@ __device__ __forceinline__ void report_err(uint32_t* err, uint32_t* herr, uint32
 }
 
 // Claim group g for pass `pass` (one thread): claim[g] p -> p + 1, counted on the claim
-// sub-counter g % 8 (cumulative over the passes of a step).
+// sub-counter g % 8 (cumulative over the passes of a step).  A workgroup's own groups are
+// normally free: one compare-and-swap, no load first.
 __device__ __forceinline__ bool grid_claim(uint32_t* ctl, uint32_t* claim, int g, int pass) {
-    if (ld_agent(&claim[g]) != (uint32_t)pass || !cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) return false;
+    if (!cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) return false;
     (void)add_agent(&ctl[kGridClaimed + 32 * (g & 7)], 1u);
     return true;
 }
@@ -223,14 +239,8 @@ __device__ __forceinline__ int grid_steal(uint32_t* ctl, uint32_t* claim, int ng
 __device__ __forceinline__ bool grid_complete(uint32_t* ctl, int g, int ngrp, int pass, uint32_t* FLAG) {
     __builtin_amdgcn_s_waitcnt(0);  // this wave's stores have completed
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t k = (uint32_t)g & 7u, n_k = ((uint32_t)ngrp + 7u - k) / 8u;
-        const uint32_t n_sub = ngrp < 8 ? (uint32_t)ngrp : 8u;
-        bool last = false;
-        if (add_agent(&ctl[32 * (1 + k)], 1u) == n_k * (uint32_t)(pass + 1) - 1u)
-            last = add_agent(&ctl[0], 1u) == n_sub * (uint32_t)(pass + 1) - 1u;
-        *FLAG = last ? 1u : 0u;
-    }
+    if (threadIdx.x == 0)
+        *FLAG = sharded_arrive(&ctl[kGridDone], &ctl[0], (uint32_t)g, (uint32_t)ngrp, (uint32_t)(pass + 1)) ? 1u : 0u;
     __syncthreads();
     const bool last = *FLAG != 0u;
     __syncthreads();
@@ -242,8 +252,7 @@ __device__ __forceinline__ bool grid_complete(uint32_t* ctl, int g, int ngrp, in
 // step's outputs with NaN, so that the bad step is visible in its own results; the sticky error
 // bit also fails the next step).
 __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, uint32_t* ctl, uint32_t* err, uint32_t* herr,
-                                   int nwords, int ngrp, int pass, int max_pass, uint32_t* RED,
-                                   unsigned long long* tm, TimerStart t0s) {
+                                   int nwords, int ngrp, int pass, int max_pass, uint32_t* RED) {
     const int nw2 = 2 * nwords;
     for (int w = threadIdx.x; w < nw2 + 2; w += blockDim.x) RED[w] = 0u;
     __syncthreads();
@@ -288,17 +297,6 @@ __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, uint32_
         if (viol && !more) report_err(err, herr, kGridErrNoConverge);
         st_agent(&ctl[2], (uint32_t)(pass + 1));
         st_agent(&ctl[kGridDec + pass], more ? 3u : 2u);
-        if (!more && tm) {  // (thread 0 holds this workgroup's start stamps)
-            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-            const unsigned long long t0 = __hip_atomic_load(&tm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            (void)__hip_atomic_fetch_add(&tm[2], t1 > t0 ? t1 - t0 : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            (void)__hip_atomic_fetch_add(&tm[4], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c1 > t0s.sc && t1 > t0s.rt) {
-                (void)__hip_atomic_fetch_add(&tm[5], c1 - t0s.sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                (void)__hip_atomic_fetch_add(&tm[6], t1 - t0s.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
     }
     __syncthreads();
     return viol && !more;
@@ -377,30 +375,39 @@ __device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ct
 // pass did not converge (the caller poisons the outputs).  Not inlined (see grid_next).
 __device__ __attribute__((noinline)) bool grid_finish(int g, const uint32_t* FL, int nfl, uint32_t* blk, uint32_t* nmask,
                                                       uint32_t* ctl, uint32_t* err, uint32_t* herr, int nwords, int ngrp,
-                                                      int pass, int max_pass, uint32_t* RED, uint32_t* FLAG,
-                                                      unsigned long long* tm, TimerStart t0s) {
+                                                      int pass, int max_pass, uint32_t* RED, uint32_t* FLAG) {
     __syncthreads();
     for (int i = threadIdx.x; i < nfl; i += blockDim.x) st_agent(&blk[(size_t)g * nfl + i], FL[i]);
     return grid_complete(ctl, g, ngrp, pass, FLAG) &&
-           grid_decide(blk, nmask, ctl, err, herr, nwords, ngrp, pass, max_pass, RED, tm, t0s);
+           grid_decide(blk, nmask, ctl, err, herr, nwords, ngrp, pass, max_pass, RED);
 }
 
 // Exit (all threads): the last workgroup out resets the control words for the next step.
 __device__ __forceinline__ void grid_exit(uint32_t* ctl, uint32_t* nmask, uint32_t* claim, int nwords, int ngrp,
-                                          int max_pass, uint32_t* FLAG) {
+                                          int max_pass, uint32_t* FLAG, unsigned long long* tm, TimerStart t0s) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const bool last = add_agent(&ctl[kGridExit], 1u) == gridDim.x - 1u;
-        *FLAG = last ? 1u : 0u;
-    }
+    if (threadIdx.x == 0) *FLAG = sharded_arrive(&ctl[kGridExit], &ctl[1], blockIdx.x, gridDim.x, 1u) ? 1u : 0u;
     __syncthreads();
     if (*FLAG == 0u) return;
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
     for (int g = threadIdx.x; g < ngrp; g += blockDim.x) st_agent(&claim[g], 0u);
     for (int p = threadIdx.x; p < max_pass; p += blockDim.x) st_agent(&ctl[kGridDec + p], 0u);
-    if (threadIdx.x == 0) st_agent(&ctl[0], 0u);
-    if (threadIdx.x >= 1 && threadIdx.x <= 8) st_agent(&ctl[32 * threadIdx.x], 0u);
-    if (threadIdx.x >= 16 && threadIdx.x < 24) st_agent(&ctl[kGridClaimed + 32 * (threadIdx.x - 16)], 0u);
+    const int t = (int)threadIdx.x;
+    if (t < 2) st_agent(&ctl[t], 0u);
+    if (t >= 64 && t < 64 + kGridShards) st_agent(&ctl[kGridDone + 32 * (t - 64)], 0u);
+    if (t >= 128 && t < 128 + kGridShards) st_agent(&ctl[kGridExit + 32 * (t - 128)], 0u);
+    if (t >= 192 && t < 200) st_agent(&ctl[kGridClaimed + 32 * (t - 192)], 0u);
+    if (tm && t == 0) {  // the launch's span: workgroup 0's start -> the last workgroup out
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t0 = __hip_atomic_load(&tm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_fetch_add(&tm[2], t1 > t0 ? t1 - t0 : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_fetch_add(&tm[4], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c1 > t0s.sc && t1 > t0s.rt) {  // (thread 0 holds this workgroup's start stamps)
+            (void)__hip_atomic_fetch_add(&tm[5], c1 - t0s.sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            (void)__hip_atomic_fetch_add(&tm[6], t1 - t0s.rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (threadIdx.x == 9) st_agent(&ctl[kGridExit], 0u);
 }
 
