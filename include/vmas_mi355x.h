@@ -391,6 +391,41 @@ typedef struct VmasBalanceIO {
 } VmasBalanceIO;
 int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream);
 
+/* flocking (reference vmas/scenarios/flocking.py:149-206): replaces, for every policy agent at
+ * once, Scenario.reward (the first policy agent's `t += 1` and pairwise collision rewards over
+ * world.agents via get_distance, then per agent the mean squared distance error to every other
+ * agent, dist_rew and the re-bound distance_shaping) and Scenario.observation (pos, vel, pos -
+ * target pos and the agent's LIDAR, cast as World.cast_rays does).  Sphere agents and sphere LIDAR
+ * targets only (checked; the scenario keeps its torch program otherwise).
+ * Grid: one thread per (env, policy agent, part): the reward + observation head, or one LIDAR ray. */
+#define VMAS_SCN_MAX_RAY_TARGETS 16
+#define VMAS_FLOCK_MAX_AGENTS 16 /* the struct travels as kernel arguments (< 4 KiB) */
+typedef struct VmasFlockingIO {
+    int32_t batch, n_all, n_policy, what;
+    int32_t target, n_rays, n_ray_targets, sum_mode; /* target: index in agents[]; sum_mode: accumulators of
+                                                        the mean's sum order (vmas_scenarios.hip ordered_sum) */
+    float min_collision_distance, collision_reward, desired_distance, dist_shaping_factor;
+    float max_range, pad0;
+    int32_t collide_reward_on, pad1;       /* the scenario's `collision_reward != 0` */
+    VmasShapeRef agents[VMAS_FLOCK_MAX_AGENTS]; /* world.agents, in order (spheres) */
+    int32_t scripted[VMAS_FLOCK_MAX_AGENTS];    /* action_script is not None */
+    int32_t policy[VMAS_FLOCK_MAX_AGENTS];      /* world.policy_agents[p] = agents[policy[p]] */
+    VmasVec vel[VMAS_FLOCK_MAX_AGENTS];         /* [B,2] per policy agent */
+    VmasVec rot[VMAS_FLOCK_MAX_AGENTS];         /* [B,1] per policy agent: the LIDAR's angle offset */
+    const float* angles[VMAS_FLOCK_MAX_AGENTS]; /* [B, n_rays] per policy agent (Lidar._angles) */
+    int32_t ang_s0[VMAS_FLOCK_MAX_AGENTS], ang_s1[VMAS_FLOCK_MAX_AGENTS];
+    VmasRayTarget ray_targets[VMAS_SCN_MAX_RAY_TARGETS];
+    float* t;                                  /* [B] in place (REWARD: t += 1) */
+    const float* shaping_in[VMAS_FLOCK_MAX_AGENTS];  /* [B] contiguous per policy agent */
+    float* shaping_out[VMAS_FLOCK_MAX_AGENTS];   /* [B] fresh */
+    float* dist_rew[VMAS_FLOCK_MAX_AGENTS];      /* [B] fresh */
+    float* collision_rew[VMAS_FLOCK_MAX_AGENTS]; /* [B] in place */
+    float* rewards[VMAS_FLOCK_MAX_AGENTS];       /* [B] fresh */
+    float* obs[VMAS_FLOCK_MAX_AGENTS];           /* [B, 6 + n_rays] fresh (OBS) */
+    float* lidar[VMAS_FLOCK_MAX_AGENTS];         /* [B, n_rays] fresh (OBS): Lidar._last_measurement */
+} VmasFlockingIO;
+int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* stream);
+
 /* Device-to-device byte copies, all spans in one launch (csrc/vmas_copy.hip): graph mode's carried
  * state, output clones and per-step backups (simulator/environment/_graph.py; no reference
  * counterpart -- the reference returns fresh tensors from its eager ops).  Spans must not

@@ -23,6 +23,8 @@ def test_fused_programs_off_on_cpu_worlds():
 # (scenario, kwargs, substeps, scenario attributes the program leaves behind)
 FUSED = [
     ("balance", dict(n_agents=4), 10, ["on_the_ground", "package_dist", "ground_rew", "pos_rew", "global_shaping"]),
+    ("flocking", dict(n_agents=5), None, ["t", "agent.dist_rew", "agent.distance_shaping", "agent.collision_rew",
+                                          "agent.sensors.0._last_measurement"]),
 ]
 
 
@@ -38,7 +40,17 @@ class _Torch:
 
 
 def _attrs(env, names):
-    return [getattr(env.scenario, n) for n in names]
+    out = []
+    for n in names:
+        if n.startswith("agent."):  # per policy agent; dotted path, integer parts index lists
+            for a in env.world.policy_agents:
+                v = a
+                for part in n.split(".")[1:]:
+                    v = v[int(part)] if part.isdigit() else getattr(v, part)
+                out.append(v)
+        else:
+            out.append(getattr(env.scenario, n))
+    return out
 
 
 @pytest.mark.gpu
@@ -101,3 +113,11 @@ def test_fused_balance_cache_follows_state_changes_gpu(gpu_device):
     r0b = sc.reward(w.agents[2])
     assert torch.equal(r0, r0b) and r0.data_ptr() != r0b.data_ptr()
     assert torch.equal(sc.done(), sc.on_the_ground + w.is_overlapping(sc.package, sc.package.goal))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [3, 4, 7, 8, 12])
+def test_reduce_order_probe_finds_torch_mean_order_gpu(gpu_device, n):
+    """The fused kernels' mean over n contiguous values reproduces torch's .mean(-1) on the device
+    bit for bit in one of the ordered_sum modes (else the scenario would keep its torch program)."""
+    assert _fused.reduce_order(torch.device(gpu_device), n) is not None

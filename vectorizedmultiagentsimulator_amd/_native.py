@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "vmas_test_hold",
     "vmas_balance_outputs",
     "vmas_copy_spans",
+    "vmas_flocking_outputs",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -255,6 +256,33 @@ class VmasBalanceIO(ctypes.Structure):
     ]
 
 
+class VmasRayTarget(ctypes.Structure):
+    _fields_ = [("shape", _i32), ("radius", _f32), ("length", _f32), ("width", _f32), ("pos", _vp), ("rot", _vp),
+                ("pos_s0", _i32), ("pos_s1", _i32), ("rot_s0", _i32), ("pad", _i32)]
+
+
+VMAS_SCN_MAX_RAY_TARGETS = 16
+VMAS_FLOCK_MAX_AGENTS = 16
+_FA = VMAS_FLOCK_MAX_AGENTS
+
+
+class VmasFlockingIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", _i32), ("n_all", _i32), ("n_policy", _i32), ("what", _i32),
+        ("target", _i32), ("n_rays", _i32), ("n_ray_targets", _i32), ("sum_mode", _i32),
+        ("min_collision_distance", _f32), ("collision_reward", _f32), ("desired_distance", _f32),
+        ("dist_shaping_factor", _f32), ("max_range", _f32), ("pad0", _f32),
+        ("collide_reward_on", _i32), ("pad1", _i32),
+        ("agents", VmasShapeRef * _FA), ("scripted", _i32 * _FA), ("policy", _i32 * _FA),
+        ("vel", VmasVec * _FA), ("rot", VmasVec * _FA), ("angles", _vp * _FA),
+        ("ang_s0", _i32 * _FA), ("ang_s1", _i32 * _FA),
+        ("ray_targets", VmasRayTarget * VMAS_SCN_MAX_RAY_TARGETS),
+        ("t", _vp),
+        ("shaping_in", _vp * _FA), ("shaping_out", _vp * _FA), ("dist_rew", _vp * _FA),
+        ("collision_rew", _vp * _FA), ("rewards", _vp * _FA), ("obs", _vp * _FA), ("lidar", _vp * _FA),
+    ]
+
+
 # Per-call pointer tables are built as numpy structured arrays (one row per entity/agent/joint);
 # their layouts must match VmasEntityIO / VmasAgentIO / VmasJointIO / VmasRayTarget.
 ENTITY_IO_DTYPE = np.dtype(
@@ -332,7 +360,7 @@ assert ACTION_APPLY_REF_DTYPE.itemsize == 56
 assert ENTITY_IO_DTYPE.itemsize == 72
 assert AGENT_IO_DTYPE.itemsize == 32
 assert JOINT_IO_DTYPE.itemsize == 16
-assert RAY_TARGET_DTYPE.itemsize == 48
+assert RAY_TARGET_DTYPE.itemsize == 48 and ctypes.sizeof(VmasRayTarget) == 48
 assert ctypes.sizeof(VmasEntityDesc) == 84
 assert ctypes.sizeof(VmasShapeRef) == 56
 
@@ -365,6 +393,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_test_hold.argtypes = [_i32, _i32, ctypes.c_int64, _vp]
     lib.vmas_balance_outputs.restype = _i32
     lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_flocking_outputs.restype = _i32
+    lib.vmas_flocking_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_copy_spans.restype = _i32
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_stream_abort_capture.restype = _i32

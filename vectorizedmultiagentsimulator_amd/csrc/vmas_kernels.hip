@@ -890,26 +890,6 @@ struct RayK {
     float* out;
 };
 
-__host__ __device__ __forceinline__ float cast_one(const VmasRayTarget* tg, int nt, V2 o, float ang,
-                                                   int b, float max_range) {
-    const float dc = cosf(ang), ds = sinf(ang);
-    float best = max_range;
-    for (int t = 0; t < nt; ++t) {
-        const VmasRayTarget& x = tg[t];
-        const V2 tp = mk(x.pos[(long)b * x.pos_s0], x.pos[(long)b * x.pos_s0 + x.pos_s1]);
-        float d;
-        if (x.shape == VMAS_SPHERE) {
-            d = ray_sphere(o, dc, ds, tp, x.radius, max_range);
-        } else if (x.shape == VMAS_BOX) {
-            d = ray_box(o, ang, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, x.width, max_range);
-        } else {
-            d = ray_line(o, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, max_range);
-        }
-        best = tmin(best, d);
-    }
-    return best;
-}
-
 __global__ void __launch_bounds__(256) k_cast_rays(RayK k) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (long)k.B * k.R) return;

@@ -76,5 +76,27 @@ __host__ __device__ __forceinline__ void store_query(void* out, int kind, int b,
     else reinterpret_cast<float*>(out)[b] = v;
 }
 
+// World.cast_rays of one (env, ray) (core.py:1661-1785): min over the targets of the ray-shape
+// distances, from max_range.  Shared by k_cast_rays (vmas_kernels.hip) and the fused scenario
+// kernels (vmas_scenarios.hip).
+__host__ __device__ __forceinline__ float cast_one(const VmasRayTarget* tg, int nt, V2 o, float ang,
+                                                   int b, float max_range) {
+    const float dc = cosf(ang), ds = sinf(ang);
+    float best = max_range;
+    for (int t = 0; t < nt; ++t) {
+        const VmasRayTarget& x = tg[t];
+        const V2 tp = mk(x.pos[(long)b * x.pos_s0], x.pos[(long)b * x.pos_s0 + x.pos_s1]);
+        float d;
+        if (x.shape == VMAS_SPHERE) {
+            d = ray_sphere(o, dc, ds, tp, x.radius, max_range);
+        } else if (x.shape == VMAS_BOX) {
+            d = ray_box(o, ang, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, x.width, max_range);
+        } else {
+            d = ray_line(o, dc, ds, tp, x.rot[(long)b * x.rot_s0], x.length, max_range);
+        }
+        best = tmin(best, d);
+    }
+    return best;
+}
 
 }  // namespace vmas

@@ -6,11 +6,14 @@ Workload of BASELINE config C5.  Restates vmas/scenarios/flocking.py:18-206.  Th
 Agent driven by an action script (a circle); each policy agent has a 12-ray LIDAR that sees the
 non-agent entities (the obstacles).
 """
+import ctypes
 from typing import Dict
 
 import torch
 from torch import Tensor
 
+from vectorizedmultiagentsimulator_amd import _native as N
+from vectorizedmultiagentsimulator_amd.simulator import _fused
 from vectorizedmultiagentsimulator_amd.simulator.core import Agent, Landmark, Sphere, World
 from vectorizedmultiagentsimulator_amd.simulator.heuristic_policy import BaseHeuristicPolicy
 from vectorizedmultiagentsimulator_amd.simulator.scenario import BaseScenario
@@ -97,6 +100,11 @@ class Scenario(BaseScenario):
             self.t[env_index] = 0
 
     def reward(self, agent: Agent):
+        if _fused.enabled(self.world) and self._fused_plan() is not None:
+            return self._fused_reward(agent)
+        return self._torch_reward(agent)
+
+    def _torch_reward(self, agent: Agent):
         w = self.world
         if w.policy_agents.index(agent) == 0:
             self.t += 1
@@ -119,6 +127,8 @@ class Scenario(BaseScenario):
         return agent.collision_rew + agent.dist_rew
 
     def observation(self, agent: Agent):
+        if _fused.enabled(self.world) and self._fused_plan() is not None:
+            return self._fused_observation(agent)
         return torch.cat(
             [agent.state.pos, agent.state.vel, agent.state.pos - self._target.state.pos,
              agent.sensors[0].measure()],
@@ -127,6 +137,172 @@ class Scenario(BaseScenario):
 
     def info(self, agent: Agent) -> Dict[str, Tensor]:
         return {"agent_collision_rew": agent.collision_rew, "agent_distance_rew": agent.dist_rew}
+
+    # ---- fused program (GPU worlds; csrc/vmas_scenarios.hip k_flocking) ------------------------
+    # The first policy agent's reward call runs ONE launch, a thread per (env, policy agent): the
+    # reward block above for every policy agent (t += 1, the pairwise collision rewards, the
+    # separation term, dist_rew / distance_shaping, the reward) and every policy agent's
+    # observation with its LIDAR.  Each agent's own reward call then re-binds its dist_rew /
+    # distance_shaping and returns its reward, its observation call returns its observation and
+    # sets its sensor's last measurement -- while the inputs are unchanged (_fused.state_key);
+    # otherwise the call recomputes, as the reference does on every call.
+
+    def _fused_plan(self):
+        w = self.world
+        agents, pol = w.agents, w.policy_agents
+        sig = (tuple(id(a) for a in agents), tuple(id(e) for e in w.entities), w.batch_dim)
+        plan = getattr(self, "_fplan", None)
+        if plan is not None and plan[0] == sig:
+            return plan[1]
+        info = None
+        dev = torch.device(w.device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        ok = (2 <= len(agents) <= N.VMAS_FLOCK_MAX_AGENTS and len(pol) >= 1 and self._target in agents
+              and all(type(a.shape).__name__ == "Sphere" for a in agents))
+        if ok:
+            tgts, R = None, None
+            for a in pol:
+                if not a.sensors or type(a.sensors[0]).__name__ != "Lidar":
+                    ok = False
+                    break
+                s = a.sensors[0]
+                ts = [e for e in w.entities if e is not a and s.entity_filter(e)]
+                if tgts is None:
+                    tgts, R = ts, s._angles.shape[-1]
+                if ([id(e) for e in ts] != [id(e) for e in tgts] or s._angles.shape != (w.batch_dim, R)
+                        or len(ts) > N.VMAS_SCN_MAX_RAY_TARGETS
+                        or any(type(e.shape).__name__ != "Sphere" for e in ts)):
+                    ok = False
+                    break
+                for e in ts:
+                    assert e.collides(a) and a.collides(e), "Rays are only casted among collidables"
+        mode = _fused.reduce_order(dev, len(agents) - 1) if ok else None
+        if ok and mode is not None:
+            info = {"dev": dev, "targets": tgts, "R": R, "mode": mode,
+                    "policy": [agents.index(a) for a in pol]}
+        self._fplan = (sig, info)
+        return info
+
+    def _fused_inputs(self):
+        w = self.world
+        ts = [a.state.pos for a in w.agents]
+        for a in w.policy_agents:
+            s = a.sensors[0]
+            ts += [a.state.vel, a.state.rot, s._angles]
+        ts += [e.state.pos for e in self._fplan[1]["targets"]]
+        ts += [e.state.rot for e in self._fplan[1]["targets"]]
+        return ts
+
+    def _run_fused(self, what: int):
+        w = self.world
+        plan = self._fused_plan()
+        dev = plan["dev"]
+        B = w.batch_dim
+        agents, pol = w.agents, w.policy_agents
+        keep = []
+        io = N.VmasFlockingIO()
+        io.batch, io.n_all, io.n_policy, io.what = B, len(agents), len(pol), what
+        io.target, io.n_rays, io.n_ray_targets, io.sum_mode = agents.index(self._target), plan["R"], len(plan["targets"]), plan["mode"]
+        io.min_collision_distance = float(self.min_collision_distance)
+        io.collision_reward = float(self.collision_reward)
+        io.desired_distance = float(self.desired_distance)
+        io.dist_shaping_factor = float(self.dist_shaping_factor)
+        io.collide_reward_on = 1 if self.collision_reward != 0 else 0
+        io.max_range = float(pol[0].sensors[0]._max_range)
+        for i, a in enumerate(agents):
+            io.agents[i] = _fused.ref(w, a, keep, 0)
+            io.scripted[i] = 0 if a.action_script is None else 1
+        for i, e in enumerate(plan["targets"]):
+            io.ray_targets[i] = _fused.ray_target(w, e, keep, dev)
+        out = {}
+        if what & N.VMAS_SCN_REWARD:
+            t = self.t
+            if t.dtype is not torch.float32 or not t.is_contiguous() or t.device != dev:
+                raise _NotFusable
+            io.t = t.data_ptr()
+            for k in ("shaping", "dist_rew", "rewards"):
+                out[k] = [torch.empty(B, device=dev, dtype=torch.float32) for _ in pol]
+        if what & N.VMAS_SCN_OBS:
+            R = plan["R"]
+            out["obs"] = [torch.empty(B, 6 + R, device=dev, dtype=torch.float32) for _ in pol]
+            out["lidar"] = [torch.empty(B, R, device=dev, dtype=torch.float32) for _ in pol]
+        for p, a in enumerate(pol):
+            io.policy[p] = plan["policy"][p]
+            if what & N.VMAS_SCN_REWARD:
+                sh, cr = a.distance_shaping, a.collision_rew
+                for x in (sh, cr):
+                    if x.dtype is not torch.float32 or not x.is_contiguous() or x.shape != (B,) or x.device != dev:
+                        raise _NotFusable
+                keep.append(sh)
+                io.shaping_in[p], io.collision_rew[p] = sh.data_ptr(), cr.data_ptr()
+                io.shaping_out[p] = out["shaping"][p].data_ptr()
+                io.dist_rew[p] = out["dist_rew"][p].data_ptr()
+                io.rewards[p] = out["rewards"][p].data_ptr()
+            if what & N.VMAS_SCN_OBS:
+                s = a.sensors[0]
+                io.vel[p] = _fused.vec(_fused.f32(a.state.vel, dev), keep)
+                io.rot[p] = _fused.vec(_fused.f32(a.state.rot, dev), keep)
+                ang = _fused.f32(s._angles, dev)
+                keep.append(ang)
+                io.angles[p], io.ang_s0[p], io.ang_s1[p] = ang.data_ptr(), ang.stride(0), ang.stride(1)
+                io.obs[p] = out["obs"][p].data_ptr()
+                io.lidar[p] = out["lidar"][p].data_ptr()
+        _fused.check(_fused.lib().vmas_flocking_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
+                     "vmas_flocking_outputs")
+        if what & N.VMAS_SCN_REWARD:
+            _fused.bump_version(self.t)
+            if io.collide_reward_on:
+                for a in pol:
+                    _fused.bump_version(a.collision_rew)
+        return out
+
+    def _fused_reward(self, agent: Agent):
+        w = self.world
+        pol = w.policy_agents
+        p = pol.index(agent)
+        if p == 0:
+            try:
+                out = self._run_fused(N.VMAS_SCN_REWARD | N.VMAS_SCN_OBS)
+            except _NotFusable:
+                self._fc = None
+                return self._torch_reward(agent)
+            self._fc = {
+                "key": _fused.state_key(self._fused_inputs()),
+                "rew": {i: (out["shaping"][i], out["dist_rew"][i], out["rewards"][i],
+                            _fused.state_key([a.distance_shaping, a.collision_rew])) for i, a in enumerate(pol)},
+                "obs": {i: (out["obs"][i], out["lidar"][i]) for i in range(len(pol))},
+            }
+        c = getattr(self, "_fc", None)
+        if c is not None and p in c["rew"]:
+            sh, dr, r, k = c["rew"][p]
+            if k == _fused.state_key([agent.distance_shaping, agent.collision_rew]) and c["key"] == _fused.state_key(
+                    self._fused_inputs()):
+                del c["rew"][p]
+                agent.dist_rew = dr
+                agent.distance_shaping = sh
+                return r
+        c = self._fc = None if c is None else {**c, "rew": {}}
+        return self._torch_reward(agent)
+
+    def _fused_observation(self, agent: Agent):
+        p = self.world.policy_agents.index(agent)
+        c = getattr(self, "_fc", None)
+        if c is None or p not in c["obs"] or c["key"] != _fused.state_key(self._fused_inputs()):
+            try:
+                out = self._run_fused(N.VMAS_SCN_OBS)
+            except _NotFusable:
+                return torch.cat([agent.state.pos, agent.state.vel, agent.state.pos - self._target.state.pos,
+                                  agent.sensors[0].measure()], dim=-1)
+            c = self._fc = {"key": _fused.state_key(self._fused_inputs()), "rew": {},
+                            "obs": {i: (out["obs"][i], out["lidar"][i]) for i in range(len(out["obs"]))}}
+        o, lid = c["obs"].pop(p)
+        agent.sensors[0]._last_measurement = lid
+        return o
+
+
+class _NotFusable(Exception):
+    """An operand the fused kernel does not take (dtype / layout / device): the torch program runs."""
 
 
 class HeuristicPolicy(BaseHeuristicPolicy):

@@ -73,6 +73,66 @@ def bump_version(t: torch.Tensor) -> None:
     torch.autograd.graph.increment_version(t)
 
 
+_ORDER_CACHE = {}
+
+
+def reduce_order(dev: torch.device, n: int):
+    """The summation order of torch's .mean(-1) over a contiguous [B, n] fp32 tensor on this
+    device, as the accumulator count of the fused kernels' ordered_sum (vmas_scenarios.hip):
+    acc strided accumulators combined by an adjacent-pair tree.  Probed once per (device, n)
+    against torch itself on random values of mixed magnitude (tools/probe_mean_order.py: on
+    MI355X / ROCm 7.2 the largest power of two <= n); None if no count reproduces it bit for
+    bit (the scenario then keeps its torch program)."""
+    key = (str(dev), n)
+    if key in _ORDER_CACHE:
+        return _ORDER_CACHE[key]
+    g = torch.Generator(device="cpu").manual_seed(1234 + n)
+    x = (torch.rand(4096, n, generator=g) * torch.exp2(torch.randint(-12, 12, (4096, n), generator=g).float()))
+    x = x.to(dev).contiguous()
+    ref = x.mean(-1)
+    cols = [x[:, i] for i in range(n)]
+    found = None
+    acc = 1
+    while acc <= min(n, N.VMAS_FLOCK_MAX_AGENTS):
+        y = []
+        for i in range(acc):
+            a = cols[i]
+            for j in range(i + acc, n, acc):
+                a = a + cols[j]
+            y.append(a)
+        w = 1
+        while w < len(y):
+            for i in range(0, len(y) - w, 2 * w):
+                y[i] = y[i] + y[i + w]
+            w *= 2
+        if torch.equal(y[0] * (1.0 / n), ref):
+            found = acc
+            break
+        acc *= 2
+    _ORDER_CACHE[key] = found
+    return found
+
+
+def ray_target(world, e, keep: list, dev) -> "N.VmasRayTarget":
+    """An entity as a VmasRayTarget (shape + state pointers), as World.cast_rays tables it."""
+    from ._engine import _f32, _shape_code, _shape_dims
+
+    code = _shape_code(e.shape)
+    dims = _shape_dims(e.shape, code)
+    r = N.VmasRayTarget()
+    r.shape = code
+    if code == N.VMAS_SPHERE:
+        r.radius = _f32(dims[0])
+    else:
+        r.length = _f32(dims[0])
+        r.width = _f32(dims[1]) if code == N.VMAS_BOX else 0.0
+    p, rot = f32(e.state.pos, dev), f32(e.state.rot, dev)
+    keep += [p, rot]
+    r.pos, r.rot = p.data_ptr(), rot.data_ptr()
+    r.pos_s0, r.pos_s1, r.rot_s0 = p.stride(0), p.stride(1), rot.stride(0)
+    return r
+
+
 def check(rc: int, what: str) -> None:
     N.check_aux(rc, what)
 

@@ -72,6 +72,8 @@ def _tracked_objects(env) -> List[Any]:
         a = getattr(e, "_action", None)
         if a is not None:
             objs.append(a)
+        for sensor in getattr(e, "_sensors", None) or ():  # Lidar._last_measurement is re-bound per step
+            objs.append(sensor)
     for jc in w._joints.values():
         objs.append(jc)
     seen = set()
