@@ -426,6 +426,80 @@ typedef struct VmasFlockingIO {
 } VmasFlockingIO;
 int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* stream);
 
+/* transport (reference vmas/scenarios/transport.py:130-190): replaces Scenario.reward (for the
+ * first agent: per package dist_to_goal, on_goal = is_overlapping(package, goal), the colour,
+ * the shaping reward and the re-bound global_shaping; the shared rew), Scenario.observation
+ * (pos, vel, then per package: package - goal, package - agent, package vel, on_goal) and
+ * Scenario.done.  Grid: one thread per (env, part): part 0 the reward + done, 1 + i agent i's
+ * observation. */
+#define VMAS_TRANSPORT_MAX_PACKAGES 8
+#define VMAS_TRANSPORT_MAX_AGENTS 16
+typedef struct VmasTransportIO {
+    int32_t batch, n_agents, n_packages, what;
+    float shaping_factor, red[3], green[3], pad0;
+    VmasShapeRef package[VMAS_TRANSPORT_MAX_PACKAGES], goal[VMAS_TRANSPORT_MAX_PACKAGES];
+    VmasVec package_vel[VMAS_TRANSPORT_MAX_PACKAGES];
+    VmasVec agent_pos[VMAS_TRANSPORT_MAX_AGENTS], agent_vel[VMAS_TRANSPORT_MAX_AGENTS];
+    const float* global_shaping[VMAS_TRANSPORT_MAX_PACKAGES]; /* [B] (stride gs_s0) in */
+    int32_t gs_s0[VMAS_TRANSPORT_MAX_PACKAGES];
+    float* global_shaping_out[VMAS_TRANSPORT_MAX_PACKAGES];   /* [B] fresh (REWARD) */
+    float* dist_to_goal[VMAS_TRANSPORT_MAX_PACKAGES];         /* [B] fresh (REWARD) */
+    uint8_t* on_goal[VMAS_TRANSPORT_MAX_PACKAGES];            /* [B] torch.bool fresh (REWARD) */
+    float* color[VMAS_TRANSPORT_MAX_PACKAGES];                /* [B, 3] fresh (REWARD) */
+    const uint8_t* on_goal_in[VMAS_TRANSPORT_MAX_PACKAGES];   /* [B] the attribute (OBS / DONE
+                                                                 without REWARD) */
+    float* rew;                                               /* [B] fresh (REWARD) */
+    float* obs[VMAS_TRANSPORT_MAX_AGENTS];                    /* [B, 4 + 7 n_packages] (OBS) */
+    uint8_t* done;                                            /* [B] torch.bool (DONE) */
+} VmasTransportIO;
+int32_t vmas_transport_outputs(int32_t device, const VmasTransportIO* io, void* stream);
+
+/* discovery (reference vmas/scenarios/discovery.py:146-246), two launches per step:
+ *   REWARD (the first agent's reward call): agents_pos / targets_pos stacks, the torch.cdist
+ *     agent-target distances, agents_per_target (int64), covered_targets, every agent's
+ *     covering_reward (in place), the shared covering reward (in place, halved where nonzero),
+ *     time_rew and every agent's reward (collision_rew + covering + time_rew; the agent
+ *     collision penalty must be 0: the scenario checks);
+ *   OBS (the first observation call, after the last agent's reward has respawned the targets):
+ *     every agent's observation (pos, vel, then each LIDAR, cast as World.cast_rays does).
+ * Entities are spheres (checked): a compact table in world.entities order; each LIDAR sees the
+ * table entries of its mask but never its own agent.  Grid: REWARD one thread per env; OBS one
+ * thread per (env, agent, part): part 0 the pos / vel head, then one per LIDAR ray. */
+#define VMAS_DISC_MAX_AGENTS 16
+#define VMAS_DISC_MAX_TARGETS 16
+#define VMAS_DISC_MAX_ENTITIES 32
+#define VMAS_DISC_MAX_LIDARS 2
+typedef struct VmasDiscoveryIO {
+    int32_t batch, n_agents, n_targets, what;
+    float covering_range, covering_rew_coeff, time_penalty;
+    int32_t agents_per_target, shared_reward, n_entities, n_lidars;
+    int32_t time_int;             /* time_rew is int64 (torch.full of a python int), value time_penalty_i */
+    int64_t time_penalty_i;
+    int32_t agent_entity[VMAS_DISC_MAX_AGENTS];  /* table index of agent i */
+    int32_t target_entity[VMAS_DISC_MAX_TARGETS]; /* table index of target j (scenario order) */
+    VmasVec pos[VMAS_DISC_MAX_ENTITIES];          /* entity table: [B,2] positions */
+    float radius[VMAS_DISC_MAX_ENTITIES];
+    VmasVec vel[VMAS_DISC_MAX_AGENTS], rot[VMAS_DISC_MAX_AGENTS];
+    int32_t n_rays[VMAS_DISC_MAX_LIDARS];
+    float max_range[VMAS_DISC_MAX_LIDARS];
+    uint32_t mask[VMAS_DISC_MAX_LIDARS];          /* entity-table bits each LIDAR sees */
+    const float* angles[VMAS_DISC_MAX_LIDARS][VMAS_DISC_MAX_AGENTS]; /* [B, n_rays] */
+    int32_t ang_s0[VMAS_DISC_MAX_LIDARS][VMAS_DISC_MAX_AGENTS], ang_s1[VMAS_DISC_MAX_LIDARS][VMAS_DISC_MAX_AGENTS];
+    float* lidar[VMAS_DISC_MAX_LIDARS][VMAS_DISC_MAX_AGENTS];        /* [B, n_rays] fresh (OBS) */
+    float* obs[VMAS_DISC_MAX_AGENTS];             /* [B, 4 + sum n_rays] fresh (OBS) */
+    float* agents_pos;                            /* [B, A, 2] fresh (REWARD) */
+    float* targets_pos;                           /* [B, T, 2] fresh */
+    float* dists;                                 /* [B, A, T] fresh */
+    int64_t* per_target;                          /* [B, T] fresh */
+    uint8_t* covered;                             /* [B, T] torch.bool fresh */
+    void* time_rew;                               /* [B] fresh: float32, or int64 when time_int */
+    float* shared;                                /* [B] in place */
+    float* covering[VMAS_DISC_MAX_AGENTS];        /* [B] in place */
+    float* collision[VMAS_DISC_MAX_AGENTS];       /* [B] in place (zeroed) */
+    float* rewards[VMAS_DISC_MAX_AGENTS];         /* [B] fresh */
+} VmasDiscoveryIO;
+int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream);
+
 /* Device-to-device byte copies, all spans in one launch (csrc/vmas_copy.hip): graph mode's carried
  * state, output clones and per-step backups (simulator/environment/_graph.py; no reference
  * counterpart -- the reference returns fresh tensors from its eager ops).  Spans must not

@@ -23,6 +23,12 @@ def test_fused_programs_off_on_cpu_worlds():
 # (scenario, kwargs, substeps, scenario attributes the program leaves behind)
 FUSED = [
     ("balance", dict(n_agents=4), 10, ["on_the_ground", "package_dist", "ground_rew", "pos_rew", "global_shaping"]),
+    ("transport", dict(n_agents=4), None, ["rew", "package.dist_to_goal", "package.on_goal", "package.color",
+                                           "package.global_shaping"]),
+    ("discovery", dict(n_agents=5, use_agent_lidar=True), None,
+     ["time_rew", "agents_pos", "targets_pos", "agents_targets_dists", "agents_per_target", "covered_targets",
+      "shared_covering_rew", "agent.covering_reward", "agent.collision_rew", "agent.sensors.0._last_measurement",
+      "agent.sensors.1._last_measurement", "target_pos"]),
     ("flocking", dict(n_agents=5), None, ["t", "agent.dist_rew", "agent.distance_shaping", "agent.collision_rew",
                                           "agent.sensors.0._last_measurement"]),
 ]
@@ -42,7 +48,11 @@ class _Torch:
 def _attrs(env, names):
     out = []
     for n in names:
-        if n.startswith("agent."):  # per policy agent; dotted path, integer parts index lists
+        if n == "target_pos":
+            out += [t.state.pos for t in env.scenario._targets]
+        elif n.startswith("package."):
+            out += [getattr(p, n.split(".", 1)[1]) for p in env.scenario.packages]
+        elif n.startswith("agent."):  # per (policy) agent; dotted path, integer parts index lists
             for a in env.world.policy_agents:
                 v = a
                 for part in n.split(".")[1:]:

@@ -58,6 +58,8 @@ EXPORTED_SYMBOLS = (
     "vmas_balance_outputs",
     "vmas_copy_spans",
     "vmas_flocking_outputs",
+    "vmas_transport_outputs",
+    "vmas_discovery_outputs",
     "vmas_world_create",
     "vmas_world_destroy",
     "vmas_world_step",
@@ -283,6 +285,44 @@ class VmasFlockingIO(ctypes.Structure):
     ]
 
 
+VMAS_TRANSPORT_MAX_PACKAGES = 8
+VMAS_TRANSPORT_MAX_AGENTS = 16
+_TP, _TA = VMAS_TRANSPORT_MAX_PACKAGES, VMAS_TRANSPORT_MAX_AGENTS
+
+
+class VmasTransportIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", _i32), ("n_agents", _i32), ("n_packages", _i32), ("what", _i32),
+        ("shaping_factor", _f32), ("red", _f32 * 3), ("green", _f32 * 3), ("pad0", _f32),
+        ("package", VmasShapeRef * _TP), ("goal", VmasShapeRef * _TP), ("package_vel", VmasVec * _TP),
+        ("agent_pos", VmasVec * _TA), ("agent_vel", VmasVec * _TA),
+        ("global_shaping", _vp * _TP), ("gs_s0", _i32 * _TP), ("global_shaping_out", _vp * _TP),
+        ("dist_to_goal", _vp * _TP), ("on_goal", _vp * _TP), ("color", _vp * _TP), ("on_goal_in", _vp * _TP),
+        ("rew", _vp), ("obs", _vp * _TA), ("done", _vp),
+    ]
+
+
+VMAS_DISC_MAX_AGENTS, VMAS_DISC_MAX_TARGETS, VMAS_DISC_MAX_ENTITIES, VMAS_DISC_MAX_LIDARS = 16, 16, 32, 2
+_DA, _DT, _DE, _DL = VMAS_DISC_MAX_AGENTS, VMAS_DISC_MAX_TARGETS, VMAS_DISC_MAX_ENTITIES, VMAS_DISC_MAX_LIDARS
+
+
+class VmasDiscoveryIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", _i32), ("n_agents", _i32), ("n_targets", _i32), ("what", _i32),
+        ("covering_range", _f32), ("covering_rew_coeff", _f32), ("time_penalty", _f32),
+        ("agents_per_target", _i32), ("shared_reward", _i32), ("n_entities", _i32), ("n_lidars", _i32),
+        ("time_int", _i32), ("time_penalty_i", ctypes.c_int64),
+        ("agent_entity", _i32 * _DA), ("target_entity", _i32 * _DT),
+        ("pos", VmasVec * _DE), ("radius", _f32 * _DE), ("vel", VmasVec * _DA), ("rot", VmasVec * _DA),
+        ("n_rays", _i32 * _DL), ("max_range", _f32 * _DL), ("mask", ctypes.c_uint32 * _DL),
+        ("angles", (_vp * _DA) * _DL), ("ang_s0", (_i32 * _DA) * _DL), ("ang_s1", (_i32 * _DA) * _DL),
+        ("lidar", (_vp * _DA) * _DL), ("obs", _vp * _DA),
+        ("agents_pos", _vp), ("targets_pos", _vp), ("dists", _vp), ("per_target", _vp), ("covered", _vp),
+        ("time_rew", _vp), ("shared", _vp), ("covering", _vp * _DA), ("collision", _vp * _DA),
+        ("rewards", _vp * _DA),
+    ]
+
+
 # Per-call pointer tables are built as numpy structured arrays (one row per entity/agent/joint);
 # their layouts must match VmasEntityIO / VmasAgentIO / VmasJointIO / VmasRayTarget.
 ENTITY_IO_DTYPE = np.dtype(
@@ -393,6 +433,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_test_hold.argtypes = [_i32, _i32, ctypes.c_int64, _vp]
     lib.vmas_balance_outputs.restype = _i32
     lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_discovery_outputs.restype = _i32
+    lib.vmas_discovery_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_transport_outputs.restype = _i32
+    lib.vmas_transport_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_flocking_outputs.restype = _i32
     lib.vmas_flocking_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_copy_spans.restype = _i32

@@ -189,6 +189,179 @@ __global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
     }
 }
 
+// transport.py:130-190 (restated in scenarios/transport.py).  Grid: x = 64-env groups, y = part:
+// 0 the reward (every package) + done, 1 + i agent i's observation.  An observation part of a
+// launch that also computes the reward recomputes on_goal (is_overlapping, deterministic) rather
+// than reading part 0's output.
+__global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
+    constexpr int MP = VMAS_TRANSPORT_MAX_PACKAGES;
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= io.batch) return;
+    const int part = blockIdx.y, np = io.n_packages;
+    if (part == 0) {
+        bool all_on = true;
+        if (io.what & VMAS_SCN_REWARD) {
+            float rew = 0.f;  // self.rew = zeros
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+                if (i >= np) continue;
+                const float dist = norm(ref_pos(io.package[i], b) - ref_pos(io.goal[i], b));
+                const bool on = overlap_box_sphere(io.package[i], io.goal[i], b);
+                io.dist_to_goal[i][b] = dist;
+                io.on_goal[i][b] = on ? 1 : 0;
+                const float* c = on ? io.green : io.red;  // where(on_goal, green, red)
+                io.color[i][(long)b * 3 + 0] = c[0];
+                io.color[i][(long)b * 3 + 1] = c[1];
+                io.color[i][(long)b * 3 + 2] = c[2];
+                const float shaping = dist * io.shaping_factor;
+                rew = rew + (on ? 0.f : io.global_shaping[i][(long)b * io.gs_s0[i]] - shaping);
+                io.global_shaping_out[i][b] = shaping;
+                all_on = all_on && on;
+            }
+            io.rew[b] = rew;
+        } else if (io.what & VMAS_SCN_DONE) {
+#pragma unroll
+            for (int i = 0; i < MP; ++i)
+                if (i < np) all_on = all_on && io.on_goal_in[i][b] != 0;
+        }
+        if (io.what & VMAS_SCN_DONE) io.done[b] = all_on ? 1 : 0;  // all(stack(on_goal), -1)
+        return;
+    }
+    const int a = part - 1;
+    const V2 p = ld_vec2(io.agent_pos[a], b), v = ld_vec2(io.agent_vel[a], b);
+    float* o = io.obs[a] + (long)b * (4 + 7 * np);
+    o[0] = p.x;
+    o[1] = p.y;
+    o[2] = v.x;
+    o[3] = v.y;
+#pragma unroll
+    for (int i = 0; i < MP; ++i) {
+        if (i >= np) continue;
+        const V2 pp = ref_pos(io.package[i], b), gp = ref_pos(io.goal[i], b), pv = ld_vec2(io.package_vel[i], b);
+        const bool on = (io.what & VMAS_SCN_REWARD) ? overlap_box_sphere(io.package[i], io.goal[i], b)
+                                                     : io.on_goal_in[i][b] != 0;
+        float* q = o + 4 + 7 * i;
+        q[0] = pp.x - gp.x;
+        q[1] = pp.y - gp.y;
+        q[2] = pp.x - p.x;
+        q[3] = pp.y - p.y;
+        q[4] = pv.x;
+        q[5] = pv.y;
+        q[6] = on ? 1.f : 0.f;
+    }
+}
+
+// discovery.py:146-246 (restated in scenarios/discovery.py), REWARD part: one thread per env.
+__global__ void __launch_bounds__(64) k_discovery_reward(VmasDiscoveryIO io) {
+    constexpr int MA = VMAS_DISC_MAX_AGENTS, MT = VMAS_DISC_MAX_TARGETS;
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= io.batch) return;
+    const int A = io.n_agents, T = io.n_targets;
+    V2 PA[MA], PT[MT];
+#pragma unroll
+    for (int i = 0; i < MA; ++i) PA[i] = i < A ? ld_vec2(io.pos[io.agent_entity[i]], b) : mk(0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) PT[j] = j < T ? ld_vec2(io.pos[io.target_entity[j]], b) : mk(0.f, 0.f);
+    // the stacks and the time reward
+#pragma unroll
+    for (int i = 0; i < MA; ++i)
+        if (i < A) reinterpret_cast<float2*>(io.agents_pos)[(long)b * A + i] = make_float2(PA[i].x, PA[i].y);
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+        if (j < T) reinterpret_cast<float2*>(io.targets_pos)[(long)b * T + j] = make_float2(PT[j].x, PT[j].y);
+    if (io.time_int) reinterpret_cast<int64_t*>(io.time_rew)[b] = io.time_penalty_i;  // torch.full(int)
+    else reinterpret_cast<float*>(io.time_rew)[b] = io.time_penalty;
+    // torch.cdist (p = 2): sqrt(fl(fl(d0^2) + fl(d1^2))); per target the count of agents in range
+    int cnt[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) cnt[j] = 0;
+#pragma unroll
+    for (int i = 0; i < MA; ++i) {
+        if (i >= A) continue;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            if (j >= T) continue;
+            const float d0 = PA[i].x - PT[j].x, d1 = PA[i].y - PT[j].y;
+            const float d = sqrtf(d0 * d0 + d1 * d1);
+            io.dists[((long)b * A + i) * T + j] = d;
+            cnt[j] += (d < io.covering_range) ? 1 : 0;
+        }
+    }
+    bool cov[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+        cov[j] = cnt[j] >= io.agents_per_target;
+        if (j < T) {
+            io.per_target[(long)b * T + j] = (int64_t)cnt[j];
+            io.covered[(long)b * T + j] = cov[j] ? 1 : 0;
+        }
+    }
+    // agent_reward: covering_reward[:] = 0; += (count of covered targets in range) * coeff;
+    // shared[:] = 0; += each agent's covering reward in agent order; halved where nonzero
+    float shared = 0.f;
+    float covr[MA];
+#pragma unroll
+    for (int i = 0; i < MA; ++i) {
+        covr[i] = 0.f;
+        if (i >= A) continue;
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            if (j >= T) continue;
+            const float d0 = PA[i].x - PT[j].x, d1 = PA[i].y - PT[j].y;
+            n += (sqrtf(d0 * d0 + d1 * d1) < io.covering_range && cov[j]) ? 1 : 0;
+        }
+        covr[i] = 0.f + (float)n * io.covering_rew_coeff;
+        io.covering[i][b] = covr[i];
+        shared = shared + covr[i];
+    }
+    if (shared != 0.f) shared = shared / 2.f;
+    io.shared[b] = shared;
+#pragma unroll
+    for (int i = 0; i < MA; ++i) {
+        if (i >= A) continue;
+        io.collision[i][b] = 0.f;  // collision_rew[:] = 0 (penalty 0: nothing added)
+        const float cv = io.shared_reward ? shared : covr[i];
+        io.rewards[i][b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
+    }
+}
+
+// discovery.py:248-255, OBS part: one thread per (env, agent, part).
+__global__ void __launch_bounds__(64) k_discovery_obs(VmasDiscoveryIO io) {
+    constexpr int ME = VMAS_DISC_MAX_ENTITIES;
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= io.batch) return;
+    int rays = 0;
+    for (int s = 0; s < io.n_lidars; ++s) rays += io.n_rays[s];
+    const int parts = 1 + rays, a = blockIdx.y / parts, part = blockIdx.y - a * parts;
+    const int self = io.agent_entity[a], W = 4 + rays;
+    const V2 p = ld_vec2(io.pos[self], b);
+    float* o = io.obs[a] + (long)b * W;
+    if (part == 0) {
+        const V2 v = ld_vec2(io.vel[a], b);
+        o[0] = p.x;
+        o[1] = p.y;
+        o[2] = v.x;
+        o[3] = v.y;
+        return;
+    }
+    int r = part - 1, s = 0, col = 4;
+    while (s + 1 < io.n_lidars && r >= io.n_rays[s]) {
+        r -= io.n_rays[s];
+        col += io.n_rays[s];
+        ++s;
+    }
+    const uint32_t mask = io.mask[s] & ~(1u << self);  // World.cast_rays skips the entity itself
+    const float ang = io.angles[s][a][(long)b * io.ang_s0[s][a] + (long)r * io.ang_s1[s][a]] + ld_vec1(io.rot[a], b);
+    const float dc = cosf(ang), ds = sinf(ang), mr = io.max_range[s];
+    float best = mr;
+#pragma unroll
+    for (int e = 0; e < ME; ++e)  // (spheres: checked by the host entry point)
+        if (e < io.n_entities && ((mask >> e) & 1u)) best = tmin(best, ray_sphere(p, dc, ds, ld_vec2(io.pos[e], b), io.radius[e], mr));
+    io.lidar[s][a][(long)b * io.n_rays[s] + r] = best;
+    o[col + r] = best;
+}
+
 }  // namespace
 
 extern "C" {
@@ -223,6 +396,48 @@ int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* st
     static_assert(sizeof(VmasFlockingIO) <= 4096, "kernel argument block");
     const int parts = (io->what & VMAS_SCN_OBS) ? 1 + io->n_rays : 1;
     hipLaunchKernelGGL(k_flocking, dim3((io->batch + 63) / 64, io->n_policy * parts), dim3(64), 0, (hipStream_t)stream, *io);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_transport_outputs(int32_t device, const VmasTransportIO* io, void* stream) {
+    if (!io || device < 0 || io->batch <= 0 || io->n_agents < 0 || io->n_agents > VMAS_TRANSPORT_MAX_AGENTS ||
+        io->n_packages < 0 || io->n_packages > VMAS_TRANSPORT_MAX_PACKAGES)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_transport_outputs: bad arguments");
+    for (int i = 0; i < io->n_packages; ++i)
+        if (io->package[i].shape != VMAS_BOX || io->goal[i].shape != VMAS_SPHERE)
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_transport_outputs: package %d is not (box, sphere goal)", i);
+    VMAS_AUX_HIP(hipSetDevice(device));
+    static_assert(sizeof(VmasTransportIO) <= 4096, "kernel argument block");
+    const int parts = 1 + ((io->what & VMAS_SCN_OBS) ? io->n_agents : 0);
+    hipLaunchKernelGGL(k_transport, dim3((io->batch + 63) / 64, parts), dim3(64), 0, (hipStream_t)stream, *io);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream) {
+    if (!io || device < 0 || io->batch <= 0 || io->n_agents < 1 || io->n_agents > VMAS_DISC_MAX_AGENTS ||
+        io->n_targets < 0 || io->n_targets > VMAS_DISC_MAX_TARGETS || io->n_entities < 1 ||
+        io->n_entities > VMAS_DISC_MAX_ENTITIES || io->n_lidars < 0 || io->n_lidars > VMAS_DISC_MAX_LIDARS)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_discovery_outputs: bad arguments");
+    for (int i = 0; i < io->n_agents; ++i)
+        if (io->agent_entity[i] < 0 || io->agent_entity[i] >= io->n_entities)
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_discovery_outputs: bad agent index %d", i);
+    for (int j = 0; j < io->n_targets; ++j)
+        if (io->target_entity[j] < 0 || io->target_entity[j] >= io->n_entities)
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_discovery_outputs: bad target index %d", j);
+    int rays = 0;
+    for (int s = 0; s < io->n_lidars; ++s) {
+        if (io->n_rays[s] < 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_discovery_outputs: bad ray count");
+        rays += io->n_rays[s];
+    }
+    VMAS_AUX_HIP(hipSetDevice(device));
+    static_assert(sizeof(VmasDiscoveryIO) <= 4096, "kernel argument block");
+    const unsigned gx = (unsigned)((io->batch + 63) / 64);
+    if (io->what & VMAS_SCN_REWARD)
+        hipLaunchKernelGGL(k_discovery_reward, dim3(gx), dim3(64), 0, (hipStream_t)stream, *io);
+    if (io->what & VMAS_SCN_OBS)
+        hipLaunchKernelGGL(k_discovery_obs, dim3(gx, io->n_agents * (1 + rays)), dim3(64), 0, (hipStream_t)stream, *io);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

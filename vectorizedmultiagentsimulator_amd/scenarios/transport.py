@@ -6,8 +6,12 @@ Workload of BASELINE config C3.  Restates vmas/scenarios/transport.py:15-190 (la
 reward, observation, done) and its dribbling heuristic policy (transport.py:193-350).
 Entities: goal (sphere r=0.15, no collide), packages (movable boxes), agents (spheres).
 """
+import ctypes
+
 import torch
 
+from vectorizedmultiagentsimulator_amd import _native as N
+from vectorizedmultiagentsimulator_amd.simulator import _fused
 from vectorizedmultiagentsimulator_amd.simulator.core import Agent, Box, Landmark, Sphere, World
 from vectorizedmultiagentsimulator_amd.simulator.heuristic_policy import BaseHeuristicPolicy
 from vectorizedmultiagentsimulator_amd.simulator.scenario import BaseScenario
@@ -70,6 +74,8 @@ class Scenario(BaseScenario):
                 package.global_shaping[env_index] = dist[env_index] * self.shaping_factor
 
     def reward(self, agent: Agent):
+        if _fused.enabled(self.world) and self._fused_ok():
+            return self._fused_reward(agent)
         w = self.world
         if agent == w.agents[0]:
             self.rew = torch.zeros(w.batch_dim, device=w.device, dtype=torch.float32)
@@ -86,6 +92,8 @@ class Scenario(BaseScenario):
         return self.rew
 
     def observation(self, agent: Agent):
+        if _fused.enabled(self.world) and self._fused_ok():
+            return self._fused_observation(agent)
         package_obs = []
         for package in self.packages:
             package_obs.append(package.state.pos - package.goal.state.pos)
@@ -95,7 +103,111 @@ class Scenario(BaseScenario):
         return torch.cat([agent.state.pos, agent.state.vel, *package_obs], dim=-1)
 
     def done(self):
+        if _fused.enabled(self.world) and self._fused_ok():
+            return self._fused_done()
         return torch.all(torch.stack([package.on_goal for package in self.packages], dim=1), dim=-1)
+
+    # ---- fused program (GPU worlds; csrc/vmas_scenarios.hip k_transport) -----------------------
+    # The first agent's reward call runs ONE launch: the reward block above (every package's
+    # dist_to_goal, on_goal, colour, re-bound global_shaping; the shared rew), every agent's
+    # observation and done().  Reward calls return self.rew as the reference does; observation /
+    # done calls hand out the precomputed tensors while their inputs are unchanged
+    # (_fused.state_key), else recompute.
+
+    def _fused_ok(self) -> bool:
+        w = self.world
+        return (len(self.packages) <= N.VMAS_TRANSPORT_MAX_PACKAGES and len(w.agents) <= N.VMAS_TRANSPORT_MAX_AGENTS
+                and all(type(p.shape).__name__ == "Box" and type(p.goal.shape).__name__ == "Sphere"
+                        for p in self.packages))
+
+    def _obs_inputs(self):
+        ts = []
+        for p in self.packages:
+            ts += [p.state.pos, p.state.rot, p.goal.state.pos, p.state.vel, p.on_goal]
+        for a in self.world.agents:
+            ts += [a.state.pos, a.state.vel]
+        return ts
+
+    def _run_fused(self, what: int):
+        w = self.world
+        dev = torch.device(w.device)
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        B = w.batch_dim
+        keep = []
+        io = N.VmasTransportIO()
+        io.batch, io.n_agents, io.n_packages, io.what = B, len(w.agents), len(self.packages), what
+        io.shaping_factor = float(self.shaping_factor)
+        for k in range(3):
+            io.red[k], io.green[k] = Color.RED.value[k], Color.GREEN.value[k]
+        out = {"dist": [], "on_goal": [], "color": [], "gs": []}
+        for i, p in enumerate(self.packages):
+            io.package[i] = _fused.ref(w, p, keep, 0)
+            io.goal[i] = _fused.ref(w, p.goal, keep, 0)
+            io.package_vel[i] = _fused.vec(_fused.f32(p.state.vel, dev), keep)
+            if what & N.VMAS_SCN_REWARD:
+                gs = _fused.f32(p.global_shaping, dev)
+                keep.append(gs)
+                io.global_shaping[i], io.gs_s0[i] = gs.data_ptr(), gs.stride(0)
+                for k, shape, dt in (("dist", (B,), torch.float32), ("on_goal", (B,), torch.bool),
+                                     ("color", (B, 3), torch.float32), ("gs", (B,), torch.float32)):
+                    out[k].append(torch.empty(shape, device=dev, dtype=dt))
+                io.dist_to_goal[i] = out["dist"][i].data_ptr()
+                io.on_goal[i] = out["on_goal"][i].data_ptr()
+                io.color[i] = out["color"][i].data_ptr()
+                io.global_shaping_out[i] = out["gs"][i].data_ptr()
+            else:
+                og = p.on_goal
+                if og.dtype is not torch.bool or og.device != dev or not og.is_contiguous():
+                    og = og.to(device=dev, dtype=torch.bool).contiguous()
+                keep.append(og)
+                io.on_goal_in[i] = og.data_ptr()
+        if what & N.VMAS_SCN_REWARD:
+            out["rew"] = torch.empty(B, device=dev, dtype=torch.float32)
+            io.rew = out["rew"].data_ptr()
+        if what & N.VMAS_SCN_OBS:
+            W = 4 + 7 * len(self.packages)
+            out["obs"] = [torch.empty(B, W, device=dev, dtype=torch.float32) for _ in w.agents]
+            for i, a in enumerate(w.agents):
+                io.agent_pos[i] = _fused.vec(_fused.f32(a.state.pos, dev), keep)
+                io.agent_vel[i] = _fused.vec(_fused.f32(a.state.vel, dev), keep)
+                io.obs[i] = out["obs"][i].data_ptr()
+        if what & N.VMAS_SCN_DONE:
+            out["done"] = torch.empty(B, device=dev, dtype=torch.bool)
+            io.done = out["done"].data_ptr()
+        _fused.check(_fused.lib().vmas_transport_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
+                     "vmas_transport_outputs")
+        if what & N.VMAS_SCN_REWARD:
+            self.rew = out["rew"]
+            for i, p in enumerate(self.packages):
+                p.dist_to_goal = out["dist"][i]
+                p.on_goal = out["on_goal"][i]
+                p.color = out["color"][i]
+                p.global_shaping = out["gs"][i]
+        return out
+
+    def _fused_reward(self, agent: Agent):
+        if agent == self.world.agents[0]:
+            out = self._run_fused(N.VMAS_SCN_REWARD | N.VMAS_SCN_OBS | N.VMAS_SCN_DONE)
+            self._fc = {"key": _fused.state_key(self._obs_inputs()), "obs": dict(enumerate(out["obs"])),
+                        "done": out["done"]}
+        return self.rew
+
+    def _fused_observation(self, agent: Agent):
+        i = self.world.agents.index(agent)
+        c = getattr(self, "_fc", None)
+        if c is None or i not in c["obs"] or c["key"] != _fused.state_key(self._obs_inputs()):
+            out = self._run_fused(N.VMAS_SCN_OBS)
+            c = self._fc = {"key": _fused.state_key(self._obs_inputs()), "obs": dict(enumerate(out["obs"])),
+                            "done": None}
+        return c["obs"].pop(i)
+
+    def _fused_done(self):
+        c = getattr(self, "_fc", None)
+        if c is not None and c["done"] is not None and c["key"] == _fused.state_key(self._obs_inputs()):
+            d, c["done"] = c["done"], None
+            return d
+        return self._run_fused(N.VMAS_SCN_DONE)["done"]
 
 
 class HeuristicPolicy(BaseHeuristicPolicy):

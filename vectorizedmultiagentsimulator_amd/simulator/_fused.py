@@ -26,8 +26,21 @@ from .. import _native as N
 _ON = os.environ.get("VMAS_FUSED_SCENARIOS", "1") != "0"
 
 
+_OFF_DEPTH = [0]
+
+
 def enabled(world) -> bool:
-    return _ON and torch.device(world.device).type == "cuda"
+    return _ON and _OFF_DEPTH[0] == 0 and torch.device(world.device).type == "cuda"
+
+
+class disabled:
+    """Context: the scenario programs run as torch ops (a fused program's fallback)."""
+
+    def __enter__(self):
+        _OFF_DEPTH[0] += 1
+
+    def __exit__(self, *exc):
+        _OFF_DEPTH[0] -= 1
 
 
 def device_index(world) -> int:
