@@ -515,6 +515,45 @@ int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, vo
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);
 
+/* Gradient of one World.step (csrc/vmas_grad.hip; autograd through the step, reference
+ * test_vmas.py:277-304, environment.py grad_enabled): the vector-Jacobian product.  `io` is the
+ * forward's VmasStepIO (inputs; its out_* pointers are ignored); `grad_out`'s out_* pointers hold
+ * the loss gradient with respect to the forward's outputs, in the forward's output layout;
+ * `grad_in` receives the gradient with respect to each entity's pos [B,2] / vel [B,2] /
+ * rot [B] / ang_vel [B] and each agent's force [B,2] / torque [B] (contiguous; a NULL entry is
+ * skipped).  Forward-mode dual numbers through the same physics functions as the forward,
+ * with the forward's batch-global broadphase mask.  device -1: host backend.  Synchronises
+ * `stream`. */
+typedef struct VmasGradIO {
+    float* const* pos;     /* [n_entities] */
+    float* const* vel;
+    float* const* rot;
+    float* const* ang_vel;
+    float* const* force;   /* [n_agents] */
+    float* const* torque;
+} VmasGradIO;
+int32_t vmas_world_step_vjp(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                            const VmasPairDesc* pairs, const VmasJointDesc* joints,
+                            const VmasStepIO* io, const VmasStepIO* grad_out,
+                            const VmasGradIO* grad_in, void* stream);
+/* Gradient of a distance query (vmas_distance's VMAS_DIST_POINT / VMAS_DIST_PAIR; core.py:1787-1904)
+ * with respect to a's pos [B,2] / rot [B], b's pos / rot and the test point [B,2] (outputs may be
+ * NULL), given grad_out [B].  Same dual-number method as vmas_world_step_vjp. */
+int32_t vmas_distance_vjp(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
+                          const VmasShapeRef* b, const float* test_point, int32_t tp_s0, int32_t tp_s1,
+                          const float* grad_out, float* grad_a_pos, float* grad_a_rot, float* grad_b_pos,
+                          float* grad_b_rot, float* grad_point, void* stream);
+/* Gradient of vmas_cast_rays (core.py:1661-1785) with respect to the origin [B,2], the angle offset
+ * `rot` [B], the angles [B,R] and every target's pos [B,2] / rot [B] (host arrays of device
+ * pointers, entries may be NULL), given grad_out [B,R] contiguous.  Synchronises `stream`. */
+int32_t vmas_cast_rays_vjp(int32_t device, int32_t batch, int32_t n_rays, const float* origin,
+                           int32_t o_s0, int32_t o_s1, const float* angles, int32_t a_s0,
+                           int32_t a_s1, const float* rot, int32_t r_s0,
+                           const VmasRayTarget* targets, int32_t n_targets, float max_range,
+                           const float* grad_out, float* grad_origin, float* grad_rot,
+                           float* grad_angles, float* const* grad_target_pos,
+                           float* const* grad_target_rot, void* stream);
+
 /* World-specialised step (csrc/vmas_jit.hip): same seam and semantics as vmas_world_create /
  * vmas_world_step (World.step, core.py:1971-2014), GPU only.  vmas_jit_world_create generates a
  * gfx950 kernel for this exact world (constants folded, per-wave straight-line pair/entity code)

@@ -323,8 +323,12 @@ class _Ent:
 class OracleWorld:
     """The reference World.step / cast_rays / distance programs on CPU tensors."""
 
-    def __init__(self, world, snap: Dict[int, dict], broadphase: str = "batch"):
+    def __init__(self, world, snap: Dict[int, dict], broadphase: str = "batch", grad_safe: bool = False):
         self.w = world
+        # the reference's ray casts write max_range into a norm's output in place (core.py:1277,
+        # 1370, 1537-1540), which torch.autograd refuses to differentiate; grad_safe restates those
+        # writes as torch.where (the same values) so tests can take the oracle's ray gradients
+        self.grad_safe = grad_safe
         self.ents: List[_Ent] = [_Ent(e, snap[i]) for i, e in enumerate(world.entities)]
         self.by_obj = {id(e): self.ents[i] for i, e in enumerate(world.entities)}
         self.batch_dim = world.batch_dim
@@ -746,8 +750,7 @@ class OracleWorld:
         intersect_world = rotate_vector(intersect_aabb, box_rot_expanded) + box_pos_expanded
         collision = (tmax >= tmin) & (tmin > 0.0)
         dist = torch.linalg.norm(ray_origin - intersect_world, dim=-1)
-        dist[~collision] = max_range
-        return dist
+        return self._miss(dist, ~collision, max_range)
 
     def _cast_rays_to_sphere(self, sphere_pos, sphere_radius, ray_origin, ray_direction, max_range):
         batch_size = ray_origin.shape[:-1]
@@ -773,8 +776,7 @@ class OracleWorld:
         u_dot_ray = (u * ray_dir_world).sum(-1)
         sphere_is_in_front = u_dot_ray > 0.0
         dist = torch.linalg.vector_norm(u1, dim=-1) - m
-        dist[~(ray_intersects & sphere_is_in_front)] = max_range
-        return dist
+        return self._miss(dist, ~(ray_intersects & sphere_is_in_front), max_range)
 
     def _cast_rays_to_line(self, line_pos, line_rot, line_length, ray_origin, ray_direction, max_range):
         batch_size = ray_origin.shape[:-1]
@@ -792,10 +794,15 @@ class OracleWorld:
         t = cross(q - line_pos_expanded, s / rxs)
         u = cross(q - line_pos_expanded, r / rxs)
         d = torch.linalg.norm(u * s, dim=-1)
-        d[(rxs == 0.0).squeeze(-1)] = max_range
-        d[(t > 0.5).squeeze(-1)] = max_range
-        d[(t < -0.5).squeeze(-1)] = max_range
-        d[(u < 0.0).squeeze(-1)] = max_range
+        for miss in ((rxs == 0.0), (t > 0.5), (t < -0.5), (u < 0.0)):
+            d = self._miss(d, miss.squeeze(-1), max_range)
+        return d
+
+    def _miss(self, d, miss, max_range):
+        """``d[miss] = max_range`` (the reference's in-place write), or its torch.where form."""
+        if self.grad_safe:
+            return torch.where(miss, torch.tensor(max_range, dtype=d.dtype), d)
+        d[miss] = max_range
         return d
 
     def cast_rays(self, entity_index: int, angles: Tensor, max_range: float, entity_filter):

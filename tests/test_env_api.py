@@ -150,11 +150,16 @@ def test_terminated_truncated_and_max_steps():
     assert trunc.all()
 
 
-def test_grad_enabled_is_refused_loudly():
+def test_grad_enabled_step_is_differentiable():
+    """grad_enabled=True (environment.py:55 of the reference): the step keeps the autograd graph
+    from the actions to the next observations; graph replay cannot carry one and says so."""
     env = make_env("balance", num_envs=4, seed=0, grad_enabled=True)
     acts = [a.requires_grad_(True) for a in env.get_random_actions()]
-    with pytest.raises(NotImplementedError):
-        env.step(acts)
+    obs, rews, _, _ = env.step(acts)
+    (g,) = torch.autograd.grad(obs[0].sum() + rews[0].sum(), acts[0])
+    assert g.shape == acts[0].shape and torch.isfinite(g).all() and g.abs().sum() > 0
+    with pytest.raises(ValueError):
+        make_env("balance", num_envs=4, seed=0, grad_enabled=True, graph_step=True)
 
 
 def test_state_replacement_semantics():

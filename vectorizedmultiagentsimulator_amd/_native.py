@@ -57,6 +57,9 @@ EXPORTED_SYMBOLS = (
     "vmas_test_hold",
     "vmas_balance_outputs",
     "vmas_copy_spans",
+    "vmas_world_step_vjp",
+    "vmas_distance_vjp",
+    "vmas_cast_rays_vjp",
     "vmas_flocking_outputs",
     "vmas_transport_outputs",
     "vmas_discovery_outputs",
@@ -233,6 +236,10 @@ def copy_spans(device_index: int, pairs, stream) -> None:
     """dst.copy_(src) for every (dst, src) pair of same-size contiguous device tensors, all in one
     native launch (vmas_copy_spans; any dtype: bytes are copied)."""
     copy_raw(device_index, [(s.data_ptr(), d.data_ptr(), d.numel() * d.element_size()) for d, s in pairs], stream)
+
+
+class VmasGradIO(ctypes.Structure):
+    _fields_ = [("pos", _vp), ("vel", _vp), ("rot", _vp), ("ang_vel", _vp), ("force", _vp), ("torque", _vp)]
 
 
 class VmasVec(ctypes.Structure):
@@ -439,6 +446,13 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_transport_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_flocking_outputs.restype = _i32
     lib.vmas_flocking_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_distance_vjp.restype = _i32
+    lib.vmas_distance_vjp.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    lib.vmas_cast_rays_vjp.restype = _i32
+    lib.vmas_cast_rays_vjp.argtypes = [_i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _vp, _i32,
+                                       ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    lib.vmas_world_step_vjp.restype = _i32
+    lib.vmas_world_step_vjp.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.vmas_copy_spans.restype = _i32
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_stream_abort_capture.restype = _i32

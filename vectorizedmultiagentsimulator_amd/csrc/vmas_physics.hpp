@@ -30,45 +30,62 @@ typedef __hip_internal::uint64_t uint64_t;
 
 #define VHD __host__ __device__ __forceinline__
 
-namespace vmas {
+// The scalar type is a parameter: Real = float everywhere the step runs; the gradient path
+// (csrc/vmas_grad.hip) includes this header once more, in its own namespace, with Real = a
+// forward-mode dual number (value + tangents), so that the derivatives follow exactly the
+// operations, branches and selections of the forward step.
+#ifndef VMAS_PHYS_NS
+#define VMAS_PHYS_NS vmas
+#define VMAS_PHYS_REAL float
+#endif
+
+namespace VMAS_PHYS_NS {
+
+using Real = VMAS_PHYS_REAL;
 
 // utils.py:27 LINE_MIN_DIST = 4 / 6e2, as the f32 value torch uses when it meets a f32 tensor
 constexpr float kLineMinDist = (float)(4.0 / 6e2);
 constexpr float kHalfPi = (float)(3.141592653589793 / 2.0);  // torch.pi / 2 -> f32
 
 struct V2 {
-    float x, y;
+    Real x, y;
 };
-VHD V2 mk(float x, float y) { return V2{x, y}; }
+VHD V2 mk(Real x, Real y) { return V2{x, y}; }
 VHD V2 operator+(V2 a, V2 b) { return V2{a.x + b.x, a.y + b.y}; }
 VHD V2 operator-(V2 a, V2 b) { return V2{a.x - b.x, a.y - b.y}; }
 VHD V2 operator-(V2 a) { return V2{-a.x, -a.y}; }
-VHD V2 operator*(V2 a, float s) { return V2{a.x * s, a.y * s}; }
-VHD V2 operator*(float s, V2 a) { return V2{s * a.x, s * a.y}; }
-VHD V2 operator/(V2 a, float s) { return V2{a.x / s, a.y / s}; }
+VHD V2 operator*(V2 a, Real s) { return V2{a.x * s, a.y * s}; }
+VHD V2 operator*(Real s, V2 a) { return V2{s * a.x, s * a.y}; }
+VHD V2 operator/(V2 a, Real s) { return V2{a.x / s, a.y / s}; }
 
 // torch.linalg.vector_norm(v, dim=-1) of a length-2 vector
-VHD float norm(V2 v) { return sqrtf(v.x * v.x + v.y * v.y); }
+VHD Real norm(V2 v) { return sqrtf(v.x * v.x + v.y * v.y); }
 // TorchUtils.cross (utils.py:194-197): a.x*b.y - a.y*b.x
-VHD float cross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
+VHD Real cross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
 // torch.sign: (0 < x) - (x < 0); NaN -> 0
-VHD float tsign(float x) { return (float)((0.f < x) - (x < 0.f)); }
+VHD Real tsign(Real x) { return Real((float)((0.f < x) - (x < 0.f))); }
 // torch.minimum / torch.maximum / torch.min(dim) / torch.max(dim): NaN propagating
-VHD float tmin(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
-VHD float tmax(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
-// torch.clamp(x, lo, hi)
-VHD float tclamp(float x, float lo, float hi) { return tmin(tmax(x, lo), hi); }
+VHD Real tmin(Real a, Real b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
+VHD Real tmax(Real a, Real b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+// torch.clamp(x, lo, hi).  Its backward passes the gradient where lo <= x <= hi, bounds
+// included; the gradient build (VMAS_PHYS_GRAD, csrc/vmas_grad.hip) keeps x itself there so a value
+// sitting exactly on a bound (an action clamped last step) carries its tangent as torch's does.
+#ifdef VMAS_PHYS_GRAD
+VHD Real tclamp(Real x, Real lo, Real hi) { return (x >= lo && x <= hi) ? x : tmin(tmax(x, lo), hi); }
+#else
+VHD Real tclamp(Real x, Real lo, Real hi) { return tmin(tmax(x, lo), hi); }
+#endif
 
 // Angle trig of one entity: cos/sin(rot) and cos/sin(rot + pi/2) (physics.py:299-301)
 struct Trig {
-    float c0, s0, c1, s1;
+    Real c0, s0, c1, s1;
 };
-VHD Trig make_trig(float rot) {
-    const float r2 = rot + kHalfPi;
+VHD Trig make_trig(Real rot) {
+    const Real r2 = rot + kHalfPi;
     return Trig{cosf(rot), sinf(rot), cosf(r2), sinf(r2)};
 }
 // Lines and joint anchors only use cos/sin(rot); boxes also use the side normal rot + pi/2.
-VHD Trig make_trig_for(float rot, bool box) {
+VHD Trig make_trig_for(Real rot, bool box) {
     if (box) return make_trig(rot);
     return Trig{cosf(rot), sinf(rot), 0.f, 0.f};
 }
@@ -80,35 +97,35 @@ __device__ __forceinline__ bool vote_all(bool b) { return __all(b); }
 __host__ __forceinline__ bool vote_all(bool b) { return b; }
 
 // TorchUtils.clamp_with_norm (utils.py:168-173)
-VHD V2 clamp_with_norm(V2 t, float max_norm) {
-    const float n = norm(t);
+VHD V2 clamp_with_norm(V2 t, Real max_norm) {
+    const Real n = norm(t);
     const V2 nt = (t / n) * max_norm;
     return (n > max_norm) ? nt : t;
 }
-VHD float clamp_with_norm1(float t, float max_norm) {  // [B,1] variant: norm = |t|
-    const float n = fabsf(t);
-    const float nt = (t / n) * max_norm;
+VHD Real clamp_with_norm1(Real t, Real max_norm) {  // [B,1] variant: norm = |t|
+    const Real n = fabsf(t);
+    const Real nt = (t / n) * max_norm;
     return (n > max_norm) ? nt : t;
 }
 
 // torch.logaddexp(0, x) (ATen logaddexp kernel: m + log1p(exp(-|a-b|)))
-VHD float logaddexp0(float x) {
-    const float m = tmax(0.f, x);
+VHD Real logaddexp0(Real x) {
+    const Real m = tmax(0.f, x);
     return m + log1pf(expf(-fabsf(0.f - x)));
 }
 
 // World._get_constraint_forces (core.py:2804-2838).  Returns the force on a; b gets -force.
-// `sc` = f32(sign * force_multiplier) (a python float product), `k` = f32(contact_margin).
-VHD V2 constraint_force(V2 pa, V2 pb, float dmin, float sc, float k, bool attractive) {
+// `sc` = f32(sign * force_multiplier) (a python Real product), `k` = f32(contact_margin).
+VHD V2 constraint_force(V2 pa, V2 pb, Real dmin, Real sc, Real k, bool attractive) {
     const V2 delta = pa - pb;
-    const float dist = norm(delta);
+    const Real dist = norm(delta);
     // The reference zeroes the force where dist < 1e-6 or (repulsive) dist > dmin /
     // (attractive) dist < dmin; when that holds in every lane the softplus is not needed.
     const bool zero = (dist < 1e-6f) || (attractive ? (dist < dmin) : (dist > dmin));
     if (vote_all(zero)) return mk(0.f, 0.f);
-    const float x = attractive ? (-(dmin - dist)) / k : (dmin - dist) / k;  // (dmin-dist)*sign/k
-    const float pen = logaddexp0(x) * k;
-    const float dsafe = (dist > 0.f) ? dist : 1e-8f;
+    const Real x = attractive ? (-(dmin - dist)) / k : (dmin - dist) / k;  // (dmin-dist)*sign/k
+    const Real pen = logaddexp0(x) * k;
+    const Real dsafe = (dist > 0.f) ? dist : 1e-8f;
     V2 f = mk(((sc * delta.x) / dsafe) * pen, ((sc * delta.y) / dsafe) * pen);
     if (dist < 1e-6f) f = mk(0.f, 0.f);
     if (!attractive) {
@@ -120,12 +137,12 @@ VHD V2 constraint_force(V2 pa, V2 pb, float dmin, float sc, float k, bool attrac
 }
 
 // physics._get_closest_point_line (physics.py:399-428); dir = (cos, sin) of the line rot.
-VHD V2 closest_point_line(V2 lp, V2 dir, float half, V2 tp, bool limit) {
+VHD V2 closest_point_line(V2 lp, V2 dir, Real half, V2 tp, bool limit) {
     const V2 d = lp - tp;
-    const float dot = d.x * dir.x + d.y * dir.y;
-    const float sg = tsign(dot);
-    const float dfc = limit ? tmin(fabsf(dot), half) : fabsf(dot);
-    const float m = sg * dfc;
+    const Real dot = d.x * dir.x + d.y * dir.y;
+    const Real sg = tsign(dot);
+    const Real dfc = limit ? tmin(fabsf(dot), half) : fabsf(dot);
+    const Real m = sg * dfc;
     return lp - dir * m;
 }
 
@@ -133,9 +150,9 @@ VHD V2 closest_point_line(V2 lp, V2 dir, float half, V2 tp, bool limit) {
 struct Seg {
     V2 p;       // centre
     V2 dir;     // (cos, sin) of the side's rot
-    float half; // half length
+    Real half; // half length
 };
-VHD Seg box_side(V2 pos, Trig t, float hl, float hw, int i) {
+VHD Seg box_side(V2 pos, Trig t, Real hl, Real hw, int i) {
     const V2 rv = mk(t.c0, t.s0);
     const V2 rv2 = mk(t.c1, t.s1);
     switch (i) {
@@ -147,14 +164,14 @@ VHD Seg box_side(V2 pos, Trig t, float hl, float hw, int i) {
 }
 
 // physics._get_closest_point_box (physics.py:262-294): first strict minimum over the 4 sides.
-VHD V2 closest_point_box(V2 pos, Trig t, float hl, float hw, V2 tp) {
+VHD V2 closest_point_box(V2 pos, Trig t, Real hl, Real hw, V2 tp) {
     V2 best = mk(INFINITY, INFINITY);
-    float bd = INFINITY;
+    Real bd = INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const Seg s = box_side(pos, t, hl, hw, i);
         const V2 p = closest_point_line(s.p, s.dir, s.half, tp, true);
-        const float d = norm(tp - p);
+        const Real d = norm(tp - p);
         if (d < bd) {
             bd = d;
             best = p;
@@ -164,11 +181,11 @@ VHD V2 closest_point_box(V2 pos, Trig t, float hl, float hw, V2 tp) {
 }
 
 // physics._get_inner_point_box (physics.py:12-22)
-VHD V2 inner_point_box(V2 outside, V2 surface, V2 box_pos, float* dmag) {
+VHD V2 inner_point_box(V2 outside, V2 surface, V2 box_pos, Real* dmag) {
     const V2 v = surface - outside;
     const V2 u = box_pos - surface;
-    const float vn = norm(v);
-    float xm = (v.x * u.x + v.y * u.y) / vn;
+    const Real vn = norm(v);
+    Real xm = (v.x * u.x + v.y * u.y) / vn;
     V2 x = (v / vn) * xm;
     if (vn == 0.f) {
         x = surface;  // reference quirk: x = surface_point when v_norm == 0
@@ -188,8 +205,8 @@ VHD void closest_points_line_line(Seg l1, Seg l2, V2* out1, V2* out2) {
     // intersection
     const V2 r = a2 - a1, s = b2 - b1;
     const V2 qp = b1 - a1;
-    const float cqpr = cross(qp, r), cqps = cross(qp, s), crs = cross(r, s);
-    const float u = cqpr / crs, t = cqps / crs;
+    const Real cqpr = cross(qp, r), cqps = cross(qp, s), crs = cross(r, s);
+    const Real u = cqpr / crs, t = cqps / crs;
     const bool cond = (crs != 0.f) && (0.f <= u) && (u <= 1.f) && (0.f <= t) && (t <= 1.f);
     // end points projected on the other segment
     const V2 a1b = closest_point_line(l2.p, l2.dir, l2.half, a1, true);
@@ -197,7 +214,7 @@ VHD void closest_points_line_line(Seg l1, Seg l2, V2* out1, V2* out2) {
     const V2 b1a = closest_point_line(l1.p, l1.dir, l1.half, b1, true);
     const V2 b2a = closest_point_line(l1.p, l1.dir, l1.half, b2, true);
     V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
-    float md = INFINITY, d;
+    Real md = INFINITY, d;
     d = norm(a1 - a1b);
     if (d < md) { md = d; c1 = a1; c2 = a1b; }
     d = norm(a2 - a2b);
@@ -216,14 +233,14 @@ VHD void closest_points_line_line(Seg l1, Seg l2, V2* out1, V2* out2) {
 }
 
 // physics._get_closest_line_box (physics.py:327-381): returns (point on box, point on line)
-VHD void closest_line_box(V2 bpos, Trig bt, float hl, float hw, Seg line, V2* pbox, V2* pline) {
+VHD void closest_line_box(V2 bpos, Trig bt, Real hl, Real hw, Seg line, V2* pbox, V2* pline) {
     V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
-    float bd = INFINITY;
+    Real bd = INFINITY;
 #pragma unroll 1
     for (int i = 0; i < 4; ++i) {
         V2 q1, q2;
         closest_points_line_line(box_side(bpos, bt, hl, hw, i), line, &q1, &q2);
-        const float d = norm(q1 - q2);
+        const Real d = norm(q1 - q2);
         if (d < bd) {
             bd = d;
             c1 = q1;
@@ -235,10 +252,10 @@ VHD void closest_line_box(V2 bpos, Trig bt, float hl, float hw, Seg line, V2* pb
 }
 
 // physics._get_closest_box_box (physics.py:25-128): (point on A, point on B)
-VHD void closest_box_box(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, float hlb,
-                         float hwb, V2* out_a, V2* out_b) {
+VHD void closest_box_box(V2 pa, Trig ta, Real hla, Real hwa, V2 pb, Trig tb, Real hlb,
+                         Real hwb, V2* out_a, V2* out_b) {
     V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
-    float bd = INFINITY;
+    Real bd = INFINITY;
 #pragma unroll 1
     for (int i = 0; i < 8; ++i) {
         V2 p1, p2;
@@ -247,7 +264,7 @@ VHD void closest_box_box(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, f
         } else {      // box A vs side j of B: closest_line_box(A, sideB) -> (on A, on B side)
             closest_line_box(pa, ta, hla, hwa, box_side(pb, tb, hlb, hwb, i - 4), &p1, &p2);
         }
-        const float d = norm(p1 - p2);
+        const Real d = norm(p1 - p2);
         if (d < bd) {
             bd = d;
             c1 = p1;
@@ -263,12 +280,12 @@ VHD void closest_box_box(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, f
 // _get_constraint_forces returns (force, -force)), torque on a, torque on b.
 struct PairOut {
     V2 fa;
-    float ta, tb;
+    Real ta, tb;
 };
 
 struct Body {  // one entity's state in one env plus its static shape numbers
     V2 p, v;
-    float rot, w;
+    Real rot, w;
 };
 
 struct WorldK {  // f32 world constants used by the narrowphases
@@ -279,12 +296,12 @@ struct WorldK {  // f32 world constants used by the narrowphases
 };
 
 // _sphere_sphere_vectorized_collision (core.py:2293-2338)
-VHD PairOut pair_ss(V2 pa, V2 pb, float dmin, const WorldK& w) {
+VHD PairOut pair_ss(V2 pa, V2 pb, Real dmin, const WorldK& w) {
     return PairOut{constraint_force(pa, pb, dmin, w.c, w.k, false), 0.f, 0.f};
 }
 
 // _sphere_line_vectorized_collision (core.py:2340-2391); a = line, b = sphere
-VHD PairOut pair_ls(V2 pl, Trig tl, float hl, V2 ps, float dmin, const WorldK& w) {
+VHD PairOut pair_ls(V2 pl, Trig tl, Real hl, V2 ps, Real dmin, const WorldK& w) {
     const V2 cp = closest_point_line(pl, mk(tl.c0, tl.s0), hl, ps, true);
     const V2 fs = constraint_force(ps, cp, dmin, w.c, w.k, false);
     const V2 fl = -fs;
@@ -293,7 +310,7 @@ VHD PairOut pair_ls(V2 pl, Trig tl, float hl, V2 ps, float dmin, const WorldK& w
 }
 
 // _line_line_vectorized_collision (core.py:2393-2456)
-VHD PairOut pair_ll(V2 pa, Trig ta, float hla, V2 pb, Trig tb, float hlb, float dmin,
+VHD PairOut pair_ll(V2 pa, Trig ta, Real hla, V2 pb, Trig tb, Real hlb, Real dmin,
                     const WorldK& w) {
     V2 qa, qb;
     closest_points_line_line(Seg{pa, mk(ta.c0, ta.s0), hla}, Seg{pb, mk(tb.c0, tb.s0), hlb}, &qa, &qb);
@@ -303,11 +320,11 @@ VHD PairOut pair_ll(V2 pa, Trig ta, float hla, V2 pb, Trig tb, float hlb, float 
 }
 
 // _box_sphere_vectorized_collision (core.py:2458-2551); a = box, b = sphere
-VHD PairOut pair_bs(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 ps, float dmin_rl,
+VHD PairOut pair_bs(V2 pbx, Trig tbx, Real hl, Real hw, bool hollow, V2 ps, Real dmin_rl,
                     const WorldK& w) {
     const V2 cpb = closest_point_box(pbx, tbx, hl, hw, ps);
     V2 inner = cpb;
-    float d = 0.f;
+    Real d = 0.f;
     if (!hollow) inner = inner_point_box(ps, cpb, pbx, &d);
     const V2 fs = constraint_force(ps, inner, dmin_rl + d, w.c, w.k, false);
     const V2 fb = -fs;
@@ -321,12 +338,12 @@ VHD PairOut pair_bs(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 ps, fl
 struct Pts {
     V2 p1, p2;
 };
-VHD Pts bl_part(V2 pbx, Trig tbx, float hl, float hw, V2 pl, Trig tl, float hll, int side) {
+VHD Pts bl_part(V2 pbx, Trig tbx, Real hl, Real hw, V2 pl, Trig tl, Real hll, int side) {
     Pts r;
     closest_points_line_line(box_side(pbx, tbx, hl, hw, side), Seg{pl, mk(tl.c0, tl.s0), hll}, &r.p1, &r.p2);
     return r;
 }
-VHD Pts bb_part(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, float hlb, float hwb, int i) {
+VHD Pts bb_part(V2 pa, Trig ta, Real hla, Real hwa, V2 pb, Trig tb, Real hlb, Real hwb, int i) {
     Pts r;
     if (i < 4) closest_line_box(pb, tb, hlb, hwb, box_side(pa, ta, hla, hwa, i), &r.p2, &r.p1);
     else closest_line_box(pa, ta, hla, hwa, box_side(pb, tb, hlb, hwb, i - 4), &r.p1, &r.p2);
@@ -335,11 +352,11 @@ VHD Pts bb_part(V2 pa, Trig ta, float hla, float hwa, V2 pb, Trig tb, float hlb,
 template <class PartFn>
 VHD Pts select_min(int n, PartFn part) {
     Pts best{mk(INFINITY, INFINITY), mk(INFINITY, INFINITY)};
-    float bd = INFINITY;
+    Real bd = INFINITY;
 #pragma unroll 1
     for (int i = 0; i < n; ++i) {
         const Pts q = part(i);
-        const float d = norm(q.p1 - q.p2);
+        const Real d = norm(q.p1 - q.p2);
         if (d < bd) {
             bd = d;
             best = q;
@@ -347,19 +364,19 @@ VHD Pts select_min(int n, PartFn part) {
     }
     return best;
 }
-VHD PairOut bl_finish(V2 pbx, bool hollow, V2 pl, Pts q, float dmin, const WorldK& w) {
+VHD PairOut bl_finish(V2 pbx, bool hollow, V2 pl, Pts q, Real dmin, const WorldK& w) {
     const V2 pb = q.p1, plp = q.p2;
     V2 inner = pb;
-    float d = 0.f;
+    Real d = 0.f;
     if (!hollow) inner = inner_point_box(plp, pb, pbx, &d);
     const V2 fbox = constraint_force(inner, plp, dmin + d, w.c, w.k, false);
     const V2 fline = -fbox;
     return PairOut{fbox, cross(pb - pbx, fbox), cross(plp - pl, fline)};
 }
-VHD PairOut bb_finish(V2 pa, bool hol_a, V2 pb, bool hol_b, Pts q, float dmin, const WorldK& w) {
+VHD PairOut bb_finish(V2 pa, bool hol_a, V2 pb, bool hol_b, Pts q, Real dmin, const WorldK& w) {
     const V2 qa = q.p1, qb = q.p2;
     V2 ia = qa, ib = qb;
-    float da = 0.f, db = 0.f;
+    Real da = 0.f, db = 0.f;
     if (!hol_a) ia = inner_point_box(qb, qa, pa, &da);
     if (!hol_b) ib = inner_point_box(qa, qb, pb, &db);
     const V2 fa = constraint_force(ia, ib, (da + db) + dmin, w.c, w.k, false);
@@ -368,39 +385,39 @@ VHD PairOut bb_finish(V2 pa, bool hol_a, V2 pb, bool hol_b, Pts q, float dmin, c
 }
 
 // _box_line_vectorized_collision (core.py:2553-2652); a = box, b = line
-VHD PairOut pair_bl(V2 pbx, Trig tbx, float hl, float hw, bool hollow, V2 pl, Trig tl, float hll,
-                    float dmin, const WorldK& w) {
+VHD PairOut pair_bl(V2 pbx, Trig tbx, Real hl, Real hw, bool hollow, V2 pl, Trig tl, Real hll,
+                    Real dmin, const WorldK& w) {
     const Pts q = select_min(4, [&](int i) { return bl_part(pbx, tbx, hl, hw, pl, tl, hll, i); });
     return bl_finish(pbx, hollow, pl, q, dmin, w);
 }
 
 // _box_box_vectorized_collision (core.py:2654-2785)
-VHD PairOut pair_bb(V2 pa, Trig ta, float hla, float hwa, bool hol_a, V2 pb, Trig tb, float hlb,
-                    float hwb, bool hol_b, float dmin, const WorldK& w) {
+VHD PairOut pair_bb(V2 pa, Trig ta, Real hla, Real hwa, bool hol_a, V2 pb, Trig tb, Real hlb,
+                    Real hwb, bool hol_b, Real dmin, const WorldK& w) {
     const Pts q = select_min(8, [&](int i) { return bb_part(pa, ta, hla, hwa, pb, tb, hlb, hwb, i); });
     return bb_finish(pa, hol_a, pb, hol_b, q, dmin, w);
 }
 
 // TorchUtils.rotate_vector (utils.py:176-191) with precomputed cos/sin of the angle
-VHD V2 rotate(V2 v, float c, float s) { return mk(v.x * c - v.y * s, v.x * s + v.y * c); }
+VHD V2 rotate(V2 v, Real c, Real s) { return mk(v.x * c - v.y * s, v.x * s + v.y * c); }
 
 // _vectorized_joint_constraints + _get_constraint_torques (core.py:2200-2291, 2840-2857)
 // fixed_rot = JointConstraint.fixed_rotation for this env.
-VHD PairOut pair_joint(V2 pa, float rota, Trig ta, V2 pb, float rotb, Trig tb, V2 da, V2 db,
-                       float dist, bool rotate_ok, float fixed_rot, const WorldK& w) {
+VHD PairOut pair_joint(V2 pa, Real rota, Trig ta, V2 pb, Real rotb, Trig tb, V2 da, V2 db,
+                       Real dist, bool rotate_ok, Real fixed_rot, const WorldK& w) {
     const V2 pja = pa + rotate(da, ta.c0, ta.s0);
     const V2 pjb = pb + rotate(db, tb.c0, tb.s0);
     const V2 fat = constraint_force(pja, pjb, dist, -w.cj, w.k, true);
     const V2 far = constraint_force(pja, pjb, dist, w.cj, w.k, false);
     const V2 fa = fat + far;
     const V2 fb = (-fat) + (-far);
-    float tra = cross(pja - pa, fa);
-    float trb = cross(pjb - pb, fb);
+    Real tra = cross(pja - pa, fa);
+    Real trb = cross(pjb - pb, fb);
     if (!rotate_ok) {
-        const float delta = rota - (rotb + fixed_rot);
-        const float ad = fabsf(delta);
-        const float pen = expf(ad) - 1.f;
-        float tq = (w.ct * tsign(delta)) * pen;
+        const Real delta = rota - (rotb + fixed_rot);
+        const Real ad = fabsf(delta);
+        const Real pen = expf(ad) - 1.f;
+        Real tq = (w.ct * tsign(delta)) * pen;
         if (ad < 1e-9f) tq = 0.f;
         tra = tra + (-tq);
         trb = trb + tq;
@@ -409,74 +426,141 @@ VHD PairOut pair_joint(V2 pa, float rota, Trig ta, V2 pb, float rotb, Trig tb, V
 }
 
 // get_friction_force (core.py:2054-2072) for a 2-vector
-VHD V2 friction2(V2 v, float coeff, float mass, float sdt) {
-    const float speed = norm(v);
-    const float ffc = coeff * mass;
-    const float den = (speed == 0.f) ? 1e-8f : speed;
+VHD V2 friction2(V2 v, Real coeff, Real mass, Real sdt) {
+    const Real speed = norm(v);
+    const Real ffc = coeff * mass;
+    const Real den = (speed == 0.f) ? 1e-8f : speed;
     V2 f = mk(-(v.x / den) * tmin(ffc, (fabsf(v.x) / sdt) * mass),
               -(v.y / den) * tmin(ffc, (fabsf(v.y) / sdt) * mass));
     if (speed == 0.f) f = mk(0.f, 0.f);
     return f;
 }
-VHD float friction1(float v, float coeff, float mass, float sdt) {
-    const float speed = fabsf(v);
-    const float ffc = coeff * mass;
-    const float den = (speed == 0.f) ? 1e-8f : speed;
-    float f = -(v / den) * tmin(ffc, (fabsf(v) / sdt) * mass);
+VHD Real friction1(Real v, Real coeff, Real mass, Real sdt) {
+    const Real speed = fabsf(v);
+    const Real ffc = coeff * mass;
+    const Real den = (speed == 0.f) ? 1e-8f : speed;
+    Real f = -(v / den) * tmin(ffc, (fabsf(v) / sdt) * mass);
     if (speed == 0.f) f = 0.f;
     return f;
 }
 
+// Action force/torque clamps + friction + gravity of one entity (core.py:1994-2003, 2017-2101).
+// af/at: the agent's current state.force/torque, updated in place (the reference writes the
+// clamped value back to agent.state.force each substep).
+VHD void pre_forces(const VmasEntityDesc& d, bool is_agent, V2& af, Real& at, V2 vel,
+                                           Real w, V2 eg, bool has_eg, Real gx, Real gy, bool has_g,
+                                           Real sdt, Real& fx, Real& fy, Real& tq) {
+    fx = 0.f;
+    fy = 0.f;
+    tq = 0.f;
+    const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+    if (is_agent) {
+        if (mov) {  // _apply_action_force (core.py:2017-2027)
+            V2 f = af;
+            if (d.flags & VMAS_F_MAX_F) f = clamp_with_norm(f, d.max_f);
+            if (d.flags & VMAS_F_F_RANGE) f = mk(tclamp(f.x, -d.f_range, d.f_range), tclamp(f.y, -d.f_range, d.f_range));
+            af = f;
+            fx = fx + f.x;
+            fy = fy + f.y;
+        }
+        if (rotb) {  // _apply_action_torque (core.py:2029-2040)
+            Real t = at;
+            if (d.flags & VMAS_F_MAX_T) t = clamp_with_norm1(t, d.max_t);
+            if (d.flags & VMAS_F_T_RANGE) t = tclamp(t, -d.t_range, d.t_range);
+            at = t;
+            tq = tq + t;
+        }
+    }
+    if (d.flags & VMAS_F_LIN_FRIC) {  // _apply_friction_force (core.py:2053-2101)
+        const V2 f = friction2(vel, d.lin_fric, d.mass, sdt);
+        fx = fx + f.x;
+        fy = fy + f.y;
+    }
+    if (d.flags & VMAS_F_ANG_FRIC) tq = tq + friction1(w, d.ang_fric, d.inertia, sdt);
+    if (mov) {  // _apply_gravity (core.py:2042-2051)
+        if (has_g) {
+            fx = fx + d.mass * gx;
+            fy = fy + d.mass * gy;
+        }
+        if (has_eg) {
+            fx = fx + d.mass * eg.x;
+            fy = fy + d.mass * eg.y;
+        }
+    }
+}
+
+// _integrate_state (core.py:2859-2907)
+VHD void integrate(const VmasEntityDesc& d, int substep, Real sdt, Real fx, Real fy,
+                                          Real tq, bool has_xs, Real xs, bool has_ys, Real ys, V2& p, V2& v,
+                                          Real& rot, Real& w) {
+    if (d.flags & VMAS_F_MOVABLE) {
+        if (substep == 0) v = mk(v.x * d.one_minus_drag, v.y * d.one_minus_drag);
+        const V2 acc = mk(fx / d.mass, fy / d.mass);
+        v = mk(v.x + acc.x * sdt, v.y + acc.y * sdt);
+        if (d.flags & VMAS_F_MAX_SPEED) v = clamp_with_norm(v, d.max_speed);
+        if (d.flags & VMAS_F_V_RANGE) v = mk(tclamp(v.x, -d.v_range, d.v_range), tclamp(v.y, -d.v_range, d.v_range));
+        V2 np = mk(p.x + v.x * sdt, p.y + v.y * sdt);
+        if (has_xs) np.x = tclamp(np.x, -xs, xs);
+        if (has_ys) np.y = tclamp(np.y, -ys, ys);
+        p = np;
+    }
+    if (d.flags & VMAS_F_ROTATABLE) {
+        if (substep == 0) w = w * d.one_minus_drag;
+        w = w + (tq / d.inertia) * sdt;
+        rot = rot + w * sdt;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Ray casts (core.py:1280-1625), one ray against one target.  `o` ray origin, (dc, ds) ray dir.
-VHD float ray_box(V2 o, float ang, float dc, float ds, V2 bp, float brot, float L, float W,
-                  float max_range) {
+VHD Real ray_box(V2 o, Real ang, Real dc, Real ds, V2 bp, Real brot, Real L, Real W,
+                  Real max_range) {
     const V2 po = o - bp;
-    const float nc = cosf(-brot), ns = sinf(-brot);
+    const Real nc = cosf(-brot), ns = sinf(-brot);
     const V2 pa = rotate(po, nc, ns);
     const V2 da = rotate(mk(dc, ds), nc, ns);
     (void)ang;
-    const float tx1 = ((-L) / 2.f - pa.x) / da.x;
-    const float tx2 = (L / 2.f - pa.x) / da.x;
-    float tmn = tmin(tx1, tx2), tmx = tmax(tx1, tx2);
-    const float ty1 = ((-W) / 2.f - pa.y) / da.y;
-    const float ty2 = (W / 2.f - pa.y) / da.y;
-    const float tymn = tmin(ty1, ty2), tymx = tmax(ty1, ty2);
+    const Real tx1 = ((-L) / 2.f - pa.x) / da.x;
+    const Real tx2 = (L / 2.f - pa.x) / da.x;
+    Real tmn = tmin(tx1, tx2), tmx = tmax(tx1, tx2);
+    const Real ty1 = ((-W) / 2.f - pa.y) / da.y;
+    const Real ty2 = (W / 2.f - pa.y) / da.y;
+    const Real tymn = tmin(ty1, ty2), tymx = tmax(ty1, ty2);
     tmn = tmax(tmn, tymn);
     tmx = tmin(tmx, tymx);
     const V2 ia = da * tmn + pa;  // tmin * dir_aabb + pos_aabb
     const V2 iw = rotate(ia, cosf(brot), sinf(brot)) + bp;
     const bool hit = (tmx >= tmn) && (tmn > 0.f);
-    const float d = norm(o - iw);
+    const Real d = norm(o - iw);
     return hit ? d : max_range;
 }
 
-VHD float ray_sphere(V2 o, float dc, float ds, V2 sp, float r, float max_range) {
+VHD Real ray_sphere(V2 o, Real dc, Real ds, V2 sp, Real r, Real max_range) {
     const V2 dir = mk(dc, ds);
     const V2 lp = o + dir * (max_range / 2.f);
     const V2 cp = closest_point_line(lp, dir, 0.f, sp, false);
-    const float dn = norm(sp - cp);
+    const Real dn = norm(sp - cp);
     const bool inter = dn < r;
-    const float a = r * r - dn * dn;
-    const float m = sqrtf((a > 0.f) ? a : 1e-8f);
+    const Real a = r * r - dn * dn;
+    const Real m = sqrtf((a > 0.f) ? a : 1e-8f);
     const V2 u = sp - o;
     const V2 u1 = cp - o;
-    const float udot = u.x * dir.x + u.y * dir.y;
+    const Real udot = u.x * dir.x + u.y * dir.y;
     const bool front = udot > 0.f;
-    const float d = norm(u1) - m;
+    const Real d = norm(u1) - m;
     return (inter && front) ? d : max_range;
 }
 
-VHD float ray_line(V2 o, float dc, float ds, V2 lp, float lrot, float L, float max_range) {
+VHD Real ray_line(V2 o, Real dc, Real ds, V2 lp, Real lrot, Real L, Real max_range) {
     const V2 r = mk(cosf(lrot) * L, sinf(lrot) * L);
     const V2 s = mk(dc, ds);
-    const float rxs = cross(r, s);
+    const Real rxs = cross(r, s);
     const V2 qp = o - lp;
-    const float t = cross(qp, s / rxs);
-    const float u = cross(qp, r / rxs);
-    const float d = norm(mk(u * s.x, u * s.y));
+    const Real t = cross(qp, s / rxs);
+    const Real u = cross(qp, r / rxs);
+    const Real d = norm(mk(u * s.x, u * s.y));
     const bool miss = (rxs == 0.f) || (t > 0.5f) || (t < -0.5f) || (u < 0.f);
     return miss ? max_range : d;
 }
 
-}  // namespace vmas
+}  // namespace VMAS_PHYS_NS

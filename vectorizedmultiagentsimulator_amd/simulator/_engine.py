@@ -60,8 +60,11 @@ def _shape_dims(shape, code):
     return (shape.length,)
 
 
+_GRAD_OK = False  # the step's autograd Function is filling the tables (tensors may require grad)
+
+
 def _check_grad(tensors) -> None:
-    if torch.is_grad_enabled():
+    if torch.is_grad_enabled() and not _GRAD_OK:
         for t in tensors:
             if t is not None and t.requires_grad:
                 raise NotImplementedError(
@@ -545,11 +548,45 @@ class PhysicsEngine:
         self._agent_seen[i] = (force, torque)
         self._agent_keep[i] = (f, t)
 
+    def _needs_grad(self) -> bool:
+        if not torch.is_grad_enabled():
+            return False
+        for e in self.world.entities:
+            st = e._state
+            if st._pos.requires_grad or st._vel.requires_grad or st._rot.requires_grad or st._ang_vel.requires_grad:
+                return True
+        for a in self.world.agents:
+            st = a._state
+            if st._force.requires_grad or st._torque.requires_grad:
+                return True
+        return False
+
     def step(self):
         self._ensure()
+        if self._needs_grad():
+            # autograd through the step: the forward is the native step, the backward the native
+            # vector-Jacobian product (csrc/vmas_grad.hip); the new state tensors are views of the
+            # autograd Function's output
+            inputs = []
+            for e in self.entities:
+                st = e._state
+                inputs += [st._pos, st._vel, st._rot, st._ang_vel]
+            for a in self.agents:
+                inputs += [a._state._force, a._state._torque]
+            out = _StepFn.apply(self, *inputs)
+            self._repoint(out)
+            return
+        out = self._launch()
+        self._repoint(out)
+
+    def _launch(self, grad_ok: bool = False) -> torch.Tensor:
+        """Fill the pointer tables from the current state tensors and run the native step into a
+        fresh output buffer (returned)."""
+        global _GRAD_OK
         w = self.world
         dev = self._dev
         B = w.batch_dim
+        _GRAD_OK = grad_ok
         # pointer tables: only tensors that are not the objects seen last step are re-read
         seen = self._ent_seen
         for i, e in enumerate(self.entities):
@@ -603,10 +640,18 @@ class PhysicsEngine:
                                              ctypes.byref(iters)), "vmas_world_step")
         self._last_iterations = iters.value
         self.steps += 1
-        del keep
+        _GRAD_OK = False
+        self._last_keep = keep
+        return out
 
-        # re-point the integrated fields at views of the fresh buffer (new tensor objects, as the
-        # reference) and update their pointer-table rows in bulk
+    def _repoint(self, out: torch.Tensor) -> None:
+        """Re-point the integrated fields at views of the fresh buffer (new tensor objects, as the
+        reference) and update their pointer-table rows in bulk."""
+        w = self.world
+        B = w.batch_dim
+        base = out.data_ptr()
+        o_pos, o_vel, o_rot, o_ang, o_force, o_torque = self._out_off
+        seen = self._ent_seen
         n_lin, n_rot, n_force, n_torque = self.n_out
         n2, n1 = self._n2, self._n1
         two = out.as_strided((n2, B, 2), (2 * B, 2, 1)).unbind(0) if n2 else ()
@@ -646,6 +691,17 @@ class PhysicsEngine:
     # ---- ray casting ------------------------------------------------------------------------------
     def cast_rays(self, entity, angles: torch.Tensor, max_range: float,
                   entity_filter: Callable, rot_offset: torch.Tensor = None) -> torch.Tensor:
+        if torch.is_grad_enabled():
+            targets = [e for e in self.world.entities if e is not entity and entity_filter(e)]
+            ins = [entity.state.pos, angles, rot_offset]
+            for e in targets:
+                ins += [e.state.pos, e.state.rot]
+            if any(t is not None and t.requires_grad for t in ins):
+                return _RaysFn.apply(self, entity, max_range, entity_filter, len(targets), *ins)
+        return self._cast_rays_native(entity, angles, max_range, entity_filter, rot_offset)
+
+    def _cast_rays_native(self, entity, angles: torch.Tensor, max_range: float,
+                          entity_filter: Callable, rot_offset: torch.Tensor = None) -> torch.Tensor:
         w = self.world
         dev = self._device()
         B = w.batch_dim
@@ -738,7 +794,14 @@ class PhysicsEngine:
             c = self._qrefs[key] = (e, shape, dims, r)
         r = c[3]
         st = e._state
-        p, rot = st._pos, st._rot
+        return self._fill_ref(r, st._pos, st._rot, dev, keep)
+
+    def _ref_from(self, e, p, rot, dev, keep, slot=0) -> N.VmasShapeRef:
+        """_ref with explicit (saved) pos / rot tensors (the distance query's backward)."""
+        r = self._ref(e, dev, [], slot)
+        return self._fill_ref(r, p.detach(), rot.detach(), dev, keep)
+
+    def _fill_ref(self, r, p, rot, dev, keep) -> N.VmasShapeRef:
         if p.dtype is not torch.float32 or p.device != dev:
             p = p.to(device=dev, dtype=torch.float32)
         if rot.dtype is not torch.float32 or rot.device != dev:
@@ -753,6 +816,23 @@ class PhysicsEngine:
         return r
 
     def _query(self, kind, a, b=None, tp=None):
+        global _GRAD_OK
+        if kind == N.OVERLAP_PAIR:  # a bool result: nothing to differentiate
+            prev, _GRAD_OK = _GRAD_OK, True
+            try:
+                return self._query_native(kind, a, b, tp)
+            finally:
+                _GRAD_OK = prev
+        if torch.is_grad_enabled():
+            ins = [a._state._pos, a._state._rot]
+            ins += [b._state._pos, b._state._rot] if b is not None else [None, None]
+            tpt = torch.as_tensor(tp) if tp is not None else None
+            ins.append(tpt)
+            if any(t is not None and t.requires_grad for t in ins):
+                return _DistFn.apply(self, kind, a, b, *ins)
+        return self._query_native(kind, a, b, tp)
+
+    def _query_native(self, kind, a, b=None, tp=None):
         w = self.world
         dev = self._device()
         B = w.batch_dim
@@ -800,3 +880,214 @@ class PhysicsEngine:
     def overlap(self, a, b):
         a, b = self._canonical(a, b)
         return self._query(N.OVERLAP_PAIR, a, b)
+
+
+class _StepFn(torch.autograd.Function):
+    """World.step with autograd: forward = the native step (k_world / k_step / host backend),
+    backward = vmas_world_step_vjp (forward-mode duals through the same physics, contracted
+    with the output gradient; csrc/vmas_grad.hip).  Inputs: every entity's pos / vel / rot /
+    ang_vel, then every agent's force / torque; output: the step's output buffer."""
+
+    @staticmethod
+    def forward(ctx, eng, *inputs):
+        out = eng._launch(grad_ok=True)
+        # the backward reads the inputs through a snapshot of this step's pointer tables
+        ctx.eng = eng
+        ctx.tables = (eng._eio.copy(), eng._aio.copy(), eng._jio.copy(), eng._io.substeps, eng._io.sub_dt,
+                      eng._io.broadphase)
+        ctx.keep = ([list(k) if k is not None else None for k in eng._ent_keep],
+                    [tuple(k) if k is not None else None for k in eng._agent_keep], eng._last_keep)
+        # the backward re-runs the step on the forward's input values: inputs that require grad
+        # are saved (autograd checks their versions), the others are copied (a scenario may edit
+        # them in place after the step, e.g. discovery's target respawn)
+        ctx.grad_mask = [x.requires_grad for x in inputs]
+        ctx.consts = [None if x.requires_grad else x.detach().clone() for x in inputs]
+        ctx.save_for_backward(*[x if x.requires_grad else None for x in inputs])
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        eng = ctx.eng
+        saved = ctx.saved_tensors
+        inputs = [s if s is not None else c for s, c in zip(saved, ctx.consts)]
+        eio, aio, jio, substeps, sub_dt, bp = ctx.tables
+        eio, aio = eio.copy(), aio.copy()
+        dev = eng._dev
+        B = eng.world.batch_dim
+        keep = []
+        for i in range(len(eng.entities)):  # the rows point at the forward's input values
+            pos, vel, rot, ang = (eng._prep(t.detach(), dev) for t in inputs[4 * i: 4 * i + 4])
+            keep += [pos, vel, rot, ang]
+            eio["pos"][i], eio["vel"][i], eio["rot"][i], eio["ang"][i] = pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr()
+            eio["pos_s0"][i], eio["pos_s1"][i] = pos.stride()
+            eio["vel_s0"][i], eio["vel_s1"][i] = vel.stride()
+            eio["rot_s0"][i], eio["ang_s0"][i] = rot.stride(0), ang.stride(0)
+        off = 4 * len(eng.entities)
+        for i in range(len(eng.agents)):
+            f, t = (eng._prep(x.detach(), dev) for x in inputs[off + 2 * i: off + 2 * i + 2])
+            keep += [f, t]
+            aio["force"][i], aio["torque"][i] = f.data_ptr(), t.data_ptr()
+            aio["force_s0"][i], aio["force_s1"][i] = f.stride()
+            aio["torque_s0"][i] = t.stride(0)
+        io = N.VmasStepIO()
+        io.entities, io.agents, io.joints = eio.ctypes.data, aio.ctypes.data, jio.ctypes.data
+        io.substeps, io.sub_dt, io.broadphase = substeps, sub_dt, bp
+        g = gout.to(device=dev, dtype=torch.float32).contiguous()
+        base = g.data_ptr()
+        go = N.VmasStepIO()
+        o_pos, o_vel, o_rot, o_ang, o_force, o_torque = eng._out_off
+        go.out_pos, go.out_vel, go.out_rot = base + 4 * o_pos, base + 4 * o_vel, base + 4 * o_rot
+        go.out_ang_vel, go.out_force, go.out_torque = base + 4 * o_ang, base + 4 * o_force, base + 4 * o_torque
+        E, A = len(eng.entities), len(eng.agents)
+        grads = []
+        ptrs = {k: (ctypes.c_void_p * max(E, 1))() for k in ("pos", "vel", "rot", "ang")}
+        ptrs.update({k: (ctypes.c_void_p * max(A, 1))() for k in ("force", "torque")})
+        for i in range(E):
+            for k, w2, key in ((0, 2, "pos"), (1, 2, "vel"), (2, 1, "rot"), (3, 1, "ang")):
+                t = torch.zeros(B, w2, device=dev, dtype=torch.float32)
+                grads.append(t)
+                ptrs[key][i] = t.data_ptr()
+        for i in range(A):
+            for w2, key in ((2, "force"), (1, "torque")):
+                t = torch.zeros(B, w2, device=dev, dtype=torch.float32)
+                grads.append(t)
+                ptrs[key][i] = t.data_ptr()
+        gio = N.VmasGradIO(*(ctypes.cast(ptrs[k], ctypes.c_void_p) for k in ("pos", "vel", "rot", "ang", "force", "torque")))
+        ed, pd, jd = eng._tables
+        N.check_aux(eng.lib.vmas_world_step_vjp(ctypes.byref(eng._cfg), ed, pd, jd, ctypes.byref(io), ctypes.byref(go),
+                                                ctypes.byref(gio), eng._stream(dev) if eng._dev_index >= 0 else None),
+                    "vmas_world_step_vjp")
+        out = []
+        for t, x, needs in zip(grads, inputs, ctx.grad_mask):
+            out.append(t.reshape(x.shape).to(dtype=x.dtype, device=x.device) if needs else None)
+        return (None, *out)
+
+
+class _DistFn(torch.autograd.Function):
+    """get_distance / get_distance_from_point with autograd: forward = vmas_distance, backward =
+    vmas_distance_vjp (dual numbers through the same closest-point functions)."""
+
+    @staticmethod
+    def forward(ctx, eng, kind, a, b, pa, ra, pb, rb, tp):
+        global _GRAD_OK
+        prev, _GRAD_OK = _GRAD_OK, True
+        try:
+            out = eng._query_native(kind, a, b, tp)
+        finally:
+            _GRAD_OK = prev
+        ctx.eng, ctx.kind, ctx.a, ctx.b = eng, kind, a, b
+        ctx.save_for_backward(pa, ra, pb if pb is not None else torch.empty(0), rb if rb is not None else torch.empty(0),
+                              tp if tp is not None else torch.empty(0))
+        ctx.has_b, ctx.has_tp = pb is not None, tp is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        eng, kind = ctx.eng, ctx.kind
+        pa, ra, pb, rb, tp = ctx.saved_tensors
+        dev = eng._device()
+        B = eng.world.batch_dim
+        keep = []
+        refa = N.VmasShapeRef()
+        ctypes.memmove(ctypes.byref(refa), ctypes.byref(eng._ref_from(ctx.a, pa, ra, dev, keep, 0)), ctypes.sizeof(refa))
+        refb = None
+        if ctx.has_b:
+            refb = N.VmasShapeRef()
+            ctypes.memmove(ctypes.byref(refb), ctypes.byref(eng._ref_from(ctx.b, pb, rb, dev, keep, 1)), ctypes.sizeof(refb))
+        tptr, t0, t1 = None, 0, 0
+        if ctx.has_tp:
+            t = eng._prep(tp.detach(), dev)
+            if t.dim() == 1:
+                t = t.unsqueeze(0)
+            t = t.expand(B, 2)
+            keep.append(t)
+            tptr, t0, t1 = t.data_ptr(), t.stride(0), t.stride(1)
+        g = gout.detach().to(device=dev, dtype=torch.float32).contiguous()
+        z = lambda n: torch.zeros(B, n, device=dev, dtype=torch.float32)  # noqa: E731
+        ga_p, ga_r, gb_p, gb_r, gt = z(2), z(1), z(2), z(1), z(2)
+        N.check_aux(eng.lib.vmas_distance_vjp(
+            eng._native_device(dev), B, kind, ctypes.byref(refa), ctypes.byref(refb) if refb is not None else None,
+            tptr, t0, t1, g.data_ptr(), ga_p.data_ptr(), ga_r.data_ptr(), gb_p.data_ptr(), gb_r.data_ptr(),
+            gt.data_ptr(), eng._stream(dev)), "vmas_distance_vjp")
+        if eng._native_device(dev) >= 0:
+            torch.cuda.current_stream(dev).synchronize()
+
+        def fit(gr, x):
+            if x is None or x.numel() == 0 or not x.requires_grad:
+                return None
+            return gr.reshape(x.shape).to(dtype=x.dtype, device=x.device) if gr.numel() == x.numel() else \
+                gr.sum(0).reshape(x.shape).to(dtype=x.dtype, device=x.device)
+
+        return (None, None, None, None, fit(ga_p, pa), fit(ga_r, ra), fit(gb_p, pb) if ctx.has_b else None,
+                fit(gb_r, rb) if ctx.has_b else None, fit(gt, tp) if ctx.has_tp else None)
+
+
+class _RaysFn(torch.autograd.Function):
+    """World.cast_rays with autograd: forward = vmas_cast_rays, backward = vmas_cast_rays_vjp."""
+
+    @staticmethod
+    def forward(ctx, eng, entity, max_range, entity_filter, n_targets, origin, angles, rot_offset, *tpr):
+        global _GRAD_OK
+        prev, _GRAD_OK = _GRAD_OK, True
+        try:
+            out = eng._cast_rays_native(entity, angles, max_range, entity_filter, rot_offset)
+        finally:
+            _GRAD_OK = prev
+        ctx.eng, ctx.max_range, ctx.nt = eng, max_range, n_targets
+        ctx.targets = [e for e in eng.world.entities if e is not entity and entity_filter(e)]
+        ctx.has_rot = rot_offset is not None
+        ctx.save_for_backward(origin, angles, rot_offset if rot_offset is not None else torch.empty(0), *tpr)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        eng = ctx.eng
+        saved = ctx.saved_tensors
+        origin, angles, rot = saved[0], saved[1], saved[2]
+        tpr = saved[3:]
+        dev = eng._device()
+        B = eng.world.batch_dim
+        keep = []
+        o = eng._prep(origin.detach(), dev)
+        ang = eng._prep(angles.detach(), dev)
+        if ang.dim() == 1:
+            ang = ang.unsqueeze(-1)
+        R = ang.shape[-1]
+        rptr, rs0 = None, 0
+        if ctx.has_rot:
+            r = eng._prep(rot.detach(), dev)
+            keep.append(r)
+            rptr, rs0 = r.data_ptr(), r.stride(0)
+        tg = eng._ray_table(ctx.targets).copy()
+        ps = [eng._prep(tpr[2 * i].detach(), dev) for i in range(ctx.nt)]
+        rs = [eng._prep(tpr[2 * i + 1].detach(), dev) for i in range(ctx.nt)]
+        keep += ps + rs + [o, ang]
+        if ctx.nt:
+            tg["pos"] = [p.data_ptr() for p in ps]
+            tg["rot"] = [x.data_ptr() for x in rs]
+            tg["pos_s0"] = [p.stride(0) for p in ps]
+            tg["pos_s1"] = [p.stride(1) for p in ps]
+            tg["rot_s0"] = [x.stride(0) for x in rs]
+        g = gout.detach().to(device=dev, dtype=torch.float32).contiguous()
+        z = lambda *shape: torch.zeros(*shape, device=dev, dtype=torch.float32)  # noqa: E731
+        g_o, g_r, g_a = z(B, 2), z(B, 1), z(B, R)
+        g_tp = [z(B, 2) for _ in range(ctx.nt)]
+        g_tr = [z(B, 1) for _ in range(ctx.nt)]
+        arr_p = (ctypes.c_void_p * max(ctx.nt, 1))(*[t.data_ptr() for t in g_tp])
+        arr_r = (ctypes.c_void_p * max(ctx.nt, 1))(*[t.data_ptr() for t in g_tr])
+        N.check_aux(eng.lib.vmas_cast_rays_vjp(
+            eng._native_device(dev), B, R, o.data_ptr(), o.stride(0), o.stride(1), ang.data_ptr(), ang.stride(0),
+            ang.stride(1), rptr, rs0, tg.ctypes.data, ctx.nt, _f32(ctx.max_range), g.data_ptr(), g_o.data_ptr(),
+            g_r.data_ptr(), g_a.data_ptr(), arr_p, arr_r, eng._stream(dev)), "vmas_cast_rays_vjp")
+
+        def fit(gr, x):
+            if x is None or x.numel() == 0 or not x.requires_grad:
+                return None
+            if gr.numel() != x.numel():
+                gr = gr.sum(0)
+            return gr.reshape(x.shape).to(dtype=x.dtype, device=x.device)
+
+        out = [None, None, None, None, None, fit(g_o, origin), fit(g_a, angles), fit(g_r, rot) if ctx.has_rot else None]
+        for i in range(ctx.nt):
+            out += [fit(g_tp[i], tpr[2 * i]), fit(g_tr[i], tpr[2 * i + 1])]
+        return tuple(out)

@@ -30,7 +30,10 @@ _OFF_DEPTH = [0]
 
 
 def enabled(world) -> bool:
-    return _ON and _OFF_DEPTH[0] == 0 and torch.device(world.device).type == "cuda"
+    if not _ON or _OFF_DEPTH[0] or torch.device(world.device).type != "cuda":
+        return False
+    # autograd (Environment(grad_enabled=True)): the programs have no backward
+    return not (getattr(world, "_grad_enabled", False) and torch.is_grad_enabled())
 
 
 class disabled:

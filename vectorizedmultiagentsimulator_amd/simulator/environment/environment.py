@@ -123,6 +123,10 @@ class Environment(TorchVectorizedObject):
         self.dict_spaces = dict_spaces
         self.clamp_action = clamp_actions
         self.grad_enabled = grad_enabled
+        # grad_enabled: the world step, ray casts and distance queries run through their native
+        # backward (simulator/_engine.py _StepFn / _RaysFn / _DistFn); the fused scenario programs
+        # (no backward) give way to the scenarios' torch programs
+        self.world._grad_enabled = bool(grad_enabled)
         self._apply_cache = None  # see _apply_continuous_actions
         self._u_persist = None  # persistent action buffer of graph mode (see _apply_continuous_actions)
         self._spec_keep = None  # action tensors a speculative action launch reads
@@ -138,6 +142,8 @@ class Environment(TorchVectorizedObject):
         if graph_step:
             if self.device.type != "cuda":
                 raise ValueError("graph_step=True needs a ROCm device (HIP graphs)")
+            if grad_enabled:
+                raise ValueError("graph_step=True replays a captured step: it cannot carry autograd (grad_enabled=True)")
             from ._graph import StepGraph
 
             self._graph = StepGraph(self)
