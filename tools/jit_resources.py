@@ -30,6 +30,9 @@ def main():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                "-fno-fast-math", "-I", str(inc), "-I", str(ROOT / "include"), "--cuda-device-only", "-c",
                "-Rpass-analysis=kernel-resource-usage", str(f), "-o", str(Path(d) / "world.o")]
+        for line in src.splitlines():  # the options compile() reads from the source
+            if line.startswith("// vmas-cflags:"):
+                cmd[5:5] = line.split(":", 1)[1].split()
         out = subprocess.run(cmd, capture_output=True, text=True)
         for line in out.stderr.splitlines():
             if "remark" in line:

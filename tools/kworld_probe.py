@@ -47,3 +47,42 @@ if os.environ.get("VMAS_JIT_PROFILE"):
     span = t[S * 4 - 1].max() - t[ms_sub * 4].min()
     print(f"profiled workgroup: {span} cycles from prologue end to last release; "
           f"{span / (1e3 * ms / max(n, 1)) / 1e3:.2f} GHz at the event time")
+    # per-workgroup records (start / group start / group end / leave, s_memrealtime; HW_ID, XCC_ID)
+    base = (ms_sub * 4 + 2) * 16
+    rec = t_full = eng.jit_profile().astype(np.int64)
+    blk = t_full.reshape(-1)[base:].reshape(-1, 8)
+    G = abs(eng.jit_grid)
+    blk = blk[:G]
+    t0 = blk[:, 0].min()
+    mhz = 100.0  # s_memrealtime ticks at 100 MHz
+    start, gs, ge, leave = [(blk[:, k] - t0) / mhz for k in (0, 4, 5, 3)]
+    hw, xcc = blk[:, 1], blk[:, 2]
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    print(f"workgroups {G}: start spread {start.min():.2f}-{start.max():.2f} us; group time "
+          f"{np.percentile(ge - gs, [0, 50, 100]).round(2).tolist()} us; leave {leave.min():.2f}-{leave.max():.2f} us")
+    keys = xcc * 1000 + se * 100 + cu
+    _, counts = np.unique(keys, return_counts=True)
+    print(f"distinct (xcc, se, cu): {len(counts)}; workgroups per CU histogram: {np.bincount(counts).tolist()}")
+    order = np.argsort(start)
+    print("start times (us) by decile:", np.percentile(start, [0, 10, 25, 50, 75, 90, 100]).round(2).tolist())
+    print("group start (us) deciles:", np.percentile(gs, [0, 10, 25, 50, 75, 90, 100]).round(2).tolist())
+    print("group end (us) deciles:", np.percentile(ge, [0, 10, 25, 50, 75, 90, 100]).round(2).tolist())
+    gt = ge - gs
+    c0, c1 = [(blk[:, k] - t0) / mhz for k in (6, 7)]
+    print("claim CAS (us) deciles:", np.percentile(c1 - c0, [0, 10, 50, 90, 100]).round(2).tolist(),
+          "; start -> claim issue:", np.percentile(c0 - start, [0, 50, 100]).round(2).tolist(),
+          "; claim done -> group start:", np.percentile(gs - c1, [0, 50, 100]).round(2).tolist())
+    for x in np.unique(xcc):
+        m = xcc == x
+        print(f"  xcc {x}: {int(m.sum())} workgroups, group time mean {gt[m].mean():.2f} max {gt[m].max():.2f} us, "
+              f"group start mean {gs[m].mean():.2f} us")
+    slow = np.argsort(gt)[-8:]
+    print("slowest groups (block, start, time):", [(int(i), round(float(gs[i]), 2), round(float(gt[i]), 2)) for i in slow])
+    # the two workgroups sharing a CU: their group times
+    pair_t = {}
+    for i, k in enumerate(keys):
+        pair_t.setdefault(int(k), []).append(float(gt[i]))
+    both = np.array([sorted(v) for v in pair_t.values() if len(v) == 2])
+    if len(both):
+        print(f"CU pairs: faster member mean {both[:, 0].mean():.2f}, slower member mean {both[:, 1].mean():.2f} us")

@@ -101,6 +101,24 @@ std::string bl(bool v) { return v ? "true" : "false"; }
 // tolerance (tests/test_gpu_parity.py, full size included), not bit-identical to k_step.
 // Measured on balance 32 768 x 10 substeps: k_world 66.3 -> 51.8 us.
 constexpr const char* kRelaxedTag = "// vmas-math: relaxed";
+// The generated source carries its own code-generation options on this line (compile() reads
+// them from there), so the source text -- and its sha256, which keys the bench's PMC record --
+// pins the code object.
+constexpr const char* kFlagsTag = "// vmas-cflags:";
+
+// -fno-slp-vectorize: the SLP vectoriser pairs independent scalar ops of the per-lane physics
+// into v_pk_add/v_pk_mul_f32, which on gfx950 costs more than it saves: register-pair moves
+// (v_mov) and hazard s_nops around the packed ops (balance C2: 4490 -> 4905 VALU in the substep
+// loops but 395 -> 123 s_nop, 494 -> 172 v_mov; k_world 55.4 -> 48.8 us,
+// profiles/r02/run9_noslp).  Packed ops round per element, so results are unchanged.
+// Relaxed worlds add the approximate-function / fast divide-sqrt options.  VMAS_JIT_CFLAGS
+// (space separated) appends options for A/B measurements.
+std::string codegen_flags(bool relaxed) {
+    std::string f = " -fno-slp-vectorize";
+    if (relaxed) f += " -fapprox-func -fno-hip-fp32-correctly-rounded-divide-sqrt";
+    if (const char* x = getenv("VMAS_JIT_CFLAGS")) f += std::string(" ") + x;
+    return f;
+}
 
 
 // Largest float x with sqrtf(x) <= r (sqrtf correctly rounded on both the host and gfx950 with
@@ -118,6 +136,7 @@ float sq_limit(float r) {
 
 constexpr int kNW = 8;      // waves per workgroup (VMAS_JIT_WAVES overrides: 8 or 16)
 constexpr int kMaxNW = 16;  // column stride of the phase-profile buffer
+constexpr int kProfBlocks = 4096;  // workgroups with a per-workgroup record in profile builds
 constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
 constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
 constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
@@ -380,6 +399,14 @@ struct Gen {
         if (prof_block < 0) return "";
         return "if ((b >> 6) == " + it(prof_block) + " && lane == 0) a.prof[(" + slot + ") * " + it(kMaxNW) + " + " +
                it(w) + "] = __builtin_amdgcn_s_memtime();\n";
+    }
+
+    // per-workgroup record (profile builds): slot 0 start (s_memrealtime), 1 HW_ID, 2 XCC_ID,
+    // 3 leaving the group loop, 4 / 5 start / end of its last group; after the phase stamps
+    std::string block_stamp(int k, const std::string& v) const {
+        if (prof_block < 0) return "";
+        return "    if (threadIdx.x == 0 && blockIdx.x < " + it(kProfBlocks) + ") a.prof[" +
+               it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + " + blockIdx.x * 8 + " + it(k) + "] = " + v + ";\n";
     }
 
     std::string desc(int e) const {
@@ -671,7 +698,9 @@ struct Gen {
     void generate() {
         std::string& o = src;
         o += "// generated by vmas_jit.hip for one world\n";
-        if (relaxed) o += std::string(kRelaxedTag) + "\n";
+        if (relaxed) o += std::string(kRelaxedTag) + "\n#define VMAS_PHYS_RELAXED 1\n";
+        o += std::string(kFlagsTag) + codegen_flags(relaxed) + "\n";
+        if (prof_block >= 0) o += "#define VMAS_JIT_PROFILE_SLOTS 1\n";
         o += "#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
@@ -739,10 +768,13 @@ struct Gen {
              "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n"
-             "    __syncthreads();\n"
+             "    __syncthreads();\n" +
+             block_stamp(0, "__builtin_amdgcn_s_memrealtime()") + block_stamp(1, "__builtin_amdgcn_s_getreg(63492)") +
+             block_stamp(2, "__builtin_amdgcn_s_getreg(30740)") +
+             (prof_block >= 0 ? "    if (threadIdx.x == 0) vmas_prof_blk = a.prof + " + it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + ";\n" : "") +
              "    for (;;) {\n"
              "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, &CUR, QL);\n"
-             "        if (g < 0) break;\n"
+             "        if (g < 0) break;\n" + block_stamp(4, "__builtin_amdgcn_s_memrealtime()") +
              "        if (persistent) {\n"
              "            for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "            __syncthreads();\n"
@@ -757,8 +789,8 @@ struct Gen {
         o += "                default: break;\n            }\n        }\n";
         o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, a.ctl, a.err, a.herr, nwords, ngrp, CUR.pass,\n"
              "                                      a.max_pass, RED, &QL[65]))\n"
-             "            poison_outputs(a);\n"
-             "    }\n"
+             "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
+             "    }\n" + block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
              "    if (!persistent) {\n"
              "        if (!a.blk) return;\n"
              "        __syncthreads();\n"
@@ -875,10 +907,23 @@ int32_t compile(const std::string& src, std::vector<char>* code) {
     const std::string inc1 = "-I" + dir + "/csrc", inc2 = "-I" + dir + "/../include";
     std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                                      inc1.c_str(), inc2.c_str()};
-    if (src.find(kRelaxedTag) != std::string::npos) {
-        opts.push_back("-fapprox-func");
-        opts.push_back("-fno-hip-fp32-correctly-rounded-divide-sqrt");
+    // the code-generation options the generator wrote into the source (kFlagsTag line)
+    std::vector<std::string> extra;
+    const size_t at = src.find(kFlagsTag);
+    if (at != std::string::npos) {
+        const size_t b = at + strlen(kFlagsTag), e = src.find('\n', b);
+        const std::string line = src.substr(b, e == std::string::npos ? std::string::npos : e - b);
+        std::string t;
+        for (char c : line + " ") {
+            if (c == ' ') {
+                if (!t.empty()) extra.push_back(t);
+                t.clear();
+            } else {
+                t += c;
+            }
+        }
     }
+    for (const std::string& x : extra) opts.push_back(x.c_str());
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "vmas_world.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return jfail(VMAS_E_HIP, "hiprtcCreateProgram failed");
@@ -916,7 +961,7 @@ struct VmasJitWorld {
     hipFunction_t fn = nullptr;  // k_world
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
     // persistent launches: d_ctl = [kGridCtlWords control words | inverted mask words | claim word
-    // per group], zeroed at create and reset by the kernel's last workgroup;
+    // per group, kClaimStride apart], zeroed at create and reset by the kernel's last workgroup;
     // d_err: sticky error bits; h_err: mapped host word the kernel stores them into (dh_err: its
     // device address)
     uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr, *dh_err = nullptr;
@@ -1027,7 +1072,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
-    const size_t ctl_words = vmas::kGridCtlWords + nwords + (size_t)W->nblk;
+    const size_t ctl_words = vmas::kGridCtlWords + nwords + (size_t)W->nblk * vmas::kClaimStride;
     if (hipMalloc((void**)&W->d_ctl, ctl_words * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_err, 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W->dh_err, W->h_err, 0) != hipSuccess ||
@@ -1059,7 +1104,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
     }
     if (g.prof_block >= 0) {
-        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW;
+        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW + (size_t)kProfBlocks * 8;
         if (hipMalloc((void**)&W->d_prof, W->n_prof * 8) != hipSuccess ||
             hipMemset(W->d_prof, 0, W->n_prof * 8) != hipSuccess)
             return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc profile buffer"));

@@ -22,11 +22,13 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 // assumes that the workgroups of the launch are co-resident.
 //
 //   * Work items are the 64-env groups.  Group g is claimed for pass p by a compare-and-swap of
-//     claim[g] from p to p + 1 (one word per group: no contended counter).  A workgroup first
-//     claims its own groups (g = blockIdx.x + k * gridDim.x), then, unless the claim counters
-//     (sharded g % 8) say every group is taken, scans for groups still unclaimed in this pass
-//     and steals them (normally none: every workgroup has started long before the first one
-//     finishes).
+//     claim[g] from p to p + 1 (one word per group, each on its own 128-byte line: no contended
+//     address).  A workgroup first claims its own groups (g = blockIdx.x + k * gridDim.x), then
+//     scans the claim words for groups still unclaimed in this pass and steals them (normally
+//     none: every workgroup has started long before the first one finishes).  Claims are never
+//     taken back within a pass, so a scan that sees no unclaimed group proves that every group
+//     is claimed: no claim counter (its adds, 64 per address at 32 768 envs, serialised at the
+//     memory side and delayed the first group of every workgroup by 2-6 us).
 //   * Processing a group ends with its R/Z activity row stored in blk[g] and one completion on a
 //     two-level counter (shard g % 32, one 128-byte line each, then the top counter; cumulative
 //     over the passes of a step).  The workgroup whose completion is the last of the
@@ -56,11 +58,11 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 // workgroups arriving together on one address serialise at the memory side: 32 shards):
 // [0] top completion counter, [1] top exit counter, [2] passes run by the last step,
 // [32 * (1 + k)] completion shard k (groups g % 32 == k, cumulative over the passes of a step),
-// [32 * (33 + k)] exit shard k (workgroups blockIdx % 32 == k), [32 * (65 + k)] claim shard k
-// (groups g % 8 == k), [32 * 73 + p] dec[p] (p < kGridMaxPasses); then the mask words (nwords)
-// and the claim words (one per group).
+// [32 * (33 + k)] exit shard k (workgroups blockIdx % 32 == k), [32 * 65 .. 32 * 73) unused,
+// [32 * 73 + p] dec[p] (p < kGridMaxPasses); then the mask words (nwords) and the claim words
+// (one per group, kClaimStride apart).
 constexpr int kGridMaxPasses = 64, kGridShards = 32;
-constexpr int kGridDone = 32, kGridExit = 32 * 33, kGridClaimed = 32 * 65, kGridDec = 32 * 73;
+constexpr int kGridDone = 32, kGridExit = 32 * 33, kGridDec = 32 * 73;
 constexpr int kGridCtlWords = kGridDec + kGridMaxPasses;
 
 // Two-level sharded arrival: add one to shard (i % kGridShards) of `base`; the arrival that
@@ -125,48 +127,35 @@ __device__ __forceinline__ void report_err(uint32_t* err, uint32_t* herr, uint32
     if (herr) __hip_atomic_store(herr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Claim group g for pass `pass` (one thread): claim[g] p -> p + 1, counted on the claim
-// sub-counter g % 8 (cumulative over the passes of a step).  A workgroup's own groups are
-// normally free: one compare-and-swap, no load first.
-__device__ __forceinline__ bool grid_claim(uint32_t* ctl, uint32_t* claim, int g, int pass) {
-    if (!cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) return false;
-    (void)add_agent(&ctl[kGridClaimed + 32 * (g & 7)], 1u);
-    return true;
+// Claim words: one per group, each on a 128-byte line of its own (the claims of hundreds of
+// workgroups arriving together serialise per line at the memory side).
+constexpr int kClaimStride = 32;
+
+// Claim group g for pass `pass` (one thread): claim[g] p -> p + 1.  A workgroup's own groups are
+// normally free: one compare-and-swap, no load first and no counter.
+__device__ __forceinline__ bool grid_claim(uint32_t* claim, int g, int pass) {
+    return cas_agent(&claim[(size_t)g * kClaimStride], (uint32_t)pass, (uint32_t)pass + 1u);
 }
 
-// Whether every group of `pass` is claimed (all threads; 8 loads).
-__device__ __forceinline__ bool grid_all_claimed(uint32_t* ctl, int ngrp, int pass, uint32_t* FLAG) {
-    if (threadIdx.x == 0) *FLAG = 0u;
-    __syncthreads();
-    if ((int)threadIdx.x < 8 && (int)threadIdx.x < ngrp) {
-        const uint32_t k = threadIdx.x, n_k = ((uint32_t)ngrp + 7u - k) / 8u;
-        if (ld_agent(&ctl[kGridClaimed + 32 * k]) != n_k * (uint32_t)(pass + 1)) atomicOr(FLAG, 1u);
-    }
-    __syncthreads();
-    const bool all = *FLAG == 0u;
-    __syncthreads();
-    return all;
-}
-
-// Steal round (all threads): claim up to 64 groups still unclaimed in `pass`; returns the count,
-// groups in LIST[0..count).  LIST: 65 words of LDS.  A claim beyond the list is put back.
-__device__ __forceinline__ int grid_steal(uint32_t* ctl, uint32_t* claim, int ngrp, int pass, uint32_t* LIST) {
+// Steal round (all threads): scan the claim words of `pass` and claim up to 64 groups still
+// unclaimed.  LIST: 65 words of LDS; returns the number of entries in LIST[0..n) (an entry whose
+// claim lost a race holds ~0u) and sets *seen when any unclaimed group was seen.  Claims are
+// never taken back within a pass, so a scan that sees none unclaimed proves every group of the
+// pass is claimed (by a running workgroup, which will complete it).
+__device__ __forceinline__ int grid_steal(uint32_t* claim, int ngrp, int pass, uint32_t* LIST, bool* seen) {
     if (threadIdx.x == 0) LIST[64] = 0u;
     __syncthreads();
-    for (int g = (int)threadIdx.x; g < ngrp; g += (int)blockDim.x)
-        if (ld_agent(&claim[g]) == (uint32_t)pass && cas_agent(&claim[g], (uint32_t)pass, (uint32_t)pass + 1u)) {
-            const uint32_t i = atomicAdd(&LIST[64], 1u);
-            if (i < 64u) {
-                LIST[i] = (uint32_t)g;
-                (void)add_agent(&ctl[kGridClaimed + 32 * (g & 7)], 1u);
-            } else {
-                st_agent(&claim[g], (uint32_t)pass);
-            }
-        }
+    for (int g = (int)threadIdx.x; g < ngrp; g += (int)blockDim.x) {
+        uint32_t* w = &claim[(size_t)g * kClaimStride];
+        if (ld_agent(w) != (uint32_t)pass) continue;
+        const uint32_t i = atomicAdd(&LIST[64], 1u);  // reserve a slot before claiming
+        if (i < 64u) LIST[i] = cas_agent(w, (uint32_t)pass, (uint32_t)pass + 1u) ? (uint32_t)g : ~0u;
+    }
     __syncthreads();
-    const int n = LIST[64] < 64u ? (int)LIST[64] : 64;
+    const uint32_t r = LIST[64];
     __syncthreads();
-    return n;
+    *seen = r != 0u;
+    return r < 64u ? (int)r : 64;
 }
 
 // Completion of group g in `pass` (all threads; the group's row and outputs are stored).
@@ -250,6 +239,11 @@ __device__ __forceinline__ bool grid_wait(const uint32_t* ctl, int pass, uint32_
     return more;
 }
 
+#ifdef VMAS_JIT_PROFILE_SLOTS
+// profile builds: the per-workgroup record array (set by the kernel's prologue)
+__device__ unsigned long long* vmas_prof_blk;
+#endif
+
 // Per-workgroup cursor of the persistent launch (LDS; thread 0 writes it, behind barriers).
 struct GridCursor {
     int pass, own, nl, il;
@@ -257,8 +251,8 @@ struct GridCursor {
 
 // The next group this workgroup processes, or -1 once the step is done (all threads).  Host-driven
 // launches (persistent false): the workgroup's own groups.  Persistent launches: own groups
-// claimed for the current pass, then the steal list, then steal rounds while the claim counters
-// say a group is unclaimed, then the pass decision -- another pass restarts the cursor and
+// claimed for the current pass, then the steal list, then steal rounds while a scan sees an
+// unclaimed group, then the pass decision -- another pass restarts the cursor and
 // reloads MSK from the (inverted) mask words.  Not inlined: its loop-invariant addresses would be
 // hoisted around the group body and spill its registers (measured: +125 SGPR spills on balance).
 __device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ctl, uint32_t* claim, const uint32_t* mask,
@@ -273,7 +267,13 @@ __device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ct
                 g = own;
                 break;
             }
-            if (threadIdx.x == 0) QL[65] = grid_claim(ctl, claim, own, c.pass) ? 1u : 0u;
+#ifdef VMAS_JIT_PROFILE_SLOTS
+            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
+            if (threadIdx.x == 0) QL[65] = grid_claim(claim, own, c.pass) ? 1u : 0u;
+#ifdef VMAS_JIT_PROFILE_SLOTS
+            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
             __syncthreads();
             const bool mine = QL[65] != 0u;
             __syncthreads();
@@ -284,19 +284,21 @@ __device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ct
         } else if (!persistent) {
             break;
         } else if (c.il < c.nl) {
-            g = (int)QL[c.il++];
-            break;
-        } else if (!grid_all_claimed(ctl, ngrp, c.pass, &QL[65])) {
-            c.nl = grid_steal(ctl, claim, ngrp, c.pass, QL);
+            const uint32_t q = QL[c.il++];
+            if (q != ~0u) {
+                g = (int)q;
+                break;
+            }
+        } else {
+            bool seen;
+            c.nl = grid_steal(claim, ngrp, c.pass, QL, &seen);
             c.il = 0;
-            if (c.nl == 0) __builtin_amdgcn_s_sleep(2);
-        } else if (grid_wait(ctl, c.pass, &QL[65])) {
+            if (seen) continue;  // stolen groups in QL (or lost races: scan again)
+            if (!grid_wait(ctl, c.pass, &QL[65])) break;
             ++c.pass;
             c.own = (int)blockIdx.x;
             c.nl = c.il = 0;
             for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&mask[i]);
-        } else {
-            break;
         }
     }
     __syncthreads();
@@ -325,13 +327,12 @@ __device__ __forceinline__ void grid_exit(uint32_t* ctl, uint32_t* nmask, uint32
     __syncthreads();
     if (*FLAG == 0u) return;
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
-    for (int g = threadIdx.x; g < ngrp; g += blockDim.x) st_agent(&claim[g], 0u);
+    for (int g = threadIdx.x; g < ngrp; g += blockDim.x) st_agent(&claim[(size_t)g * kClaimStride], 0u);
     for (int p = threadIdx.x; p < max_pass; p += blockDim.x) st_agent(&ctl[kGridDec + p], 0u);
     const int t = (int)threadIdx.x;
     if (t < 2) st_agent(&ctl[t], 0u);
     if (t >= 64 && t < 64 + kGridShards) st_agent(&ctl[kGridDone + 32 * (t - 64)], 0u);
     if (t >= 128 && t < 128 + kGridShards) st_agent(&ctl[kGridExit + 32 * (t - 128)], 0u);
-    if (t >= 192 && t < 200) st_agent(&ctl[kGridClaimed + 32 * (t - 192)], 0u);
     if (tm && t == 0) {  // the launch's span: workgroup 0's start -> the last workgroup out
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long c1 = __builtin_amdgcn_s_memtime();

@@ -76,18 +76,37 @@ VHD Real tclamp(Real x, Real lo, Real hi) { return (x >= lo && x <= hi) ? x : tm
 VHD Real tclamp(Real x, Real lo, Real hi) { return tmin(tmax(x, lo), hi); }
 #endif
 
+// Transcendentals.  Relaxed builds (VMAS_PHYS_RELAXED: the world-specialised kernels of jointless
+// worlds, csrc/vmas_jit.hip relaxed_math) use the hardware instructions: v_sin/v_cos_f32 for the
+// entity trig and Kahan's log1p(y) = log(u) * y / (u - 1), u = 1 + y, with v_log_f32 for the
+// soft-contact penetration (y = exp(-|x|) in (0, 1]) -- a few ulp instead of ocml's
+// double-float log1pf (~110 VALU instructions per contact) and its range-reduced sin/cos
+// (~100 each).  Every other build keeps the correctly rounded library functions.
+#ifdef VMAS_PHYS_RELAXED
+VHD Real tsin(Real x) { return __sinf(x); }
+VHD Real tcos(Real x) { return __cosf(x); }
+VHD Real tlog1p(Real y) {
+    const Real u = 1.f + y;
+    return u == 1.f ? y : __logf(u) * (y / (u - 1.f));
+}
+#else
+VHD Real tsin(Real x) { return sinf(x); }
+VHD Real tcos(Real x) { return cosf(x); }
+VHD Real tlog1p(Real y) { return log1pf(y); }
+#endif
+
 // Angle trig of one entity: cos/sin(rot) and cos/sin(rot + pi/2) (physics.py:299-301)
 struct Trig {
     Real c0, s0, c1, s1;
 };
 VHD Trig make_trig(Real rot) {
     const Real r2 = rot + kHalfPi;
-    return Trig{cosf(rot), sinf(rot), cosf(r2), sinf(r2)};
+    return Trig{tcos(rot), tsin(rot), tcos(r2), tsin(r2)};
 }
 // Lines and joint anchors only use cos/sin(rot); boxes also use the side normal rot + pi/2.
 VHD Trig make_trig_for(Real rot, bool box) {
     if (box) return make_trig(rot);
-    return Trig{cosf(rot), sinf(rot), 0.f, 0.f};
+    return Trig{tcos(rot), tsin(rot), 0.f, 0.f};
 }
 
 // Wave-uniform vote used for exact early-outs: on gfx950 true iff the predicate holds in every
@@ -111,7 +130,7 @@ VHD Real clamp_with_norm1(Real t, Real max_norm) {  // [B,1] variant: norm = |t|
 // torch.logaddexp(0, x) (ATen logaddexp kernel: m + log1p(exp(-|a-b|)))
 VHD Real logaddexp0(Real x) {
     const Real m = tmax(0.f, x);
-    return m + log1pf(expf(-fabsf(0.f - x)));
+    return m + tlog1p(expf(-fabsf(0.f - x)));
 }
 
 // World._get_constraint_forces (core.py:2804-2838).  Returns the force on a; b gets -force.
