@@ -50,7 +50,7 @@ if os.environ.get("VMAS_JIT_PROFILE"):
     # per-workgroup records (start / group start / group end / leave, s_memrealtime; HW_ID, XCC_ID)
     base = (ms_sub * 4 + 2) * 16
     rec = t_full = eng.jit_profile().astype(np.int64)
-    blk = t_full.reshape(-1)[base:].reshape(-1, 8)
+    blk = t_full.reshape(-1)[base:].reshape(-1, 24)
     G = abs(eng.jit_grid)
     blk = blk[:G]
     t0 = blk[:, 0].min()
@@ -86,3 +86,9 @@ if os.environ.get("VMAS_JIT_PROFILE"):
     both = np.array([sorted(v) for v in pair_t.values() if len(v) == 2])
     if len(both):
         print(f"CU pairs: faster member mean {both[:, 0].mean():.2f}, slower member mean {both[:, 1].mean():.2f} us")
+    simd = (blk[:, 8:16] >> 4) & 3
+    print("SIMD of waves 0-7, first 4 workgroups:", simd[:4].tolist())
+    cnt = {}
+    for row in simd:
+        cnt[tuple(row.tolist())] = cnt.get(tuple(row.tolist()), 0) + 1
+    print("wave->SIMD patterns:", sorted(cnt.items(), key=lambda x: -x[1])[:4])

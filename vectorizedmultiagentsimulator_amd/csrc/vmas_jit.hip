@@ -137,6 +137,7 @@ float sq_limit(float r) {
 constexpr int kNW = 8;      // waves per workgroup (VMAS_JIT_WAVES overrides: 8 or 16)
 constexpr int kMaxNW = 16;  // column stride of the phase-profile buffer
 constexpr int kProfBlocks = 4096;  // workgroups with a per-workgroup record in profile builds
+constexpr int kProfRec = 24;       // words per record (16 waves' HW_ID at most)
 constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
 constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
 constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
@@ -255,6 +256,10 @@ struct Gen {
         // VMAS_JIT_FINISH_LPT=0 override (A/B).
         float kCost[7] = {1.5f, 0.5f, 2.0f, 1.8f, 2.2f, 7.4f, 30.f};
         float finish_cost = 3.0f;
+        // (measured and rejected, profiles/r02/run10_sched: a table rescaled to relaxed-math VALU
+        // counts and SIMD-aware placement (waves w and w + 4 share a SIMD) -- balance C2 k_world
+        // 40.8 -> 42.6-45.7 us: the two workgroups on a CU map waves to SIMDs with different
+        // rotations, so per-SIMD sums even out, and the per-wave makespan is what binds)
         if (const char* c = getenv("VMAS_JIT_COST_SS")) kCost[VMAS_PAIR_SS] = (float)atof(c);
         if (const char* c = getenv("VMAS_JIT_COST_FINISH")) finish_cost = (float)atof(c);
         const char* fl_lpt = getenv("VMAS_JIT_FINISH_LPT");
@@ -401,12 +406,14 @@ struct Gen {
                it(w) + "] = __builtin_amdgcn_s_memtime();\n";
     }
 
-    // per-workgroup record (profile builds): slot 0 start (s_memrealtime), 1 HW_ID, 2 XCC_ID,
-    // 3 leaving the group loop, 4 / 5 start / end of its last group; after the phase stamps
+    // per-workgroup record (profile builds, kProfRec words): slot 0 start (s_memrealtime), 1 HW_ID,
+    // 2 XCC_ID, 3 leaving the group loop, 4 / 5 start / end of its last group, 6 / 7 around the
+    // first claim (vmas_jit_ops.hpp), 8 + w HW_ID of wave w; after the phase stamps
     std::string block_stamp(int k, const std::string& v) const {
         if (prof_block < 0) return "";
         return "    if (threadIdx.x == 0 && blockIdx.x < " + it(kProfBlocks) + ") a.prof[" +
-               it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + " + blockIdx.x * 8 + " + it(k) + "] = " + v + ";\n";
+               it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + " + blockIdx.x * " + it(kProfRec) + " + " + it(k) +
+               "] = " + v + ";\n";
     }
 
     std::string desc(int e) const {
@@ -771,6 +778,10 @@ struct Gen {
              "    __syncthreads();\n" +
              block_stamp(0, "__builtin_amdgcn_s_memrealtime()") + block_stamp(1, "__builtin_amdgcn_s_getreg(63492)") +
              block_stamp(2, "__builtin_amdgcn_s_getreg(30740)") +
+             (prof_block >= 0 ? "    if (lane == 0 && blockIdx.x < " + it(kProfBlocks) + ") a.prof[" +
+                                    it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + " + blockIdx.x * " + it(kProfRec) +
+                                    " + 8 + wave] = __builtin_amdgcn_s_getreg(63492);\n"
+                              : "") +
              (prof_block >= 0 ? "    if (threadIdx.x == 0) vmas_prof_blk = a.prof + " + it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + ";\n" : "") +
              "    for (;;) {\n"
              "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, &CUR, QL);\n"
@@ -1104,7 +1115,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
     }
     if (g.prof_block >= 0) {
-        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW + (size_t)kProfBlocks * 8;
+        W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW + (size_t)kProfBlocks * kProfRec;
         if (hipMalloc((void**)&W->d_prof, W->n_prof * 8) != hipSuccess ||
             hipMemset(W->d_prof, 0, W->n_prof * 8) != hipSuccess)
             return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc profile buffer"));

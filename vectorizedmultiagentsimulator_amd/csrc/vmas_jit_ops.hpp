@@ -240,7 +240,8 @@ __device__ __forceinline__ bool grid_wait(const uint32_t* ctl, int pass, uint32_
 }
 
 #ifdef VMAS_JIT_PROFILE_SLOTS
-// profile builds: the per-workgroup record array (set by the kernel's prologue)
+// profile builds: the per-workgroup record array (set by the kernel's prologue; 24 words per
+// workgroup, csrc/vmas_jit.hip kProfRec)
 __device__ unsigned long long* vmas_prof_blk;
 #endif
 
@@ -268,11 +269,11 @@ __device__ __attribute__((noinline)) int grid_next(bool persistent, uint32_t* ct
                 break;
             }
 #ifdef VMAS_JIT_PROFILE_SLOTS
-            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 24 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
             if (threadIdx.x == 0) QL[65] = grid_claim(claim, own, c.pass) ? 1u : 0u;
 #ifdef VMAS_JIT_PROFILE_SLOTS
-            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+            if (threadIdx.x == 0 && blockIdx.x < 4096u) vmas_prof_blk[blockIdx.x * 24 + 7] = __builtin_amdgcn_s_memrealtime();
 #endif
             __syncthreads();
             const bool mine = QL[65] != 0u;
