@@ -13,7 +13,9 @@ from vectorizedmultiagentsimulator_amd import make_env  # noqa: E402
 scenario = sys.argv[1] if len(sys.argv) > 1 else "balance"
 n_envs = int(sys.argv[2]) if len(sys.argv) > 2 else 32768
 kw = {"n_agents": 4} if scenario != "discovery" else {"n_agents": 8, "use_agent_lidar": True}
-env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, **kw)
+import os  # noqa: E402
+
+env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, graph_step=os.environ.get("GRAPH", "1") == "1", **kw)
 if scenario == "balance":
     env.world._substeps = 10
     env.world._sub_dt = env.world._dt / 10
@@ -32,5 +34,5 @@ for _ in range(50):
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(25)
-st.sort_stats("cumtime").print_stats(25)
+st.sort_stats("tottime").print_stats(30)
+st.sort_stats("cumtime").print_stats(40)

@@ -69,7 +69,7 @@ def launch(self):
 
 
 _graph.StepGraph._launch = launch
-wrap(_graph.StepGraph, "_clone_outputs", "clone0", "clone1")
+wrap(_graph.StepGraph, "_post_replay", "clone0", "clone1")
 
 N = 100
 torch.cuda.synchronize()
@@ -96,7 +96,7 @@ out = {
         "step_before_actions": round(mean_us("before_actions0", "before_actions1"), 1),
         "apply_actions_incl_wait": round(mean_us("apply0", "apply1"), 1),
         "graph_replay_launch": round(mean_us("replay0", "replay1"), 1),
-        "clone_outputs": round(mean_us("clone0", "clone1"), 1),
+        "post_replay_copies": round(mean_us("clone0", "clone1"), 1),
         "whole_step_call": round(mean_us("draw1", "step1"), 1),
     },
     "gpu_us": {"graph_replay": round(gpu_graph, 1)},

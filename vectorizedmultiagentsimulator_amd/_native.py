@@ -232,6 +232,16 @@ def copy_raw(device_index: int, spans, stream) -> None:
     check_aux(load_library().vmas_copy_spans(device_index, arr, n, stream), "vmas_copy_spans")
 
 
+COPY_SPAN_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("nbytes", np.int64)])  # VmasCopySpan
+
+
+def copy_table(device_index: int, table: np.ndarray, lo: int, hi: int, stream) -> None:
+    """One native launch (vmas_copy_spans) for rows lo..hi of a COPY_SPAN_DTYPE table."""
+    if hi > lo:
+        check_aux(load_library().vmas_copy_spans(device_index, table.ctypes.data + lo * COPY_SPAN_DTYPE.itemsize,
+                                                 hi - lo, stream), "vmas_copy_spans")
+
+
 def copy_spans(device_index: int, pairs, stream) -> None:
     """dst.copy_(src) for every (dst, src) pair of same-size contiguous device tensors, all in one
     native launch (vmas_copy_spans; any dtype: bytes are copied)."""

@@ -5,10 +5,10 @@
 //
 // The reference runs ~5 torch ops and one host sync per agent; here one launch covers all agents
 // and the host learns the flags without a stream synchronisation: every workgroup stores its
-// flag bits into its own slot and arrives on a device counter; the last to arrive ORs the slots
+// flag bits into its own slot and arrives on a sharded device counter; the last to arrive ORs the slots
 // and publishes (sequence number << 32 | flag bits) into mapped pinned host memory with ONE
 // 64-bit system-scope store -- the number and the flags land together, so no system fence is
-// needed -- and clears the counter.  The host spins on that word (checking the stream for errors
+// needed -- and clears the counters.  The host spins on that word (checking the stream for errors
 // while it waits).  Slots are overwritten by every call; nothing is memset per call.  u is
 // written for every env even when a flag is set (the caller raises and drops it, as the
 // reference raises before it assigns u).
@@ -30,12 +30,13 @@ constexpr int kMaxRefsPerLaunch = 8;  // refs travel in the kernel arguments (16
 // (kPerThread 2 / up to 256 workgroups per ref: 8 per thread and 64 per ref left most CUs idle
 // and took 9.8 us per balance step in the kernel alone)
 constexpr int kThreads = 256, kPerThread = 2, kMaxBlocksPerRef = 256;
+constexpr uint32_t kShards = 32;  // arrival counter shards (+ the top counter), one line each
 
 struct ApplyArgs {
     VmasActionApplyRef r[kMaxRefsPerLaunch];
     float* out;
     uint32_t* slots;    // [kMaxRefsPerLaunch][kMaxBlocksPerRef] flag bits of each workgroup
-    uint32_t* counter;  // device arrival counter, zero between calls
+    uint32_t* counter;  // device arrival counter: [0] top, [32 * (1 + k)] shard k; zero between calls
     uint64_t* hsig;     // mapped host word: seq << 32 | flags (bit 2i NaN, 2i+1 out of range, ref i)
     uint32_t seq;
     int B, n, gx;
@@ -51,6 +52,19 @@ __host__ __device__ inline void apply_one(const VmasActionApplyRef& r, float* ou
         const float v = r.clamp ? fminf(fmaxf(x, -rr), rr) : x;
         out[r.out_offset + (long)b * r.n_phys + c] = v * r.u_mult[c];
     }
+}
+
+// Arrival of workgroup i of n on the sharded counter (one thread): shard i % kShards, each on a
+// 128-byte line of its own, then the top counter for the arrival that completes its shard; true
+// for the last arrival overall.  (One unsharded counter serialised the arrivals of all n
+// workgroups at the memory side, ~11-13 ns each: 512 workgroups took 11 us per balance step;
+// MI355X_MICROARCH.md "fanin".)
+__device__ __forceinline__ bool arrive(uint32_t* counter, uint32_t i, uint32_t n) {
+    const uint32_t k = i % kShards, n_k = (n + kShards - 1u - k) / kShards;
+    const uint32_t n_top = n < (uint32_t)kShards ? n : (uint32_t)kShards;
+    if (__hip_atomic_fetch_add(&counter[32 * (1 + k)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != n_k - 1u)
+        return false;
+    return __hip_atomic_fetch_add(&counter[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_top - 1u;
 }
 
 __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
@@ -74,8 +88,7 @@ __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
         __hip_atomic_store(&a.slots[ref * kMaxBlocksPerRef + blockIdx.x], bits, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_s_waitcnt(0);  // the slot store has completed before the arrival
-        last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               (uint32_t)(a.gx * a.n) - 1u;
+        last = arrive(a.counter, (uint32_t)(ref * a.gx + (int)blockIdx.x), (uint32_t)(a.gx * a.n));
     }
     __syncthreads();
     if (!last) return;
@@ -90,10 +103,9 @@ __global__ void __launch_bounds__(kThreads) k_apply_actions(ApplyArgs a) {
     __syncthreads();
     if (f) atomicOr(&bits, f);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x <= kShards) __hip_atomic_store(&a.counter[32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
         __hip_atomic_store(a.hsig, ((uint64_t)a.seq << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 struct DevState {
@@ -109,8 +121,8 @@ std::mutex g_mu;
 int32_t dev_init(DevState& d) {
     if (d.slots) return VMAS_OK;
     VMAS_AUX_HIP(hipMalloc((void**)&d.slots, kMaxRefsPerLaunch * kMaxBlocksPerRef * 4));
-    VMAS_AUX_HIP(hipMalloc((void**)&d.counter, 4));
-    VMAS_AUX_HIP(hipMemset(d.counter, 0, 4));
+    VMAS_AUX_HIP(hipMalloc((void**)&d.counter, 4 * 32 * (kShards + 1)));
+    VMAS_AUX_HIP(hipMemset(d.counter, 0, 4 * 32 * (kShards + 1)));
     VMAS_AUX_HIP(hipHostMalloc((void**)&d.hsig, 8, hipHostMallocMapped | hipHostMallocCoherent));
     VMAS_AUX_HIP(hipHostGetDevicePointer((void**)&d.dsig, d.hsig, 0));
     *d.hsig = 0u;

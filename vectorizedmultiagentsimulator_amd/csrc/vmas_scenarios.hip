@@ -35,42 +35,74 @@ __device__ __forceinline__ float torch_remainder(float a, float b) {
 // balance.py:205-262 (restated in scenarios/balance.py): reward of the first agent (on-the-ground
 // test, package-goal distance, ground / position rewards and the global shaping update), every
 // agent's reward (ground_rew + pos_rew), every agent's 16-entry observation, and done
-// (on_the_ground + is_overlapping(package, goal)).  Grid: x = 64-env groups, y = part: 0 the
-// reward / done part, 1 + i agent i's observation (one 64-thread workgroup per (group, part): at
-// 32 768 envs 512 x 5 workgroups instead of 128 x 1, whose long per-thread chains -- the box-line
-// distance -- left half the chip idle and took 16 us).
-__global__ void __launch_bounds__(64) k_balance(VmasBalanceIO io) {
-    const int b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= io.batch) return;
-    const int part = blockIdx.y;
-    const V2 pkg = ref_pos(io.package, b), goal = ref_pos(io.goal, b);
-    if (part == 0) {
-        bool og = false;
-        if (io.what & VMAS_SCN_REWARD) {
-            // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
-            // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
-            og = (dist_pair(io.floor, io.line, b) < 0.f) || overlap_box_sphere(io.floor, io.package, b);
-            io.on_the_ground[b] = og ? 1 : 0;
-            const float dist = norm(pkg - goal);  // vector_norm(package.pos - goal.pos, dim=1)
-            io.package_dist[b] = dist;
-            const float ground = og ? io.fall_reward : 0.f;  // zeros, masked_fill_(on_the_ground, fall)
-            io.ground_rew[b] = ground;
-            const float gs = dist * io.shaping_factor;
-            const float pos_rew = io.global_shaping[(long)b * io.gs_s0] - gs;
-            io.global_shaping_out[b] = gs;
-            if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
-            io.pos_rew[b] = pos_rew;
-            const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
-            for (int i = 0; i < io.n_agents; ++i) io.rewards[i][b] = r;
-        } else if (io.what & VMAS_SCN_DONE) {
-            og = io.on_the_ground[b] != 0;
+// (on_the_ground + is_overlapping(package, goal)).  Grid: x = 64-env groups, y = part, 4 waves
+// per workgroup.  Part 0 is the reward / done part: the (floor, line) box-line distance of the
+// on-the-ground test is split over the 4 waves, one box side each (bl_part), and wave 0 picks the
+// first strict minimum over the sides in order, as closest_line_box does, then finishes.  Parts
+// 1 + k are the observations of agents 4k .. 4k + 3, one per wave.  (One 64-thread workgroup per
+// (group, part), the box-line distance in one chain: 11 us per step at 32 768 envs, the chain's
+// latency at two waves per CU; before that 128 x 1 workgroups took 16 us.)
+__global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
+    __shared__ float Q[4][4][64];  // [side][q1.x, q1.y, q2.x, q2.y][lane]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x * 64 + lane;
+    const bool valid = b < io.batch;
+    const int bb = valid ? b : io.batch - 1;
+    if (blockIdx.y == 0) {
+        if (!(io.what & VMAS_SCN_REWARD)) {
+            if (wave != 0 || !valid || !(io.what & VMAS_SCN_DONE)) return;
+            const bool og = io.on_the_ground[b] != 0;
+            io.done[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
+            return;
         }
+        {  // side `wave` of closest_line_box(floor, line) (get_distance's box-line branch)
+            const VmasShapeRef &fl = io.floor, &ln = io.line;
+            const float rb = ref_rot(ln, bb);
+            const Pts q = bl_part(ref_pos(fl, bb), make_trig(ref_rot(fl, bb)), fl.length / 2.f, fl.width / 2.f,
+                                  ref_pos(ln, bb), Trig{cosf(rb), sinf(rb), 0.f, 0.f}, ln.length / 2.f, wave);
+            Q[wave][0][lane] = q.p1.x;
+            Q[wave][1][lane] = q.p1.y;
+            Q[wave][2][lane] = q.p2.x;
+            Q[wave][3][lane] = q.p2.y;
+        }
+        __syncthreads();
+        if (wave != 0 || !valid) return;
+        V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
+        float bd = INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const V2 q1 = mk(Q[i][0][lane], Q[i][1][lane]), q2 = mk(Q[i][2][lane], Q[i][3][lane]);
+            const float d = norm(q1 - q2);
+            if (d < bd) {
+                bd = d;
+                c1 = q1;
+                c2 = q2;
+            }
+        }
+        const V2 pkg = ref_pos(io.package, b), goal = ref_pos(io.goal, b);
+        // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
+        // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
+        const bool og = (norm(c1 - c2) - kLineMinDist < 0.f) || overlap_box_sphere(io.floor, io.package, b);
+        io.on_the_ground[b] = og ? 1 : 0;
+        const float dist = norm(pkg - goal);  // vector_norm(package.pos - goal.pos, dim=1)
+        io.package_dist[b] = dist;
+        const float ground = og ? io.fall_reward : 0.f;  // zeros, masked_fill_(on_the_ground, fall)
+        io.ground_rew[b] = ground;
+        const float gs = dist * io.shaping_factor;
+        const float pos_rew = io.global_shaping[(long)b * io.gs_s0] - gs;
+        io.global_shaping_out[b] = gs;
+        if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
+        io.pos_rew[b] = pos_rew;
+        const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
+        for (int i = 0; i < io.n_agents; ++i) io.rewards[i][b] = r;
         if (io.what & VMAS_SCN_DONE)  // done = on_the_ground + is_overlapping(package, goal)
             io.done[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
         return;
     }
-    // part 1 + i: agent i's observation
-    const int i = part - 1;
+    // agent i's observation
+    const int i = (blockIdx.y - 1) * 4 + wave;
+    if (i >= io.n_agents || !valid) return;
+    const V2 pkg = ref_pos(io.package, b), goal = ref_pos(io.goal, b);
     const V2 lpos = ref_pos(io.line, b), pv = ld_vec2(io.package_vel, b), lv = ld_vec2(io.line_vel, b);
     const float law = ld_vec1(io.line_ang_vel, b);
     const float lrot = torch_remainder(ref_rot(io.line, b), io.pi);
@@ -373,8 +405,8 @@ int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stre
         io->floor.shape != VMAS_BOX)
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_balance_outputs: unexpected entity shapes");
     VMAS_AUX_HIP(hipSetDevice(device));
-    const int parts = 1 + ((io->what & VMAS_SCN_OBS) ? io->n_agents : 0);
-    hipLaunchKernelGGL(k_balance, dim3((io->batch + 63) / 64, parts), dim3(64), 0, (hipStream_t)stream, *io);
+    const int parts = 1 + ((io->what & VMAS_SCN_OBS) ? (io->n_agents + 3) / 4 : 0);
+    hipLaunchKernelGGL(k_balance, dim3((io->batch + 63) / 64, parts), dim3(256), 0, (hipStream_t)stream, *io);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

@@ -807,30 +807,77 @@ class StepGraph:
         outputs, the carry of the re-bound state to the next step (Y -> X, which before_actions
         then skips while no Y changes) and the next step's backups (which backup() then skips
         while no in-place tensor changes).  The outputs are copied before the carry when one
-        of them lies in a carry destination (two launches)."""
-        views, spans, rest = self._clone_prepare()
-        carry, bk, n_bk = self._post_spans()
-        out_ranges = [(s, nb) for s, _, nb in spans]
-        clash = any(lo < x + cn and x < lo + nb for lo, nb in out_ranges for _, x, cn in carry)
-        if self._carry_other or bk is None:  # non-contiguous carries / backups: the old order
-            N.copy_raw(self._dev_index(), spans, self._stream())
+        of them lies in a carry destination (two launches).  The span table is built once per
+        (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
+        t = self._post_table()
+        views, rest = self._clone_alloc(t)
+        dev, st = self._dev_index(), self._stream()
+        tbl, n_out, n_all = t["tbl"], t["n_out"], t["n_all"]
+        if t["plain"]:  # non-contiguous carries / backups: the old order
+            N.copy_table(dev, tbl, 0, n_out, st)
             self._clone_finish(rest)
             self._post = None
         else:
-            if clash:
-                N.copy_raw(self._dev_index(), spans, self._stream())
-                N.copy_raw(self._dev_index(), carry + bk, self._stream())
+            if t["clash"]:
+                N.copy_table(dev, tbl, 0, n_out, st)
+                N.copy_table(dev, tbl, n_out, n_all, st)
             else:
-                N.copy_raw(self._dev_index(), spans + carry + bk, self._stream())
+                N.copy_table(dev, tbl, 0, n_all, st)
             self._clone_finish(rest)
             self._post = {"carry_ver": tuple(y._version for y in self._carry_ys),
-                          "bk_ver": tuple(t._version for t in self._inplace), "bk_n": n_bk}
+                          "bk_ver": tuple(x._version for x in self._inplace), "bk_n": t["n_bk"]}
         fn, consts = self._clone_build
         return fn(views, consts)
 
+    def _post_table(self):
+        """The post-replay span table (N.COPY_SPAN_DTYPE rows): the contiguous outputs (their
+        destinations are filled per step by _clone_alloc), then the carry and backup spans."""
+        ts = self._out_tensors
+        if getattr(self, "_clone_src_of", None) is not ts:
+            self._clone_plan()
+            self._clone_src_of = ts
+        c = getattr(self, "_post_cache", None)  # (objects compared by identity, not id())
+        if (c is not None and c[0] is ts and c[1] is self._bk_dst and c[2] == len(self._bk_dst)
+                and c[3] == len(self._bk_src)):
+            return c[4]
+        out_rows = [(x.data_ptr(), 0, x.numel() * x.element_size()) for _, _, srcs in self._clone_group_srcs
+                    for x in srcs if x.is_contiguous()]
+        carry, bk, n_bk = self._post_spans()
+        plain = bool(self._carry_other) or bk is None
+        extra = [] if plain else carry + bk
+        tbl = np.zeros(len(out_rows) + len(extra), dtype=N.COPY_SPAN_DTYPE)
+        for i, row in enumerate(out_rows + extra):
+            tbl[i] = row
+        clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows for _, x, cn in carry)
+        t = {"tbl": tbl, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra), "plain": plain,
+             "clash": clash, "n_bk": n_bk}
+        self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
+        return t
+
+    def _clone_alloc(self, t):
+        """Fresh output tensors for one step, their addresses written into the table's output
+        rows: (views in the plan's order, the non-contiguous (dst, src) rest)."""
+        dev = self._out_tensors[0].device
+        views = ()
+        dst = t["tbl"]["dst"]
+        row = 0
+        rest = []
+        for (dt, shape, n), (_, _, srcs) in zip(self._clone_groups, self._clone_group_srcs):
+            buf = torch.empty((n,) + shape, dtype=dt, device=dev)
+            vs = buf.unbind(0)
+            views += vs
+            base, step = buf.data_ptr(), buf.stride(0) * buf.element_size()
+            for k, src in enumerate(srcs):
+                if src.is_contiguous():
+                    dst[row] = base + k * step
+                    row += 1
+                else:
+                    rest.append((vs[k], src))
+        return views, rest
+
     def _clone_plan(self):
         """Outputs grouped by (dtype, shape): per group one allocation [n, *shape] whose unbind
-        gives the n fresh tensors; per dtype one multi-tensor copy; the result tree rebuilt by a
+        gives the n fresh tensors, all filled by the post-replay copy launch; the result tree rebuilt by a
         function generated for its structure.  Built once per capture (the replay's output tensors
         are fixed), so a step makes a handful of host calls instead of several per output."""
         ts = self._out_tensors
@@ -841,14 +888,11 @@ class StepGraph:
         self._clone_groups = [(dt, shape, len(idx)) for (dt, shape), idx in plan]
         order = [i for _, idx in plan for i in idx]  # position in the concatenated views -> output
         pos = {i: p for p, i in enumerate(order)}
-        spans, start = [], 0
-        for (dt, _), idx in plan:
-            if spans and spans[-1][0] == dt:
-                spans[-1] = (dt, spans[-1][1], start + len(idx))
-            else:
-                spans.append((dt, start, start + len(idx)))
+        # per (dtype, shape) group, in view order: its sources
+        self._clone_group_srcs, start = [], 0
+        for _, idx in plan:
+            self._clone_group_srcs.append((start, start + len(idx), [ts[i] for i in idx]))
             start += len(idx)
-        self._clone_spans = [(lo, hi, [ts[order[p]] for p in range(lo, hi)]) for _, lo, hi in spans]
         consts: List[Any] = []
         counter = [0]
 
@@ -873,26 +917,6 @@ class StepGraph:
         fn = eval("lambda v, c: " + body)  # noqa: S307 -- generated from the output tree's structure only
         self._clone_build = (fn, consts)
 
-    def _clone_prepare(self):
-        """Fresh output tensors and the spans that fill them: (views, contiguous spans as
-        (src_ptr, dst_ptr, nbytes), the non-contiguous (dst, src) rest)."""
-        ts = self._out_tensors
-        if getattr(self, "_clone_src_of", None) is not ts:
-            self._clone_plan()
-            self._clone_src_of = ts
-        dev = ts[0].device
-        views = ()
-        for dt, shape, n in self._clone_groups:
-            views += torch.empty((n,) + shape, dtype=dt, device=dev).unbind(0)
-        spans, rest = [], []
-        for lo, hi, srcs in self._clone_spans:
-            for v, t in zip(views[lo:hi], srcs):
-                if t.is_contiguous():
-                    spans.append((t.data_ptr(), v.data_ptr(), t.numel() * t.element_size()))
-                else:
-                    rest.append((v, t))
-        return views, spans, rest
-
     @staticmethod
     def _clone_finish(rest):
         for v, t in rest:
@@ -900,8 +924,9 @@ class StepGraph:
 
     def _clone_outputs(self):
         """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
-        views, spans, rest = self._clone_prepare()
-        N.copy_raw(self._dev_index(), spans, self._stream())
+        t = self._post_table()
+        views, rest = self._clone_alloc(t)
+        N.copy_table(self._dev_index(), t["tbl"], 0, t["n_out"], self._stream())
         self._clone_finish(rest)
         fn, consts = self._clone_build
         return fn(views, consts)
