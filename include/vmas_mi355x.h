@@ -352,6 +352,37 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
                            int32_t* resolved, int32_t* max_accepted, int32_t* n_unresolved,
                            void* stream);
 
+/* Spawn sampler for a sequence of entities in one stream-ordered call: the loop of
+ * discovery's target respawn (discovery.py:237-252 of the reference; scenarios/discovery.py
+ * _respawn) -- for target i = 0 .. n_targets-1, find_random_pos_for_entity over
+ * occupied = [agents, every other target] (targets before i already moved), then
+ * target_i.pos = where(covered[:, i], new, old).  The tries are drawn on the device with the
+ * reference's numbers: try k of target i is torch's uniform_ on [B] for x at generator offset
+ * o_i + k * per_try and for y at o_i + k * per_try + inc, per_try = 2 * inc, with inc, the element
+ * to (philox subsequence, offset) mapping and the float mapping (`mode`, vmas_uniform_columns) of
+ * PyTorch's distribution kernel; o_0 = offset and o_{i+1} = o_i + consumed_i * per_try, consumed_i
+ * = 1 if every env accepts try 0, else max accepted try + 2 (the reference loop).  One kernel per
+ * target, chained on `stream` through max_accepted (device int32 [n_targets], written by the
+ * call): no host wait inside.  The caller reads max_accepted once afterwards and advances the
+ * generator by sum_i consumed_i * per_try (*increment returns inc).  max_accepted[n_targets]
+ * counts envs that found no position within VMAS_SPAWN_MAX_TRIES tries (the reference would loop
+ * on; the caller raises). */
+#define VMAS_SPAWN_MAX_TARGETS 16
+#define VMAS_SPAWN_MAX_TRIES 65536
+typedef struct VmasSpawnTargetsIO {
+    int32_t batch, n_agents, n_targets, mode;
+    const float* agents;                  /* [B, n_agents, 2] */
+    int32_t ag_s0, ag_s1, ag_s2, pad0;
+    float* pos[VMAS_SPAWN_MAX_TARGETS];   /* target i's [B, 2] position, updated in place */
+    int32_t pos_s0[VMAS_SPAWN_MAX_TARGETS], pos_s1[VMAS_SPAWN_MAX_TARGETS];
+    const uint8_t* covered;               /* [B, n_targets] torch.bool */
+    int32_t cov_s0, cov_s1;
+    float min_dist, x_lo, x_hi, y_lo, y_hi, pad1;
+    uint64_t seed, offset;
+    int32_t* max_accepted;                /* [n_targets + 1] device int32 */
+} VmasSpawnTargetsIO;
+int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream);
+
 /* ---- fused scenario programs (csrc/vmas_scenarios.hip) -------------------
  * One launch computes a benchmark scenario's per-step observation / reward / done tensor program
  * (one thread per env, the reference's fp32 operations in its order).  Error reporting as the

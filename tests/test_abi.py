@@ -36,11 +36,12 @@ def test_struct_sizes_match_header_compilation():
 #include <stdio.h>
 #include "vmas_mi355x.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(VmasEntityDesc), sizeof(VmasPairDesc),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(VmasEntityDesc), sizeof(VmasPairDesc),
     sizeof(VmasJointDesc), sizeof(VmasWorldConfig), sizeof(VmasEntityIO), sizeof(VmasAgentIO), sizeof(VmasJointIO),
     sizeof(VmasStepIO), sizeof(VmasRayTarget), sizeof(VmasShapeRef), sizeof(VmasActionRef), sizeof(int),
     sizeof(VmasActionApplyRef), sizeof(VmasUniformColumn), sizeof(VmasVec), sizeof(VmasBalanceIO),
-    sizeof(VmasFlockingIO), sizeof(VmasCopySpan), sizeof(VmasTransportIO), sizeof(VmasDiscoveryIO));
+    sizeof(VmasFlockingIO), sizeof(VmasCopySpan), sizeof(VmasTransportIO), sizeof(VmasDiscoveryIO),
+    sizeof(VmasSpawnTargetsIO), sizeof(VmasGradIO));
   return 0; }
 '''
     import tempfile
@@ -57,8 +58,9 @@ int main(void) {
           ctypes.sizeof(N.VmasShapeRef), N.ACTION_REF_DTYPE.itemsize, 4, N.ACTION_APPLY_REF_DTYPE.itemsize,
           N.UNIFORM_COLUMN_DTYPE.itemsize, ctypes.sizeof(N.VmasVec), ctypes.sizeof(N.VmasBalanceIO),
           ctypes.sizeof(N.VmasFlockingIO), ctypes.sizeof(N.VmasCopySpan), ctypes.sizeof(N.VmasTransportIO),
-          ctypes.sizeof(N.VmasDiscoveryIO)]
+          ctypes.sizeof(N.VmasDiscoveryIO), ctypes.sizeof(N.VmasSpawnTargetsIO), ctypes.sizeof(N.VmasGradIO)]
     assert sizes == py
+    assert N.COPY_SPAN_DTYPE.itemsize == ctypes.sizeof(N.VmasCopySpan)
 
 
 def test_invalid_arguments_return_errors_not_crashes():

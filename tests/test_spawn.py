@@ -57,3 +57,35 @@ def test_spawn_matches_reference_loop_gpu(gpu_device, b, n_occ, min_dist):
         _case(gpu_device, b, n_occ, min_dist, seed)
     if n_occ:  # the tries were drawn by the fused native launch (vmas_uniform_columns)
         assert _uniform.MODES.get((str(torch.device(gpu_device)), b)) is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,a,t,min_dist", [(1, 3, 2, 0.2), (16384, 8, 7, 0.2), (4096, 5, 7, 0.45), (333, 4, 16, 0.2)])
+def test_respawn_targets_matches_reference_loop_gpu(gpu_device, b, a, t, min_dist):
+    """Discovery's respawn loop (discovery.py:237-252: per target, find_random_pos_for_entity over
+    the agents and every other target, then where(covered)) as ONE stream-ordered native call
+    (vmas_spawn_targets, tries drawn on the device): the loop's positions bit for bit and the
+    generator left where the loop leaves it."""
+    from vectorizedmultiagentsimulator_amd.scenarios.discovery import respawn_targets_native
+
+    dev = gpu_device
+    for seed in range(3):
+        g = _gen(dev)
+        g.manual_seed(seed)
+        agents = torch.empty((b, a, 2), device=dev).uniform_(-1, 1)
+        tpos0 = [torch.empty((b, 2), device=dev).uniform_(-1, 1) for _ in range(t)]
+        covered = torch.rand(b, t, device=dev) < 0.3
+        exp = [p.clone() for p in tpos0]
+        g.manual_seed(seed + 1)
+        for i in range(t):
+            occ = torch.cat([agents] + [exp[j].unsqueeze(1) for j in range(t) if j != i], dim=1)
+            pos = O.find_random_pos_for_entity(occ, b, dev, min_dist, (-1.0, 1.0), (-1.0, 1.0))
+            exp[i] = torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), exp[i])
+        after_ref = torch.rand(4, device=dev)
+        got = [p.clone() for p in tpos0]
+        g.manual_seed(seed + 1)
+        respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
+        after_native = torch.rand(4, device=dev)
+        for i, (e, x) in enumerate(zip(exp, got)):
+            assert torch.equal(e, x), f"target {i}"
+        assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"

@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "vmas_test_hold",
     "vmas_balance_outputs",
     "vmas_copy_spans",
+    "vmas_spawn_targets",
     "vmas_world_step_vjp",
     "vmas_distance_vjp",
     "vmas_cast_rays_vjp",
@@ -230,6 +231,22 @@ def copy_raw(device_index: int, spans, stream) -> None:
     for i, (src, dst, nb) in enumerate(spans):
         arr[i].src, arr[i].dst, arr[i].nbytes = src, dst, nb
     check_aux(load_library().vmas_copy_spans(device_index, arr, n, stream), "vmas_copy_spans")
+
+
+VMAS_SPAWN_MAX_TARGETS = 16
+VMAS_SPAWN_MAX_TRIES = 65536
+
+
+class VmasSpawnTargetsIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", _i32), ("n_agents", _i32), ("n_targets", _i32), ("mode", _i32),
+        ("agents", _vp), ("ag_s0", _i32), ("ag_s1", _i32), ("ag_s2", _i32), ("pad0", _i32),
+        ("pos", _vp * VMAS_SPAWN_MAX_TARGETS), ("pos_s0", _i32 * VMAS_SPAWN_MAX_TARGETS),
+        ("pos_s1", _i32 * VMAS_SPAWN_MAX_TARGETS),
+        ("covered", _vp), ("cov_s0", _i32), ("cov_s1", _i32),
+        ("min_dist", _f32), ("x_lo", _f32), ("x_hi", _f32), ("y_lo", _f32), ("y_hi", _f32), ("pad1", _f32),
+        ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp),
+    ]
 
 
 COPY_SPAN_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("nbytes", np.int64)])  # VmasCopySpan
@@ -463,6 +480,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
                                        ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.vmas_world_step_vjp.restype = _i32
     lib.vmas_world_step_vjp.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    lib.vmas_spawn_targets.restype = _i32
+    lib.vmas_spawn_targets.argtypes = [_i32, _vp, ctypes.POINTER(ctypes.c_uint64), _vp]
     lib.vmas_copy_spans.restype = _i32
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_stream_abort_capture.restype = _i32

@@ -16,6 +16,9 @@
 // comparison `dist < min_dist` runs in fp32.  Compiled with -ffp-contract=off like the engine.
 #include <hip/hip_runtime.h>
 
+#include <rocrand/rocrand_philox4x32_10.h>
+
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -149,6 +152,85 @@ __global__ void __launch_bounds__(256) k_spawn_resolve(SpawnArgs a, int32_t* out
     }
 }
 
+// ---- the respawn loop of several entities, tries drawn on the device (vmas_spawn_targets) --------
+constexpr int kUniformThreads = 256;  // PyTorch's distribution kernel block (vmas_actions.hip)
+
+struct DrawGrid {
+    long long step;  // threads of torch's uniform_ grid on B elements
+    unsigned long long inc;
+};
+
+// Element b of torch's uniform_(lo, hi) on B floats at generator offset `off`: thread b % step of
+// the distribution kernel, 4 numbers per grid-stride round (k_uniform_columns, which is probed bit
+// for bit against torch: `mode` bit 0 fused (0, 1] mapping, bit 1 fused affine transform).
+__device__ __forceinline__ float uniform_at(unsigned long long seed, unsigned long long off, const DrawGrid& g, int b,
+                                            float lo, float hi, int mode) {
+    const long long t = b % g.step, q = b / g.step;
+    rocrand_state_philox4x32_10 st;
+    rocrand_init(seed, (unsigned long long)t, off, &st);
+    uint4 v = rocrand4(&st);
+    for (long long r = 0; r < q / 4; ++r) v = rocrand4(&st);
+    const int k = (int)(q % 4);
+    const unsigned int u = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+    const float inv = 2.3283064e-10f;  // ROCRAND_2POW32_INV
+    const float unit = (mode & 1) ? __builtin_fmaf((float)u, inv, inv) : inv + (float)u * inv;
+    const float range = hi - lo;
+    const float val = (mode & 2) ? __builtin_fmaf(unit, range, lo) : unit * range + lo;
+    return val == hi ? lo : val;  // (0, 1] -> [lo, hi)
+}
+
+__device__ __forceinline__ bool near(float ox, float oy, float x, float y, float min_dist) {
+    const float d0 = ox - x, d1 = oy - y;  // torch.cdist: sqrt(fl(fl(d0^2) + fl(d1^2)))
+    return sqrtf(d0 * d0 + d1 * d1) < min_dist;
+}
+
+// Target i of the respawn loop: one thread per env.  The generator offset of its first try
+// follows from the earlier targets' max accepted tries (stream order: their kernels completed).
+__global__ void __launch_bounds__(64) k_spawn_target(VmasSpawnTargetsIO io, DrawGrid g, int i) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= io.batch) return;
+    const unsigned long long per_try = 2ull * g.inc;
+    unsigned long long off = io.offset;
+    for (int j = 0; j < i; ++j) {
+        const int m = io.max_accepted[j];
+        off += (unsigned long long)(m == 0 ? 1 : m + 2) * per_try;
+    }
+    // occupied: the agents, then every other target (earlier ones already moved)
+    float occ[2 * (32 + VMAS_SPAWN_MAX_TARGETS)];
+    int n = 0;
+    for (int a = 0; a < io.n_agents; ++a) {
+        const float* p = io.agents + (long)b * io.ag_s0 + (long)a * io.ag_s1;
+        occ[n++] = p[0];
+        occ[n++] = p[io.ag_s2];
+    }
+    for (int j = 0; j < io.n_targets; ++j) {
+        if (j == i) continue;
+        const float* p = io.pos[j] + (long)b * io.pos_s0[j];
+        occ[n++] = p[0];
+        occ[n++] = p[io.pos_s1[j]];
+    }
+    float x = 0.f, y = 0.f;
+    int k = 0;
+    for (; k < VMAS_SPAWN_MAX_TRIES; ++k) {
+        const unsigned long long o = off + (unsigned long long)k * per_try;
+        x = uniform_at(io.seed, o, g, b, io.x_lo, io.x_hi, io.mode);
+        y = uniform_at(io.seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
+        bool hit = false;
+        for (int m = 0; m < n; m += 2) hit = hit || near(occ[m], occ[m + 1], x, y, io.min_dist);
+        if (!hit) break;
+    }
+    if (k == VMAS_SPAWN_MAX_TRIES) {  // counted in the extra word after the per-target maxima
+        atomicAdd(&io.max_accepted[io.n_targets], 1);
+        return;
+    }
+    if (k > 0) atomicMax(&io.max_accepted[i], k);
+    if (io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1]) {
+        float* p = io.pos[i] + (long)b * io.pos_s0[i];
+        p[0] = x;
+        p[io.pos_s1[i]] = y;
+    }
+}
+
 struct DevScratch {
     int32_t* d_out = nullptr;
     int32_t* h_out = nullptr;
@@ -203,6 +285,38 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
     VMAS_AUX_HIP(hipStreamSynchronize(st));
     *max_accepted = s.h_out[0];
     *n_unresolved = s.h_out[1];
+    return VMAS_OK;
+}
+
+int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream) {
+    if (!io || !increment || device < 0 || device >= 64 || io->batch <= 0 || io->n_agents < 0 || io->n_agents > 32 ||
+        io->n_targets < 1 || io->n_targets > VMAS_SPAWN_MAX_TARGETS || !io->covered || !io->max_accepted ||
+        (io->n_agents > 0 && !io->agents) || io->mode < 0 || io->mode > 3)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_targets: bad arguments");
+    for (int i = 0; i < io->n_targets; ++i)
+        if (!io->pos[i]) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_targets: null target %d", i);
+    int cur = -1;
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
+    static int max_blocks[64] = {0};
+    if (!max_blocks[device]) {
+        hipDeviceProp_t prop;
+        VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
+        max_blocks[device] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / kUniformThreads);
+        if (max_blocks[device] <= 0) return vmas_aux::fail(VMAS_E_HIP, "vmas_spawn_targets: device properties");
+    }
+    // torch's distribution-kernel grid and per-call philox increment on B elements (as
+    // vmas_uniform_columns)
+    const long long B = io->batch;
+    const long long gx = std::min<long long>((B + kUniformThreads - 1) / kUniformThreads, max_blocks[device]);
+    DrawGrid g{kUniformThreads * gx, (unsigned long long)((B - 1) / (kUniformThreads * gx * 4) + 1) * 4};
+    hipStream_t st = (hipStream_t)stream;
+    VMAS_AUX_HIP(hipMemsetAsync(io->max_accepted, 0, sizeof(int32_t) * (io->n_targets + 1), st));
+    for (int i = 0; i < io->n_targets; ++i) {
+        hipLaunchKernelGGL(k_spawn_target, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, *io, g, i);
+        VMAS_AUX_HIP(hipGetLastError());
+    }
+    *increment = g.inc;
     return VMAS_OK;
 }
 

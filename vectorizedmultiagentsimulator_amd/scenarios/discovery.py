@@ -137,6 +137,8 @@ class Scenario(BaseScenario):
 
     def _respawn(self):
         w = self.world
+        if self.targets_respawn and self._respawn_native():
+            return
         if self.targets_respawn:
             occupied_agents = [self.agents_pos]
             for i, target in enumerate(self._targets):
@@ -155,6 +157,34 @@ class Scenario(BaseScenario):
             for i, target in enumerate(self._targets):
                 covered = self.covered_targets[:, i].unsqueeze(-1)
                 target.state.pos.copy_(torch.where(covered, self.get_outside_pos(None), target.state.pos))
+
+    def _respawn_native(self) -> bool:
+        """The respawn loop above in one stream-ordered native call (vmas_spawn_targets: a kernel
+        per target, the tries drawn on the device with the reference's numbers, each target's
+        generator offset chained on the device) and ONE host read of the tries consumed -- in a
+        graph-mode step one host hole instead of one per target.  False (the loop above runs)
+        off the GPU or where the device draws cannot reproduce torch's (_uniform.mode)."""
+        w = self.world
+        ap = self.agents_pos
+        dev = torch.device(w.device)
+        if (dev.type != "cuda" or not _fused.enabled(w) or len(self._targets) > N.VMAS_SPAWN_MAX_TARGETS
+                or ap.dim() != 3 or ap.shape[1] > 32 or ap.dtype != torch.float32
+                or self.covered_targets.dtype != torch.bool):
+            return False
+        from vectorizedmultiagentsimulator_amd.simulator.environment import _uniform
+
+        if _uniform.mode(dev, w.batch_dim) is None:
+            return False
+        args = (ap, self.covered_targets, float(self._min_dist_between_entities), float(w.x_semidim),
+                float(w.y_semidim), *[t.state.pos for t in self._targets])
+        sink = getattr(w, "_hole_sink", None)
+        if sink is not None:  # a graph-mode capture: the host read stays a hole of the step
+            sink(respawn_targets_native, args)
+        else:
+            respawn_targets_native(*args)
+        for t in self._targets:  # written in place, as the reference's copy_
+            _fused.bump_version(t.state.pos)
+        return True
 
     # ---- fused program (GPU worlds; csrc/vmas_scenarios.hip k_discovery_reward / _obs) ---------
     # The first agent's reward call runs ONE launch for the reward block above (the stacks, the
@@ -395,3 +425,48 @@ class HeuristicPolicy(BaseHeuristicPolicy):
             des_pos[agent_visible] = des_pos_agent[agent_visible]
 
         return torch.clamp((des_pos - current_pos) * 10, min=-u_range, max=u_range)
+
+
+def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
+                           *target_pos: Tensor, out: Tensor = None) -> Tensor:
+    """Discovery's target respawn loop (_respawn) through vmas_spawn_targets: target i moves to
+    find_random_pos_for_entity(occupied = agents + the other targets) where covered[:, i].
+    Returns the device int32 [n_targets + 1] of per-target max accepted tries (+ the count of
+    envs that found no position) after reading it once and advancing the device generator by the
+    tries the reference loop consumes.  ``out``: the tensor of a graph-mode hole's replay."""
+    import numpy as np
+
+    from vectorizedmultiagentsimulator_amd.simulator.environment import _uniform
+
+    dev = agents_pos.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    B, A = agents_pos.shape[0], agents_pos.shape[1]
+    T = len(target_pos)
+    gen = torch.cuda.default_generators[idx]
+    mx = out if out is not None else torch.empty(T + 1, dtype=torch.int32, device=dev)
+    f32 = lambda v: float(np.float32(v))  # noqa: E731 -- torch casts the bounds to float
+    io = N.VmasSpawnTargetsIO()
+    io.batch, io.n_agents, io.n_targets, io.mode = B, A, T, _uniform.mode(dev, B)
+    io.agents = agents_pos.data_ptr()
+    io.ag_s0, io.ag_s1, io.ag_s2 = agents_pos.stride()
+    for i, p in enumerate(target_pos):
+        io.pos[i] = p.data_ptr()
+        io.pos_s0[i], io.pos_s1[i] = p.stride()
+    cov = covered.view(torch.uint8)
+    io.covered = cov.data_ptr()
+    io.cov_s0, io.cov_s1 = cov.stride()
+    io.min_dist = float(torch.tensor(min_dist, dtype=torch.float32))
+    io.x_lo, io.x_hi, io.y_lo, io.y_hi = f32(-x_semidim), f32(x_semidim), f32(-y_semidim), f32(y_semidim)
+    io.seed, io.offset = gen.initial_seed(), gen.get_offset()
+    io.max_accepted = mx.data_ptr()
+    inc = ctypes.c_uint64(0)
+    N.check_aux(N.load_library().vmas_spawn_targets(idx, ctypes.byref(io), ctypes.byref(inc),
+                                                      ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
+                "vmas_spawn_targets")
+    h = mx.tolist()  # the step's one host wait
+    if h[T]:
+        raise RuntimeError(
+            f"find_random_pos_for_entity: {h[T]} env(s) found no free position within {N.VMAS_SPAWN_MAX_TRIES} "
+            "tries; make sure the bounds or the min_dist_between_entities are not too tight to fit all entities")
+    gen.set_offset(io.offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc.value)
+    return mx
