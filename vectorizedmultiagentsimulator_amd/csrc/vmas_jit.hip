@@ -165,6 +165,7 @@ struct Gen {
     int nw = kNW;         // waves per workgroup
     int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
     bool relaxed = false;  // relaxed fp32 math (VMAS_JIT_MATH=relaxed, worlds without joints; see compile())
+    int prio_mode = 1;     // VMAS_JIT_PRIO=0 turns off the wave issue priority falling with the substep
     std::vector<char> dyn, in_pair, need_trig, need_rot, split;
     std::vector<int> owner;  // wave owning a dynamic entity / loading a static pair entity
     std::vector<std::vector<int>> wave_ents, wave_static;
@@ -629,6 +630,13 @@ struct Gen {
         o += "    __syncthreads();\n";
         o += "    " + stamp(w, pro + " + 1");
         o += "    for (int s = 0; s < a.S; ++s) {\n";
+        // Issue priority falling with the substep: of the two workgroups on a CU the one behind
+        // gets the issue slots, so they finish together instead of the second running its last
+        // substeps alone at half occupancy (balance 40.6-41.0 -> 39.7-40.0 us, flocking 38.2 ->
+        // 37.1 us, interleaved; priority by wave load measured no gain: profiles/r02/run14_prio)
+        if (prio_mode == 1)
+            o += "        if (4 * s < a.S) __builtin_amdgcn_s_setprio(3); else if (2 * s < a.S) __builtin_amdgcn_s_setprio(2);"
+                 " else if (4 * s < 3 * a.S) __builtin_amdgcn_s_setprio(1); else __builtin_amdgcn_s_setprio(0);\n";
         std::vector<char> word(W, 0);  // mask words this wave reads
         for (const Task& t : wave_tasks[w]) word[t.pair >> 5] = 1;
         for (int e : wave_ents[w])
@@ -1053,6 +1061,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
         Gen& g = *gp;
         if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
+        if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
         g.relaxed = relaxed_math(W->cfg);
         g.generate();
         std::vector<char> code;
