@@ -255,8 +255,18 @@ COPY_SPAN_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("nbytes", n
 def copy_table(device_index: int, table: np.ndarray, lo: int, hi: int, stream) -> None:
     """One native launch (vmas_copy_spans) for rows lo..hi of a COPY_SPAN_DTYPE table."""
     if hi > lo:
-        check_aux(load_library().vmas_copy_spans(device_index, table.ctypes.data + lo * COPY_SPAN_DTYPE.itemsize,
-                                                 hi - lo, stream), "vmas_copy_spans")
+        rc = (_copy_fn or _bind_copy())(device_index, table.ctypes.data + lo * COPY_SPAN_DTYPE.itemsize, hi - lo, stream)
+        if rc:
+            check_aux(rc, "vmas_copy_spans")
+
+
+_copy_fn = None
+
+
+def _bind_copy():
+    global _copy_fn
+    _copy_fn = load_library().vmas_copy_spans
+    return _copy_fn
 
 
 def copy_spans(device_index: int, pairs, stream) -> None:

@@ -532,16 +532,23 @@ class Environment(TorchVectorizedObject):
         if st is None:
             return None
         N, cols, widths, idx, mode, gen = st
-        outs = []
-        k = 0
         f_out = cols["out"]
-        for n in widths:
-            out = torch.empty(B, n, device=dev, dtype=torch.float32)
-            base = out.data_ptr()
-            for j in range(n):
-                f_out[k] = base + 4 * j
-                k += 1
-            outs.append(out)
+        if len(set(widths)) == 1:  # one allocation, one [B, n] view per agent (disjoint rows)
+            n = widths[0]
+            buf = torch.empty(len(widths), B, n, device=dev, dtype=torch.float32)
+            outs = list(buf.unbind(0))
+            base, step = buf.data_ptr(), 4 * B * n
+            f_out[:] = [base + a * step + 4 * j for a in range(len(widths)) for j in range(n)]
+        else:
+            outs = []
+            k = 0
+            for n in widths:
+                out = torch.empty(B, n, device=dev, dtype=torch.float32)
+                base = out.data_ptr()
+                for j in range(n):
+                    f_out[k] = base + 4 * j
+                    k += 1
+                outs.append(out)
         _uniform.launch(idx, B, cols, mode, gen)
         return outs
 
