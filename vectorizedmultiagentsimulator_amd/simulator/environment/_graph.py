@@ -736,6 +736,9 @@ class StepGraph:
         self._first_replay = False
         self._launch()
         self.replays += 1
+        # the host side of the post-replay copies (fresh output tensors, span table) while the
+        # action kernel's flags are still in flight; nothing is launched before they pass
+        prep = self._post_prepare()
         if not flags_ok():
             self._asserts.after_replay(dev, raise_=False)
             self._rollback(rng, restore_actions=True)
@@ -746,7 +749,7 @@ class StepGraph:
             self._rollback(rng, restore_actions=False)
             raise
         # only now: the post-replay carry overwrites X, which a rollback restores Y from
-        return self._post_replay()
+        return self._post_replay(prep)
 
     def _rollback(self, rng: Tensor, restore_actions: bool):
         self._post = None
@@ -802,15 +805,20 @@ class StepGraph:
             bk.append((src, d.data_ptr(), nb))
         return carry, bk, n
 
-    def _post_replay(self):
+    def _post_prepare(self):
+        """The host half of _post_replay: (span table, fresh output views, non-contiguous rest)."""
+        t = self._post_table()
+        views, rest = self._clone_alloc(t)
+        return t, views, rest
+
+    def _post_replay(self, prep=None):
         """After a replay, in ONE native launch (vmas_copy_spans): the fresh copies of the
         outputs, the carry of the re-bound state to the next step (Y -> X, which before_actions
         then skips while no Y changes) and the next step's backups (which backup() then skips
         while no in-place tensor changes).  The outputs are copied before the carry when one
         of them lies in a carry destination (two launches).  The span table is built once per
         (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
-        t = self._post_table()
-        views, rest = self._clone_alloc(t)
+        t, views, rest = prep if prep is not None else self._post_prepare()
         dev, st = self._dev_index(), self._stream()
         tbl, n_out, n_all = t["tbl"], t["n_out"], t["n_all"]
         if t["plain"]:  # non-contiguous carries / backups: the old order
