@@ -166,6 +166,7 @@ struct Gen {
     int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
     bool relaxed = false;  // relaxed fp32 math (VMAS_JIT_MATH=relaxed, worlds without joints; see compile())
     int prio_mode = 1;     // VMAS_JIT_PRIO=0 turns off the wave issue priority falling with the substep
+    bool entity_preload = true;  // VMAS_JIT_PRELOAD=0 (A/B): contribution reads inside their branches
     std::vector<char> dyn, in_pair, need_trig, need_rot, split;
     std::vector<int> owner;  // wave owning a dynamic entity / loading a static pair entity
     std::vector<std::vector<int>> wave_ents, wave_static;
@@ -663,14 +664,36 @@ struct Gen {
             o += "            float fx, fy, tq;\n";
             o += "            pre_forces(D" + s + ", " + bl(d.agent_index >= 0) + ", af" + s + ", at" + s + ", v" + s +
                  ", w" + s + ", eg" + s + ", " + bl(d.flags & VMAS_F_GRAVITY) + ", GX, GY, HAS_G, a.sdt, fx, fy, tq);\n";
-            for (const Item& x : items[e]) {
-                const int r = res(x.pair);
-                std::string body;
-                if (mov)
-                    body += x.side ? "fx = fx + -" + row(r) + "; fy = fy + -" + row(r, 1) + "; "
-                                   : "fx = fx + " + row(r) + "; fy = fy + " + row(r, 1) + "; ";
-                if (rotb && x.torque) body += "tq = tq + " + row(r, x.side ? 3 : 2) + "; ";
-                if (!body.empty()) o += "            if " + mbit(x.pair) + " { " + body + "}\n";
+            // every contribution row read up front (independent LDS reads in flight together),
+            // then added in the reference's order where its pair is active (a select: the same
+            // sums as the branch)
+            if (entity_preload) {
+                int k = 0;
+                for (const Item& x : items[e]) {
+                    const int r = res(x.pair);
+                    const std::string c = "c" + it(k++);
+                    if (mov) o += "            const float " + c + "x = " + row(r) + ", " + c + "y = " + row(r, 1) + ";\n";
+                    if (rotb && x.torque) o += "            const float " + c + "t = " + row(r, x.side ? 3 : 2) + ";\n";
+                }
+                k = 0;
+                for (const Item& x : items[e]) {
+                    const std::string c = "c" + it(k++), m = mbit(x.pair);
+                    if (mov) {
+                        const std::string sx = x.side ? "-" + c + "x" : c + "x", sy = x.side ? "-" + c + "y" : c + "y";
+                        o += "            fx = " + m + " ? fx + " + sx + " : fx; fy = " + m + " ? fy + " + sy + " : fy;\n";
+                    }
+                    if (rotb && x.torque) o += "            tq = " + m + " ? tq + " + c + "t : tq;\n";
+                }
+            } else {
+                for (const Item& x : items[e]) {
+                    const int r = res(x.pair);
+                    std::string body;
+                    if (mov)
+                        body += x.side ? "fx = fx + -" + row(r) + "; fy = fy + -" + row(r, 1) + "; "
+                                       : "fx = fx + " + row(r) + "; fy = fy + " + row(r, 1) + "; ";
+                    if (rotb && x.torque) body += "tq = tq + " + row(r, x.side ? 3 : 2) + "; ";
+                    if (!body.empty()) o += "            if " + mbit(x.pair) + " { " + body + "}\n";
+                }
             }
             o += "            integrate(D" + s + ", s, a.sdt, fx, fy, tq, HAS_XS, XS, HAS_YS, YS, p" + s + ", v" + s +
                  ", r" + s + ", w" + s + ");\n";
@@ -1062,6 +1085,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         Gen& g = *gp;
         if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
         if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
+        if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
         g.relaxed = relaxed_math(W->cfg);
         g.generate();
         std::vector<char> code;
