@@ -167,6 +167,7 @@ struct Gen {
     bool relaxed = false;  // relaxed fp32 math (VMAS_JIT_MATH=relaxed, worlds without joints; see compile())
     int prio_mode = 1;     // VMAS_JIT_PRIO=0 turns off the wave issue priority falling with the substep
     bool entity_preload = true;  // VMAS_JIT_PRELOAD=0 (A/B): contribution reads inside their branches
+    bool pair_preload = true;    // VMAS_JIT_PAIR_PRELOAD=0 (A/B): other waves' entity rows read at each use
     std::vector<char> dyn, in_pair, need_trig, need_rot, split;
     std::vector<int> owner;  // wave owning a dynamic entity / loading a static pair entity
     std::vector<std::vector<int>> wave_ents, wave_static;
@@ -377,18 +378,54 @@ struct Gen {
     // expressions for entity e as seen by wave w (registers when w owns it)
     static std::string row(int r, int k = 0) { return "L[" + it((long)(r + k) * 64) + " + lane]"; }
     bool mine(int e, int w) const { return dyn[e] && owner[e] == w; }
+    // Other waves' entities a wave's pair tasks read: with pair_preload, held in registers (q/u/o
+    // <e>) -- static ones loaded once per group, dynamic ones at the top of each pair phase, all
+    // reads in flight together -- instead of LDS reads at each use (inside the pairs' branches).
+    std::vector<char> pre_pos, pre_trig, pre_rot;  // of the wave being generated
     std::string pos(int e, int w) const {
         if (mine(e, w)) return "p" + it(e);
+        if (!pre_pos.empty() && pre_pos[e]) return "q" + it(e);
         return "mk(" + row(r_p[e]) + ", " + row(r_p[e], 1) + ")";
     }
     std::string rot(int e, int w) const {
         if (mine(e, w)) return "r" + it(e);
+        if (!pre_rot.empty() && pre_rot[e]) return "o" + it(e);
         return row(r_rot[e]);
     }
     std::string trig(int e, int w) const {
         if (mine(e, w)) return "t" + it(e);
+        if (!pre_trig.empty() && pre_trig[e]) return "u" + it(e);
         return "Trig{" + row(r_trig[e]) + ", " + row(r_trig[e], 1) + ", " + row(r_trig[e], 2) + ", " +
                row(r_trig[e], 3) + "}";
+    }
+    // the entities (and which of their rows) wave w's pair tasks read, outside its own registers
+    void task_reads(int w, std::vector<char>& rp, std::vector<char>& rt, std::vector<char>& rr) const {
+        rp.assign(E, 0);
+        rt.assign(E, 0);
+        rr.assign(E, 0);
+        for (const Task& k : wave_tasks[w]) {
+            if (k.part == kFinish) continue;
+            const VmasPairDesc& q = pd[k.pair];
+            for (int side = 0; side < 2; ++side) {
+                const int e = side ? q.eb : q.ea;
+                if (mine(e, w)) continue;
+                rp[e] = 1;
+                const bool t = q.cls == VMAS_PAIR_LL || q.cls == VMAS_PAIR_BL || q.cls == VMAS_PAIR_BB ||
+                               q.cls == VMAS_PAIR_JOINT ||
+                               (side == 0 && (q.cls == VMAS_PAIR_LS || q.cls == VMAS_PAIR_BS));
+                if (t && r_trig[e] >= 0) rt[e] = 1;
+                if (q.cls == VMAS_PAIR_JOINT && r_rot[e] >= 0) rr[e] = 1;
+            }
+        }
+    }
+    std::string preload(int e, bool p, bool t, bool r) const {
+        std::string o;
+        if (p) o += "        const V2 q" + it(e) + " = mk(" + row(r_p[e]) + ", " + row(r_p[e], 1) + ");\n";
+        if (t)
+            o += "        const Trig u" + it(e) + " = Trig{" + row(r_trig[e]) + ", " + row(r_trig[e], 1) + ", " +
+                 row(r_trig[e], 2) + ", " + row(r_trig[e], 3) + "};\n";
+        if (r) o += "        const float o" + it(e) + " = " + row(r_rot[e]) + ";\n";
+        return o;
     }
     std::string P_(Src s, int i) const { return "a.ptr[" + it(ptr_of[s][i]) + "]"; }
     std::string S_(Src s, int k, int i) const { return "a.str[" + it(str_of[s][k][i]) + "]"; }
@@ -630,6 +667,12 @@ struct Gen {
         o += "    " + stamp(w, pro);
         o += "    __syncthreads();\n";
         o += "    " + stamp(w, pro + " + 1");
+        std::vector<char> rp, rt, rr;
+        if (pair_preload) {
+            task_reads(w, rp, rt, rr);
+            for (int e = 0; e < E; ++e)  // static entities: once per group
+                if (!dyn[e] && (rp[e] || rt[e] || rr[e])) o += preload(e, rp[e], rt[e], rr[e]).substr(4);
+        }
         o += "    for (int s = 0; s < a.S; ++s) {\n";
         // Issue priority falling with the substep: of the two workgroups on a CU the one behind
         // gets the issue slots, so they finish together instead of the second running its last
@@ -648,7 +691,17 @@ struct Gen {
         for (const Task& t : wave_tasks[w]) fword[t.pair >> 5] = 1;
         for (int k = 0; k < W; ++k)
             if (fword[k]) o += "        uint32_t fr" + it(k) + " = 0u, fz" + it(k) + " = 0u;\n";
+        if (pair_preload) {
+            for (int e = 0; e < E; ++e)  // dynamic entities: at the top of each pair phase
+                if (dyn[e] && (rp[e] || rt[e] || rr[e])) o += preload(e, rp[e], rt[e], rr[e]);
+            pre_pos = rp;
+            pre_trig = rt;
+            pre_rot = rr;
+        }
         for (const Task& t : wave_tasks[w]) task_code(o, t, w);
+        pre_pos.clear();
+        pre_trig.clear();
+        pre_rot.clear();
         o += flag_flush(fword);
         o += "        " + stamp(w, "s * 4");
         o += "        __syncthreads();\n";
@@ -845,6 +898,13 @@ struct Gen {
         o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
     }
 };
+
+// Code-generation A/B knobs (environment): VMAS_JIT_PRIO, VMAS_JIT_PRELOAD, VMAS_JIT_PAIR_PRELOAD.
+void codegen_knobs(Gen& g) {
+    if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
+    if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
+    if (const char* pp = getenv("VMAS_JIT_PAIR_PRELOAD")) g.pair_preload = atoi(pp) != 0;
+}
 
 // Plan a world: box pairs split with two workgroups per CU, else unsplit, else unsplit with the
 // whole LDS (one workgroup per CU).  VMAS_JIT_SPLIT=0 disables splitting.
@@ -1084,8 +1144,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         }
         Gen& g = *gp;
         if (const char* pb = getenv("VMAS_JIT_PROFILE")) g.prof_block = std::max(0, atoi(pb));
-        if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
-        if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
+        codegen_knobs(g);
         g.relaxed = relaxed_math(W->cfg);
         g.generate();
         std::vector<char> code;
@@ -1182,6 +1241,7 @@ int32_t vmas_jit_compile_check(const VmasWorldConfig* cfg, const VmasEntityDesc*
     std::unique_ptr<Gen> gp = make_plan(*cfg, ed, pd, jd, &why);
     if (!gp) return jfail(VMAS_E_INVALID, "world not specialised: %s", why.c_str());
     Gen& g = *gp;
+    codegen_knobs(g);
     g.relaxed = relaxed_math(*cfg);
     g.generate();
     std::vector<char> code;
