@@ -252,6 +252,19 @@ class VmasSpawnTargetsIO(ctypes.Structure):
 COPY_SPAN_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("nbytes", np.int64)])  # VmasCopySpan
 
 
+def stream_ptr(index: int) -> int:
+    """The raw hipStream_t of torch's current stream on device `index` (what
+    torch.cuda.current_stream(index).cuda_stream returns, without building a Stream object: the
+    host path of a step asks for it several times)."""
+    return _raw_stream(index)
+
+
+def _raw_stream(index):
+    import torch
+
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
 def copy_table(device_index: int, table: np.ndarray, lo: int, hi: int, stream) -> None:
     """One native launch (vmas_copy_spans) for rows lo..hi of a COPY_SPAN_DTYPE table."""
     if hi > lo:

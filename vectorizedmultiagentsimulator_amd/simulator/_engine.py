@@ -148,7 +148,7 @@ class PhysicsEngine:
 
     def _stream(self, dev: torch.device):
         if dev.type == "cuda":
-            return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            return N.stream_ptr(dev.index if dev.index is not None else torch.cuda.current_device())
         return None
 
     def _prep(self, t: torch.Tensor, dev: torch.device) -> torch.Tensor:

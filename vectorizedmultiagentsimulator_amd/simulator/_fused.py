@@ -52,7 +52,7 @@ def device_index(world) -> int:
 
 
 def stream(world):
-    return ctypes.c_void_p(torch.cuda.current_stream(device_index(world)).cuda_stream)
+    return N.stream_ptr(device_index(world))
 
 
 def f32(t: torch.Tensor, dev) -> torch.Tensor:

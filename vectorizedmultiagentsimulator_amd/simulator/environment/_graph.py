@@ -50,6 +50,7 @@ from __future__ import annotations
 
 import ctypes
 import gc
+import operator
 import os
 import random
 from typing import Any, Dict, List, Optional, Tuple
@@ -59,6 +60,8 @@ import torch
 from torch import Tensor
 
 from ... import _native as N
+
+_VERSION = operator.attrgetter("_version")  # a tensor's version counter (map() without a Python frame)
 
 WARM_STEPS = 2  # eager steps before the capture (JIT compile, engine tables, allocator warm)
 
@@ -675,8 +678,8 @@ class StepGraph:
             from ... import _native as N
 
             dev = self.env.device
-            stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            N.check(N.load_library().vmas_graph_launch(self._raw_exec, stream), "vmas_graph_launch")
+            N.check(N.load_library().vmas_graph_launch(self._raw_exec, N.stream_ptr(self._dev_index())),
+                    "vmas_graph_launch")
             return
         dev = self.env.device
         gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
@@ -769,19 +772,19 @@ class StepGraph:
         return dev.index if dev.index is not None else torch.cuda.current_device()
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self._dev_index()).cuda_stream)
+        return N.stream_ptr(self._dev_index())
 
     def _carry_current(self) -> bool:
         """The last post-replay launch carried Y -> X and no Y was modified since (version
         counters: a native replay bumps none, a caller's in-place edit or the re-bind copy of
         before_actions bumps them)."""
         p = self._post
-        return p is not None and p["carry_ver"] == tuple(y._version for y in self._carry_ys)
+        return p is not None and p["carry_ver"] == tuple(map(_VERSION, self._carry_ys))
 
     def _backup_current(self, n: int) -> bool:
         p = self._post
         return (p is not None and p["bk_n"] >= n and self._carry_current()
-                and p["bk_ver"] == tuple(t._version for t in self._inplace))
+                and p["bk_ver"] == tuple(map(_VERSION, self._inplace)))
 
     def _post_spans(self):
         """Per capture: the carry spans (Y -> X, contiguous byte views) and the backup spans of
@@ -832,8 +835,8 @@ class StepGraph:
             else:
                 N.copy_table(dev, tbl, 0, n_all, st)
             self._clone_finish(rest)
-            self._post = {"carry_ver": tuple(y._version for y in self._carry_ys),
-                          "bk_ver": tuple(x._version for x in self._inplace), "bk_n": t["n_bk"]}
+            self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),
+                          "bk_ver": tuple(map(_VERSION, self._inplace)), "bk_n": t["n_bk"]}
         fn, consts = self._clone_build
         return fn(views, consts)
 
@@ -858,7 +861,8 @@ class StepGraph:
             tbl[i] = row
         clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows for _, x, cn in carry)
         t = {"tbl": tbl, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra), "plain": plain,
-             "clash": clash, "n_bk": n_bk}
+             "clash": clash, "n_bk": n_bk,
+             "contig": [[x.is_contiguous() for x in srcs] for _, _, srcs in self._clone_group_srcs]}
         self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
         return t
 
@@ -870,17 +874,17 @@ class StepGraph:
         dst = t["tbl"]["dst"]
         row = 0
         rest = []
-        for (dt, shape, n), (_, _, srcs) in zip(self._clone_groups, self._clone_group_srcs):
+        for (dt, shape, n), (_, _, srcs), contig in zip(self._clone_groups, self._clone_group_srcs, t["contig"]):
             buf = torch.empty((n,) + shape, dtype=dt, device=dev)
             vs = buf.unbind(0)
             views += vs
             base, step = buf.data_ptr(), buf.stride(0) * buf.element_size()
-            for k, src in enumerate(srcs):
-                if src.is_contiguous():
+            for k, c in enumerate(contig):
+                if c:
                     dst[row] = base + k * step
                     row += 1
                 else:
-                    rest.append((vs[k], src))
+                    rest.append((vs[k], srcs[k]))
         return views, rest
 
     def _clone_plan(self):

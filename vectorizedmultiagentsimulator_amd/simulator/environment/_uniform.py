@@ -35,7 +35,7 @@ def launch(idx: int, B: int, cols: np.ndarray, mode: int, gen: torch.Generator) 
     rows with out / stride / from_ / to set)."""
     N = _native()
     inc = ctypes.c_uint64(0)
-    stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
+    stream = N.stream_ptr(idx)
     N.check_aux(N.load_library().vmas_uniform_columns(idx, B, cols.ctypes.data, len(cols), gen.initial_seed(),
                                                        gen.get_offset(), mode, ctypes.byref(inc), stream),
                 "vmas_uniform_columns")

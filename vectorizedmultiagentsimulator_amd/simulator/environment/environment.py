@@ -734,7 +734,7 @@ class Environment(TorchVectorizedObject):
             out = pc[1]
         else:
             out = torch.empty(B * total, device=dev, dtype=torch.float32)
-        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream) if idx >= 0 else None
+        stream = N.stream_ptr(idx) if idx >= 0 else None
         lib = N.load_library()
         if speculative:
             seq = ctypes.c_uint32(0)
@@ -788,8 +788,7 @@ class Environment(TorchVectorizedObject):
         """Waits for the flags of a speculative launch; True when every agent's actions pass."""
         refs, _, flags, _, _, _, idx, N = self._apply_cache[1]
         n = len(self.agents)
-        stream = ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
-        N.check_aux(N.load_library().vmas_apply_actions_flags(idx, seq, n, flags.ctypes.data, stream),
+        N.check_aux(N.load_library().vmas_apply_actions_flags(idx, seq, n, flags.ctypes.data, N.stream_ptr(idx)),
                     "vmas_apply_actions_flags")
         self._spec_keep = None
         return not flags[: 2 * n].any()
