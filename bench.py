@@ -224,7 +224,7 @@ def main():
             # replayed launches: HIP records no events inside a graph; the kernel's own timer
             kernel_ms, launches = dev_ms, dev_n
             world.engine.get_timing(reset=True)
-            timer = "in-kernel s_memrealtime (workgroup 0 start -> last workgroup out), graph replays"
+            timer = "in-kernel s_memrealtime (workgroup 0 start -> final pass decided), graph replays"
         else:
             kernel_ms, launches = world.engine.get_timing(reset=True)
             timer = "HIP events on the launch's dispatch packet (hipExtModuleLaunchKernel)"

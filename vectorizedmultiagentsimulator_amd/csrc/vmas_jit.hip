@@ -853,10 +853,10 @@ struct Gen {
         // duplicate the per-wave code).  DONE is back to zero at the end of every substep's pair
         // phase, so it carries over between groups.
         o += "    const bool persistent = a.ctl != nullptr;\n"
-             "    uint32_t* claim = a.mask + " + it((long)cfg.max_substeps * W) + ";\n"
+             "    uint32_t* claim = a.mask + " + it(vmas::grid_claim_offset((long)cfg.max_substeps * W)) + ";\n"
              "    const TimerStart t0s = device_timer_start(persistent ? a.tm : nullptr, true);\n"
              "    __shared__ GridCursor CUR;\n"
-             "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0};\n"
+             "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0, 0, persistent ? ld64(&a.ctl[kGridEpoch]) : 0ull};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n"
              "    __syncthreads();\n" +
@@ -882,8 +882,8 @@ struct Gen {
         for (int w = 0; w < nw; ++w)
             o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
         o += "                default: break;\n            }\n        }\n";
-        o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, a.ctl, a.err, a.herr, nwords, ngrp, CUR.pass,\n"
-             "                                      a.max_pass, RED, &QL[65]))\n"
+        o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, &CUR,\n"
+             "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
              "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
              "    }\n" + block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
              "    if (!persistent) {\n"
@@ -892,7 +892,6 @@ struct Gen {
              "        for (int i = threadIdx.x; i < nfl; i += blockDim.x) st_agent(&a.blk[(size_t)blockIdx.x * nfl + i], FL[i]);\n"
              "        return;\n"
              "    }\n"
-             "    grid_exit(a.ctl, a.mask, claim, nwords, ngrp, a.max_pass, &QL[65], a.tm, t0s);\n"
              "}\n\n";
         const std::string bounds = "__launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) + ")";
         o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
@@ -1063,7 +1062,8 @@ struct VmasJitWorld {
     hipFunction_t fn = nullptr;  // k_world
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
     // persistent launches: d_ctl = [kGridCtlWords control words | inverted mask words | claim word
-    // per group, kClaimStride apart], zeroed at create and reset by the kernel's last workgroup;
+    // per group (u64, kClaimStride apart, from grid_claim_offset)], zeroed at create and never
+    // reset (global pass numbers, vmas_jit_ops.hpp);
     // d_err: sticky error bits; h_err: mapped host word the kernel stores them into (dh_err: its
     // device address)
     uint32_t *d_ctl = nullptr, *d_err = nullptr, *h_err = nullptr, *dh_err = nullptr;
@@ -1175,7 +1175,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         hipMalloc((void**)&W->d_viol, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_viol, 4, hipHostMallocDefault) != hipSuccess)
         return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc broadphase scratch"));
-    const size_t ctl_words = vmas::kGridCtlWords + nwords + (size_t)W->nblk * vmas::kClaimStride;
+    const size_t ctl_words = vmas::kGridCtlWords + (size_t)vmas::grid_claim_offset((long)nwords) +
+                             (size_t)W->nblk * vmas::kClaimStride;
     if (hipMalloc((void**)&W->d_ctl, ctl_words * 4) != hipSuccess || hipMalloc((void**)&W->d_err, 4) != hipSuccess ||
         hipHostMalloc((void**)&W->h_err, 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&W->dh_err, W->h_err, 0) != hipSuccess ||
@@ -1358,7 +1359,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     W->last_stream = stream;
     W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
-    // (the persistent kernel resets its own control words: see grid_exit)
+    // (the persistent kernel's control words need no reset: global pass numbers, vmas_jit_ops.hpp)
     if (!persistent) JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
     // Timing (vmas_jit_world_set_timing): the events ride on the kernel's own dispatch packet
     // (hipExtModuleLaunchKernel), so they bracket its execution alone, as rocprofv3's kernel
@@ -1453,7 +1454,7 @@ int32_t vmas_jit_world_set_timing(VmasJitWorld* W, int32_t enable) {
 }
 
 // Device timer totals (timing on, persistent launches): every launch -- eager or replayed from a
-// HIP graph -- adds (last workgroup out - workgroup 0 start) in s_memrealtime ticks; *clock_ghz is
+// HIP graph -- adds (final decision - workgroup 0 start) in s_memrealtime ticks; *clock_ghz is
 // the in-kernel shader clock of the reducing workgroups.  Waits for the device.
 int32_t vmas_jit_world_device_timing(VmasJitWorld* W, int32_t reset, double* total_ms, int64_t* launches,
                                      double* clock_ghz) {
