@@ -223,10 +223,13 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_target(VmasSpawnTarg
                                                                  float d2_min) {
     __shared__ int best[64];
     __shared__ float2 occ[kSpawnMaxOcc][64];  // the occupied positions of the workgroup's 64 envs
+    __shared__ float2 won[kSpawnWaves][64];   // each wave's accepted position (at most one per lane)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
+    // (read early: wave 0 applies the accepted position where the target was covered)
+    const bool cov = wave == 0 && valid && io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1];
     if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
     const unsigned long long per_try = 2ull * g.inc;
     unsigned long long off = io.offset;
@@ -262,6 +265,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_target(VmasSpawnTarg
                 hit = hit || near(o2.x, o2.y, x, y, d2_min);
             }
             if (!hit) {
+                won[wave][lane] = make_float2(x, y);
                 atomicMin(&best[lane], k);
                 break;
             }
@@ -275,11 +279,11 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_target(VmasSpawnTarg
     int km = unresolved ? 0 : k;  // one atomic per wave
     for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
     if (lane == 0 && km > 0) atomicMax(&io.max_accepted[i], km);
-    if (valid && !unresolved && io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1]) {
-        const unsigned long long o = off + (unsigned long long)k * per_try;
+    if (cov && !unresolved) {  // try k was drawn and accepted by wave k % kSpawnWaves
+        const float2 xy = won[k % kSpawnWaves][lane];
         float* p = io.pos[i] + (long)b * io.pos_s0[i];
-        p[0] = uniform_at(io.seed, o, g, b, io.x_lo, io.x_hi, io.mode);
-        p[io.pos_s1[i]] = uniform_at(io.seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
+        p[0] = xy.x;
+        p[io.pos_s1[i]] = xy.y;
     }
 }
 

@@ -385,8 +385,20 @@ class Scenario(BaseScenario):
         return {
             "covering_reward": agent.covering_reward if not self.shared_reward else self.shared_covering_rew,
             "collision_rew": agent.collision_rew,
-            "targets_covered": self.covered_targets.sum(-1),
+            "targets_covered": self._targets_covered_count(),
         }
+
+    def _targets_covered_count(self) -> Tensor:
+        """covered_targets.sum(-1) (ref discovery.py info), computed once per covered_targets
+        tensor and version: every agent's info holds the same count.  The reference sums it once
+        per agent; the environment returns each info value cloned (and a captured step copies
+        each output separately), so every agent still gets a tensor of its own -- one reduction
+        per step instead of one cast + reduction per agent."""
+        ct = self.covered_targets
+        c = getattr(self, "_cov_count", None)
+        if c is None or c[0] is not ct or c[1] != ct._version:
+            c = self._cov_count = (ct, ct._version, ct.sum(-1))
+        return c[2]
 
     def done(self):
         return self.all_time_covered_targets.all(dim=-1)
