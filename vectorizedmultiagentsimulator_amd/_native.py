@@ -267,8 +267,14 @@ def _raw_stream(index):
 
 def copy_table(device_index: int, table: np.ndarray, lo: int, hi: int, stream) -> None:
     """One native launch (vmas_copy_spans) for rows lo..hi of a COPY_SPAN_DTYPE table."""
+    copy_table_at(device_index, table.ctypes.data, lo, hi, stream)
+
+
+def copy_table_at(device_index: int, table_addr: int, lo: int, hi: int, stream) -> None:
+    """copy_table with the table's address (ndarray.ctypes.data, taken once by a caller that keeps
+    the table: each access of .ctypes builds a helper object)."""
     if hi > lo:
-        rc = (_copy_fn or _bind_copy())(device_index, table.ctypes.data + lo * COPY_SPAN_DTYPE.itemsize, hi - lo, stream)
+        rc = (_copy_fn or _bind_copy())(device_index, table_addr + lo * COPY_SPAN_DTYPE.itemsize, hi - lo, stream)
         if rc:
             check_aux(rc, "vmas_copy_spans")
 

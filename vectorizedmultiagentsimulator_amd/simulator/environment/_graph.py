@@ -823,17 +823,17 @@ class StepGraph:
         (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
         t, views, rest = prep if prep is not None else self._post_prepare()
         dev, st = self._dev_index(), self._stream()
-        tbl, n_out, n_all = t["tbl"], t["n_out"], t["n_all"]
+        tbl, n_out, n_all = t["addr"], t["n_out"], t["n_all"]
         if t["plain"]:  # non-contiguous carries / backups: the old order
-            N.copy_table(dev, tbl, 0, n_out, st)
+            N.copy_table_at(dev, tbl, 0, n_out, st)
             self._clone_finish(rest)
             self._post = None
         else:
             if t["clash"]:
-                N.copy_table(dev, tbl, 0, n_out, st)
-                N.copy_table(dev, tbl, n_out, n_all, st)
+                N.copy_table_at(dev, tbl, 0, n_out, st)
+                N.copy_table_at(dev, tbl, n_out, n_all, st)
             else:
-                N.copy_table(dev, tbl, 0, n_all, st)
+                N.copy_table_at(dev, tbl, 0, n_all, st)
             self._clone_finish(rest)
             self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),
                           "bk_ver": tuple(map(_VERSION, self._inplace)), "bk_n": t["n_bk"]}
@@ -860,7 +860,8 @@ class StepGraph:
         for i, row in enumerate(out_rows + extra):
             tbl[i] = row
         clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows for _, x, cn in carry)
-        t = {"tbl": tbl, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra), "plain": plain,
+        t = {"tbl": tbl, "addr": tbl.ctypes.data, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra),
+             "plain": plain,
              "clash": clash, "n_bk": n_bk,
              "contig": [[x.is_contiguous() for x in srcs] for _, _, srcs in self._clone_group_srcs]}
         self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
@@ -938,7 +939,7 @@ class StepGraph:
         """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
         t = self._post_table()
         views, rest = self._clone_alloc(t)
-        N.copy_table(self._dev_index(), t["tbl"], 0, t["n_out"], self._stream())
+        N.copy_table_at(self._dev_index(), t["addr"], 0, t["n_out"], self._stream())
         self._clone_finish(rest)
         fn, consts = self._clone_build
         return fn(views, consts)

@@ -29,17 +29,19 @@ def _native():
     return N
 
 
-def launch(idx: int, B: int, cols: np.ndarray, mode: int, gen: torch.Generator) -> None:
+def launch(idx: int, B: int, cols: np.ndarray, mode: int, gen: torch.Generator, cols_addr: Optional[int] = None) -> None:
     """Draws len(cols) columns of B floats at the generator's current (seed, offset) and advances
     the generator's offset as the equivalent uniform_ calls would (cols: UNIFORM_COLUMN_DTYPE
-    rows with out / stride / from_ / to set)."""
+    rows with out / stride / from_ / to set; cols_addr: its address, when the caller has it)."""
     N = _native()
     inc = ctypes.c_uint64(0)
     stream = N.stream_ptr(idx)
-    N.check_aux(N.load_library().vmas_uniform_columns(idx, B, cols.ctypes.data, len(cols), gen.initial_seed(),
-                                                       gen.get_offset(), mode, ctypes.byref(inc), stream),
+    off = gen.get_offset()
+    N.check_aux(N.load_library().vmas_uniform_columns(idx, B, cols.ctypes.data if cols_addr is None else cols_addr,
+                                                       len(cols), gen.initial_seed(), off, mode, ctypes.byref(inc),
+                                                       stream),
                 "vmas_uniform_columns")
-    gen.set_offset(gen.get_offset() + inc.value)
+    gen.set_offset(off + inc.value)
 
 
 def mode(device: torch.device, B: int) -> Optional[int]:

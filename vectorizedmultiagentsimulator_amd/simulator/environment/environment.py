@@ -505,9 +505,11 @@ class Environment(TorchVectorizedObject):
         agents = self.agents
         if not agents:
             return None
+        c = self._uniform_cache
+        if c is not None and c[1] is not None and self._uniform_same(c[2]):
+            return self._uniform_draw(c[1])
         plans = [self._column_plan(a) for a in agents]
         B, dev = plans[0][0], plans[0][1]
-        c = self._uniform_cache
         if c is None or len(c[0]) != len(plans) or any(a is not b for a, b in zip(c[0], plans)):
             key = tuple(plans)
             n_cols = sum(p[2] for p in plans)
@@ -526,19 +528,46 @@ class Environment(TorchVectorizedObject):
                     k += 1
             d = torch.device(dev)
             idx = d.index if d.index is not None else torch.cuda.current_device()
-            c = self._uniform_cache = (key, (N, cols, [p[2] for p in plans], idx,
-                                             _uniform.mode(d, B), torch.cuda.default_generators[idx]))
-        st = c[1]
-        if st is None:
+            widths = [p[2] for p in plans]
+            # column k's byte offset in the [A, B, n] allocation of equal widths
+            offs = (np.array([a * 4 * B * widths[0] + 4 * j for a in range(len(widths)) for j in range(widths[0])],
+                             dtype=np.uint64) if len(set(widths)) == 1 else None)
+            c = (key, (N, cols, widths, idx, _uniform.mode(d, B), torch.cuda.default_generators[idx],
+                       cols.ctypes.data, B, dev, offs))
+        if c[1] is None:
+            self._uniform_cache = c
             return None
-        N, cols, widths, idx, mode, gen = st
+        self._uniform_cache = (c[0], c[1], self._uniform_sig())
+        return self._uniform_draw(c[1])
+
+    def _uniform_sig(self):
+        """What _column_plan's keys depend on, compared by identity (None when a u_range is a
+        mutable sequence: then the plans are rebuilt every call)."""
+        sig = []
+        for a in self.agents:
+            act = a.action
+            ur = act.u_range
+            if type(ur) not in (float, int):
+                return None
+            sig.append((a, act, ur, a.silent, a.action_size, a.batch_dim))
+        return (self.world.dim_c, sig)
+
+    def _uniform_same(self, sig) -> bool:
+        if sig is None or sig[0] != self.world.dim_c or len(sig[1]) != len(self.agents):
+            return False
+        for a, (ag, act, ur, sil, asz, bd) in zip(self.agents, sig[1]):
+            if (a is not ag or a.action is not act or act.u_range is not ur or a.silent is not sil
+                    or a.action_size != asz or a.batch_dim != bd):
+                return False
+        return True
+
+    def _uniform_draw(self, st):
+        N, cols, widths, idx, mode, gen, cols_addr, B, dev, offs = st
         f_out = cols["out"]
-        if len(set(widths)) == 1:  # one allocation, one [B, n] view per agent (disjoint rows)
-            n = widths[0]
-            buf = torch.empty(len(widths), B, n, device=dev, dtype=torch.float32)
+        if offs is not None:  # one allocation, one [B, n] view per agent (disjoint rows)
+            buf = torch.empty(len(widths), B, widths[0], device=dev, dtype=torch.float32)
             outs = list(buf.unbind(0))
-            base, step = buf.data_ptr(), 4 * B * n
-            f_out[:] = [base + a * step + 4 * j for a in range(len(widths)) for j in range(n)]
+            np.add(offs, buf.data_ptr(), out=f_out, casting="unsafe")
         else:
             outs = []
             k = 0
@@ -549,7 +578,7 @@ class Environment(TorchVectorizedObject):
                     f_out[k] = base + 4 * j
                     k += 1
                 outs.append(out)
-        _uniform.launch(idx, B, cols, mode, gen)
+        _uniform.launch(idx, B, cols, mode, gen, cols_addr)
         return outs
 
     @local_seed(vmas_random_state)
@@ -703,12 +732,14 @@ class Environment(TorchVectorizedObject):
             else:
                 idx = -1
             fields = (refs["u"], refs["s0"], refs["s1"], refs["n_cols"])
-            flags = np.zeros(2 * n, dtype=np.uint8)
-            c = self._apply_cache = (key, (refs, fields, flags, tensors, sizes, sum(sizes), idx, N))
+            flags = np.zeros(max(16, (2 * n + 7) // 8 * 8), dtype=np.uint8)  # (whole uint64 words)
+            # the arrays' addresses once (ndarray.ctypes builds a helper object per access: ~1.6 us)
+            c = self._apply_cache = (key, (refs, fields, flags, tensors, sizes, sum(sizes), idx, N,
+                                           refs.ctypes.data, flags.ctypes.data, flags.view(np.uint64)))
         st = c[1]
         if st is None:
             return False
-        refs, (f_u, f_s0, f_s1, f_nc), flags, tensors, sizes, total, idx, N = st
+        refs, (f_u, f_s0, f_s1, f_nc), flags, tensors, sizes, total, idx, N, refs_addr, flags_addr, _ = st
         for i, ag in enumerate(agents):  # range / multiplier tensors are cached by the Action
             if ag.action._u_range_tensor is not tensors[i][0] or ag.action._u_multiplier_tensor is not tensors[i][1]:
                 self._apply_cache = None
@@ -738,11 +769,11 @@ class Environment(TorchVectorizedObject):
         lib = N.load_library()
         if speculative:
             seq = ctypes.c_uint32(0)
-            N.check_aux(lib.vmas_apply_actions_launch(idx, B, refs.ctypes.data, n, out.data_ptr(), ctypes.byref(seq),
-                                                      stream), "vmas_apply_actions_launch")
+            N.check_aux(lib.vmas_apply_actions_launch(idx, B, refs_addr, n, out.data_ptr(), ctypes.byref(seq), stream),
+                        "vmas_apply_actions_launch")
             self._spec_keep = keep  # the kernel reads them: alive until the flags are in
         else:
-            N.check_aux(lib.vmas_apply_actions(idx, B, refs.ctypes.data, n, out.data_ptr(), flags.ctypes.data, stream),
+            N.check_aux(lib.vmas_apply_actions(idx, B, refs_addr, n, out.data_ptr(), flags_addr, stream),
                         "vmas_apply_actions")
         del keep
         k = sizes[0]
@@ -786,12 +817,12 @@ class Environment(TorchVectorizedObject):
 
     def _speculative_flags_ok(self, seq: int) -> bool:
         """Waits for the flags of a speculative launch; True when every agent's actions pass."""
-        refs, _, flags, _, _, _, idx, N = self._apply_cache[1]
-        n = len(self.agents)
-        N.check_aux(N.load_library().vmas_apply_actions_flags(idx, seq, n, flags.ctypes.data, N.stream_ptr(idx)),
+        st = self._apply_cache[1]
+        idx, N, flags_addr, words = st[6], st[7], st[9], st[10]
+        N.check_aux(N.load_library().vmas_apply_actions_flags(idx, seq, len(self.agents), flags_addr, N.stream_ptr(idx)),
                     "vmas_apply_actions_flags")
         self._spec_keep = None
-        return not flags[: 2 * n].any()
+        return not (int(words[0]) | int(words[1]))  # (speculation: at most 8 agents, 16 flag bytes)
 
     def _set_action(self, action, agent, validated: bool = False):
         # The reference clones the action so that its in-place ops never touch the caller's
