@@ -133,6 +133,8 @@ typedef struct VmasWorldConfig {
     float x_semidim, y_semidim;
     int32_t has_x_semidim, has_y_semidim;
     int32_t max_substeps;     /* capacity of the broadphase flag scratch */
+    int32_t export_forces;    /* 1: the step fills VmasStepIO.out_fdict / out_tdict (World.forces_dict /
+                                 torques_dict, core.py:1975-1992); 0: those pointers must be NULL */
 } VmasWorldConfig;
 
 /* Per-call input pointers.  Strides are in elements (torch .stride()). */
@@ -171,6 +173,12 @@ typedef struct VmasStepIO {
     float sub_dt;      /* f32(dt / substeps) */
     int32_t broadphase;/* VMAS_BROADPHASE_* */
     int32_t pad;
+    /* World.forces_dict / torques_dict (core.py:1975-1992, 2027-2198): each dynamic entity's force
+     * and torque totals of the LAST substep, [n_entities][B][2] / [n_entities][B] in entity
+     * order; rows of entities that neither move nor rotate are not written.  NULL = not exported
+     * (required when VmasWorldConfig.export_forces is 0). */
+    float* out_fdict;
+    float* out_tdict;
 } VmasStepIO;
 
 typedef struct VmasWorld VmasWorld;

@@ -177,6 +177,7 @@ class VmasWorldConfig(ctypes.Structure):
         ("has_x_semidim", _i32),
         ("has_y_semidim", _i32),
         ("max_substeps", _i32),
+        ("export_forces", _i32),
     ]
 
 
@@ -195,6 +196,8 @@ class VmasStepIO(ctypes.Structure):
         ("sub_dt", _f32),
         ("broadphase", _i32),
         ("pad", _i32),
+        ("out_fdict", _vp),
+        ("out_tdict", _vp),
     ]
 
 

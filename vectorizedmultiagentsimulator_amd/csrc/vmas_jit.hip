@@ -369,9 +369,12 @@ struct Gen {
         return true;
     }
 
+    // output pointers: pos, vel, rot, ang_vel, force, torque (+ forces_dict, torques_dict rows)
+    size_t n_out() const { return cfg.export_forces ? 8 : 6; }
+
     size_t arg_bytes() const {  // layout of the generated struct Args
         // (+4 ints: B, S, sdt, max_pass; the struct is padded to its 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + 6 + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
         return (n + 7) & ~(size_t)7;
     }
 
@@ -662,6 +665,8 @@ struct Gen {
             if (need_trig[e])
                 o += "    Trig t" + s + " = make_trig_for(r" + s + ", " + bl(d.shape == VMAS_BOX) + ");\n";
             publish(o, e, "    ", true, true);
+            // World.forces_dict / torques_dict: the totals of the last substep (core.py:1975-1992)
+            if (cfg.export_forces) o += "    float lfx" + s + " = 0.f, lfy" + s + " = 0.f, ltq" + s + " = 0.f;\n";
         }
         const std::string pro = it((long)cfg.max_substeps * 4);
         o += "    " + stamp(w, pro);
@@ -748,6 +753,7 @@ struct Gen {
                     if (!body.empty()) o += "            if " + mbit(x.pair) + " { " + body + "}\n";
                 }
             }
+            if (cfg.export_forces) o += "            lfx" + s + " = fx; lfy" + s + " = fy; ltq" + s + " = tq;\n";
             o += "            integrate(D" + s + ", s, a.sdt, fx, fy, tq, HAS_XS, XS, HAS_YS, YS, p" + s + ", v" + s +
                  ", r" + s + ", w" + s + ");\n";
             if (need_trig[e] && rotb)
@@ -780,6 +786,9 @@ struct Gen {
                     if (d.out_torque >= 0)
                         o += "        st_out1(a.out[5], (size_t)" + it(d.out_torque) + " * a.B + b, at" + s + ");\n";
                 }
+                if (cfg.export_forces)
+                    o += "        st_out2(a.out[6], (size_t)" + s + " * a.B + b, mk(lfx" + s + ", lfy" + s +
+                         "));\n        st_out1(a.out[7], (size_t)" + s + " * a.B + b, ltq" + s + ");\n";
             }
             o += "    }\n";
         }
@@ -794,7 +803,7 @@ struct Gen {
         if (prof_block >= 0) o += "#define VMAS_JIT_PROFILE_SLOTS 1\n";
         o += "#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
-             "];\n    float* out[6];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
+             "];\n    float* out[" + it(n_out()) + "];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
@@ -1307,6 +1316,10 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(io->out_ang_vel);
     put_ptr(io->out_force);
     put_ptr(io->out_torque);
+    if (W->cfg.export_forces) {
+        put_ptr(io->out_fdict);
+        put_ptr(io->out_tdict);
+    }
     const bool batch_bp = io->broadphase == VMAS_BROADPHASE_BATCH;
     const bool persistent = batch_bp && W->grid > 0;
     uint32_t* nmask = persistent ? W->d_ctl + vmas::kGridCtlWords : W->d_mask;

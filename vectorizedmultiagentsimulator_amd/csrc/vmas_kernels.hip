@@ -287,6 +287,8 @@ struct StepK {
     float* out_ang;
     float* out_force;
     float* out_torque;
+    float* out_fd;  // [E][B][2] or NULL (VmasStepIO.out_fdict)
+    float* out_td;  // [E][B]
     const uint32_t* mask;
     uint32_t* blk;
     float* scratch;
@@ -556,6 +558,10 @@ __global__ void __launch_bounds__(512, 4) k_step(StepK k) {
                 if (c + 1 < k.n_chunks) {
                     acc[0] = fx; acc[64] = fy; acc[128] = tq;
                 } else {
+                    if (k.out_fd && s == k.S - 1 && valid) {  // World.forces_dict / torques_dict
+                        reinterpret_cast<float2*>(k.out_fd)[(size_t)e * k.B + b] = make_float2(fx, fy);
+                        k.out_td[(size_t)e * k.B + b] = tq;
+                    }
                     V2 p = mk(sb[0], sb[64]), v = mk(sb[128], sb[192]);
                     float rot = sb[256], w = sb[320];
                     integrate(d, s, k.sdt, fx, fy, tq, k.has_xs != 0, k.xs, k.has_ys != 0, k.ys,
@@ -734,6 +740,12 @@ static void host_step_env(const VmasWorld& W, const VmasStepIO& io, const uint32
                     fy = fy + (side ? -res[p].fa.y : res[p].fa.y);
                 }
                 if (rotb && (it & 1)) tq = tq + (side ? res[p].tb : res[p].ta);
+            }
+            if (io.out_fdict && s == S - 1) {  // World.forces_dict / torques_dict (core.py:1975-1992)
+                const size_t r = (size_t)e * W.cfg.batch + b;
+                io.out_fdict[r * 2] = fx;
+                io.out_fdict[r * 2 + 1] = fy;
+                io.out_tdict[r] = tq;
             }
             // integration must not disturb other entities' substep-start state: stage it
             V2 p2 = pos[e], v2 = vel[e];
@@ -1179,6 +1191,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     k.jio = (const VmasJointIO*)((const char*)dtab + oj);
     k.out_pos = io->out_pos; k.out_vel = io->out_vel; k.out_rot = io->out_rot;
     k.out_ang = io->out_ang_vel; k.out_force = io->out_force; k.out_torque = io->out_torque;
+    k.out_fd = io->out_fdict; k.out_td = io->out_tdict;
     k.mask = W->d_mask;
     const bool batch_bp = io->broadphase == VMAS_BROADPHASE_BATCH;
     k.blk = batch_bp ? W->d_blk : nullptr;

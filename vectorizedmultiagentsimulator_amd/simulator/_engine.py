@@ -180,6 +180,7 @@ class PhysicsEngine:
             tuple(es), tuple(js), w._drag, w._linear_friction, w._angular_friction, w._x_semidim,
             w._y_semidim, w._collision_force, w._joint_force, w._torque_constraint_force,
             w._contact_margin, id(w._gravity), id(w._collidable_pairs), w.batch_dim, str(w.device),
+            bool(w.export_forces),
         )
 
     def _build(self, sig, max_substeps: int):
@@ -362,6 +363,7 @@ class PhysicsEngine:
         cfg.x_semidim = _f32(w._x_semidim) if w._x_semidim is not None else 0.0
         cfg.y_semidim = _f32(w._y_semidim) if w._y_semidim is not None else 0.0
         cfg.max_substeps = max_substeps
+        cfg.export_forces = int(bool(w.export_forces))
         handle = ctypes.c_void_p()
         N.check(self.lib.vmas_world_create(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(handle)),
                 "vmas_world_create")
@@ -631,6 +633,15 @@ class PhysicsEngine:
             io.sub_dt = _f32(w._sub_dt)
             io.broadphase = N.BROADPHASE_BATCH if w.broadphase == "batch" else N.BROADPHASE_ENV
             self._step_params = params
+        fd = None
+        if self._cfg.export_forces:
+            # World.forces_dict / torques_dict rows ([E][B][2] | [E][B]); entities that neither move
+            # nor rotate are not written by the kernels (zeros, or their friction: _static_forces)
+            E = len(self.entities)
+            fd = torch.zeros(E * B * 3, device=dev, dtype=torch.float32)
+            io.out_fdict, io.out_tdict = fd.data_ptr(), fd.data_ptr() + 4 * E * B * 2
+        else:
+            io.out_fdict = io.out_tdict = 0
         iters = ctypes.c_int32(0)
         if self._jit is not None:
             N.check_jit(self.lib.vmas_jit_world_step(self._jit, ctypes.byref(io), self._stream(dev),
@@ -639,10 +650,47 @@ class PhysicsEngine:
             N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
                                              ctypes.byref(iters)), "vmas_world_step")
         self._last_iterations = iters.value
+        if fd is not None:
+            self._publish_force_dicts(fd, B)
         self.steps += 1
         _GRAD_OK = False
         self._last_keep = keep
         return out
+
+    def _publish_force_dicts(self, fd: torch.Tensor, B: int) -> None:
+        """World.forces_dict / torques_dict (ref core.py:1975-1992): per entity, views of the step's
+        last-substep force [B,2] and torque [B,1] totals."""
+        w = self.world
+        E = len(self.entities)
+        f2 = fd[: E * B * 2].view(E, B, 2)
+        f1 = fd[E * B * 2:].view(E, B, 1)
+        forces, torques = {}, {}
+        for i, e in enumerate(self.entities):
+            forces[e], torques[e] = f2[i], f1[i]
+            if not (e.movable or e.rotatable):
+                self._static_forces(e, f2[i], f1[i], w)
+        w._forces_dict, w._torques_dict = forces, torques
+
+    @staticmethod
+    def _static_forces(e, f, t, w) -> None:
+        """An entity that neither moves nor rotates only receives friction from its (constant)
+        velocity (ref core.py:2053-2101; contacts and gravity need movable / rotatable)."""
+
+        def friction(vel, coeff, mass):  # get_friction_force (ref core.py:2054-2072)
+            speed = torch.linalg.vector_norm(vel, dim=-1)
+            static = speed == 0
+            ff = -(vel / torch.where(static, 1e-8, speed).unsqueeze(-1)) * torch.minimum(
+                torch.full_like(vel, coeff) * mass, (vel.abs() / w._sub_dt) * mass)
+            return torch.where(static.unsqueeze(-1).expand(vel.shape), 0.0, ff)
+
+        lin = e.linear_friction if e.linear_friction is not None else (
+            w._linear_friction if w._linear_friction > 0 else None)
+        ang = e.angular_friction if e.angular_friction is not None else (
+            w._angular_friction if w._angular_friction > 0 else None)
+        if lin is not None:
+            f.copy_(friction(e.state.vel.to(f.dtype), lin, e.mass))
+        if ang is not None:
+            t.copy_(friction(e.state.ang_vel.to(t.dtype), ang, e.moment_of_inertia))
 
     def _repoint(self, out: torch.Tensor) -> None:
         """Re-point the integrated fields at views of the fresh buffer (new tensor objects, as the

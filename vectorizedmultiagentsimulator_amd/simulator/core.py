@@ -919,6 +919,11 @@ class World(TorchVectorizedObject):
         ]
         self.entity_index_map = {}
         self.broadphase = "batch"
+        # World.forces_dict / torques_dict (core.py:1975-1992) are exported by the step only when
+        # asked for: each dynamic entity's last-substep totals (12 B per entity and env)
+        self.export_forces = False
+        self._forces_dict = None
+        self._torques_dict = None
         self._engine = None
 
     def add_agent(self, agent: Agent):
@@ -1039,6 +1044,22 @@ class World(TorchVectorizedObject):
         return value[env_index] if point_based else value
 
     # ---- the step (core.py:1970-2014) -------------------------------------------------------------
+    @property
+    def forces_dict(self):
+        """{entity: [B, 2]} force totals of the last step's last substep (core.py:1975-2198)."""
+        if self._forces_dict is None:
+            raise AttributeError("forces_dict is exported by the step only with world.export_forces = True "
+                                 "(set it before the step)")
+        return self._forces_dict
+
+    @property
+    def torques_dict(self):
+        """{entity: [B, 1]} torque totals of the last step's last substep (core.py:1984-2198)."""
+        if self._torques_dict is None:
+            raise AttributeError("torques_dict is exported by the step only with world.export_forces = True "
+                                 "(set it before the step)")
+        return self._torques_dict
+
     def step(self):
         self.entity_index_map = {e: i for i, e in enumerate(self.entities)}
         self.engine.step()
