@@ -139,3 +139,24 @@ def test_export_leaves_the_step_unchanged_gpu(gpu_device):
     for i in off:
         for k in off[i]:
             assert torch.equal(off[i][k], on[i][k]), (i, k)
+
+
+@pytest.mark.gpu
+def test_force_dicts_graph_mode_gpu(gpu_device):
+    """A replayed step exports the same totals as the eager step (bit-identical), through the
+    graph's own buffer (graph mode: views of the graph's tensors)."""
+    from vectorizedmultiagentsimulator_amd import make_env
+
+    envs = [make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=g, n_agents=4)
+            for g in (True, False)]
+    for env in envs:
+        env.world.export_forces = True
+    for _ in range(6):
+        acts = envs[0].get_random_actions()
+        for env in envs:
+            env.step([a.clone() for a in acts])
+        ga, ea = envs[0].world, envs[1].world
+        for x, y in zip(ga.entities, ea.entities):
+            assert torch.equal(ga.forces_dict[x], ea.forces_dict[y]), x.name
+            assert torch.equal(ga.torques_dict[x], ea.torques_dict[y]), x.name
+    assert envs[0].graph_status == "graph"
