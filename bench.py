@@ -40,9 +40,11 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--scenario", default="balance")
-    p.add_argument("--envs", type=int, default=32768, help="envs per GPU")
-    p.add_argument("--n-agents", type=int, default=4)
-    p.add_argument("--substeps", type=int, default=10)
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the scenario's §8(d) config)")
+    p.add_argument("--n-agents", type=int, default=None, help="default: the scenario's §8(d) config")
+    p.add_argument("--substeps", type=int, default=None,
+                   help="physics substeps; default: the scenario's §8(d) config (balance C2: 10), else the "
+                        "scenario's own World(substeps=...); 0 = the scenario's own")
     p.add_argument("--broadphase", default="batch", choices=["batch", "env"])
     p.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-oracle steps per repeat (0 = skip)")
     p.add_argument("--cpu-repeats", type=int, default=5, help="CPU-oracle repeats (the median is reported)")
@@ -53,8 +55,27 @@ def parse():
     p.add_argument("--graph", default="on", choices=["on", "off"],
                    help="on: make_env(graph_step=True) -- each step replayed as one HIP graph once warm "
                         "(same results as eager; falls back to eager if the step cannot be captured)")
-    p.add_argument("--kw", default="{}", help='extra scenario kwargs as JSON, e.g. \'{"use_agent_lidar": true}\'')
-    return p.parse_args()
+    p.add_argument("--kw", default=None, help='extra scenario kwargs as JSON, e.g. \'{"use_agent_lidar": true}\' '
+                                                '(default: the scenario\'s §8(d) config)')
+    args = p.parse_args()
+    preset = PRESETS.get(args.scenario, {})
+    for k in ("envs", "n_agents", "substeps"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset.get(k, {"envs": 32768, "n_agents": 4, "substeps": 0}[k]))
+    if args.kw is None:
+        args.kw = json.dumps(preset.get("kw", {}))
+    return args
+
+
+# SURVEY.md §8(d) configurations (BASELINE.json configs[1..4]); flags override each field.
+# substeps 0 = the scenario's own World(substeps=...) (transport 1, discovery 2, flocking 5 --
+# ref flocking.py:36); only C2 sets 10 on the world after make_env (§8(d) C2).
+PRESETS = {
+    "balance": {"envs": 32768, "n_agents": 4, "substeps": 10},                          # C2
+    "transport": {"envs": 32768, "n_agents": 4, "substeps": 0},                         # C3
+    "discovery": {"envs": 16384, "n_agents": 8, "substeps": 0, "kw": {"use_agent_lidar": True}},  # C4
+    "flocking": {"envs": 32768, "n_agents": 8, "substeps": 0},                          # C5 (per GPU)
+}
 
 
 def make_world_env(args, device, seed):
@@ -73,20 +94,85 @@ def make_world_env(args, device, seed):
 
 
 def alg_bytes_per_env_step(world) -> int:
-    """read pos/vel/rot/ang_vel of every entity (24 B), write them for every
-    movable-or-rotatable entity (24 B), read every agent's force + torque (12 B), write every
-    LIDAR ray distance (4 B per ray of every agent sensor)."""
+    """SURVEY.md §8d, the physics step's share: read pos/vel/rot/ang_vel of every entity (24 B),
+    write them for every movable-or-rotatable entity (24 B), read every agent's force + torque
+    (12 B).  The LIDAR ray distances (§8d's 4 B per ray) are written by the scenario program, not
+    by the step kernel, so they are charged to that kernel (program_bytes_per_env_step)."""
     ents = world.entities
     e_dyn = sum(1 for e in ents if e.movable or e.rotatable)
     n_agents = len(world.agents)
-    rays = sum(s._angles.shape[-1] for a in world.agents for s in a.sensors if hasattr(s, "_angles"))
-    return 24 * len(ents) + 24 * e_dyn + 12 * n_agents + 4 * rays
+    return 24 * len(ents) + 24 * e_dyn + 12 * n_agents
+
+
+def lidar_rays(world) -> int:
+    return sum(s._angles.shape[-1] for a in world.agents for s in a.sensors if hasattr(s, "_angles"))
+
+
+def program_bytes_per_env_step(env) -> int:
+    """Algorithmic bytes of the scenario's observation / reward / done program per env-step:
+    read pos, vel, rot of every entity once (20 B; its inputs), write every agent's observation
+    and reward (4 B per float, including the LIDAR distances inside the observations -- §8d's
+    4 B per ray) and the done flag (1 B)."""
+    world = env.world
+    out = 20 * len(world.entities) + 1
+    for a in world.agents:
+        obs = env.scenario.observation(a)
+        out += 4 * sum(int(o.shape[-1]) for o in (obs.values() if isinstance(obs, dict) else [obs])) + 4
+    return out
+
+
+def time_program(env, n: int):
+    """GPU time of the scenario program per step: the first agent's reward + observation calls
+    (those launch the fused program(s) k_balance / k_transport / k_flocking / k_discovery_*; the
+    other agents' calls return cached results) after a fresh eager step, captured into a HIP
+    graph and replayed ``n`` times between HIP events, so that the host time of the eager calls
+    is not counted.  Returns (ms per step, timer description); eager events if the calls cannot
+    be captured."""
+    world = env.world
+    a0 = world.agents[0]
+
+    def calls():
+        env.scenario.reward(a0)
+        env.scenario.observation(a0)
+
+    world.step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            calls()
+        g.replay()
+        e0.record()
+        for _ in range(n):
+            g.replay()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n, f"HIP events around {n} replays of the captured calls"
+    except Exception as exc:  # noqa: BLE001 -- report how it was timed instead
+        ms = []
+        for _ in range(n):
+            world.step()
+            e0.record()
+            calls()
+            e1.record()
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        return statistics.median(ms), f"HIP events around eager calls (capture failed: {type(exc).__name__})"
 
 
 def kernel_source_hash(world) -> str:
     """sha256 of the generated step kernel's source (k_world) -- what a PMC record must match."""
     src = world.engine.jit_source()
-    return hashlib.sha256(src.encode()).hexdigest() if src else ""
+    if not src:
+        return ""
+    # the generated source #includes these at compile time (hipRTC reads them from csrc/ and
+    # include/): the kernel's identity is the source AND their text
+    h = hashlib.sha256(src.encode())
+    for f in ("vectorizedmultiagentsimulator_amd/csrc/vmas_jit_ops.hpp",
+              "vectorizedmultiagentsimulator_amd/csrc/vmas_physics.hpp", "include/vmas_mi355x.h"):
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()
 
 
 def load_pmc(workload: str, kernel: str, src_hash: str) -> dict:
@@ -164,9 +250,38 @@ def cpu_baseline(args):
     }
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, device) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code.  Runs before this process
+    touches the GPU (no HIP call has been made yet; counting devices does not initialise it)."""
+    if device is None or str(device).startswith("cuda"):
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, args.device))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world_size} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -237,6 +352,19 @@ def main():
                 world.step()
             ev_ms, ev_n = world.engine.get_timing(reset=True)
             event_us = 1e3 * ev_ms / ev_n if ev_n else None
+    program = None
+    if on_gpu and args.event_launches > 0:
+        prog_ms, prog_timer = time_program(env, args.event_launches)
+        p_env = program_bytes_per_env_step(env)
+        ach = p_env * args.envs / (prog_ms * 1e-3) / 1e9
+        program = {
+            "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5),
+            "kernel": f"{args.scenario} scenario program (first agent's reward + observation calls)",
+            "us_per_step": round(prog_ms * 1e3, 3), "alg_bytes_per_env_step": p_env,
+            "lidar_rays_per_env": lidar_rays(world),
+            "timer": prog_timer,
+        }
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -250,6 +378,10 @@ def main():
     if json.loads(args.kw):
         workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)
+    src = world.engine.jit_source() if on_gpu else ""
+    # relaxed: the generated step kernel uses hardware rcp / sqrt / exp / log / sin / cos (fp32,
+    # within the oracle tolerance); exact: IEEE div / sqrt, ocml transcendentals
+    math_mode = ("relaxed" if "VMAS_PHYS_RELAXED" in (src or "") else "exact") if on_gpu else "exact (host backend)"
     roofline = None
     if on_gpu and launches:
         per_launch_ms = kernel_ms / launches
@@ -312,8 +444,10 @@ def main():
             "substeps": world._substeps,
             "parallelism": f"replicas x{world_size} (one process per GPU, no collective in the step)",
             "step_mode": step_mode,
+            "math": math_mode,
         },
         "roofline": roofline,
+        "roofline_program": program,
     }
     if rank == 0 and world_size == 1 and args.cpu_steps > 0:
         out["cpu_baseline"] = cpu_baseline(args)

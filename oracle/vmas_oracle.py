@@ -933,15 +933,57 @@ def sensitivity_band(world, snap, expected, broadphase="batch", n=2, eps=1.2e-7,
 # per-env smallest |dist - cut-off| over every contact evaluation of the step
 # (OracleWorld.cutoff_margin); an env is certified when it is <= ``cutoff_tol``: 4e-6, i.e.
 # a few tens of fp32 ulps at the configs' contact distances (0.05-0.3), which covers the
-# last-bit state drift of up to 10 substeps before the crossing.  ``max_bad_frac`` (default 0)
-# additionally allows uncertified envs (kept for callers that opt in; no test does).
+# last-bit state drift of up to 10 substeps before the crossing.  A certified env's error is
+# still BOUNDED (``cutoff_bound``): by what contact switches can change in one step -- each of an
+# entity's (E - 1) pairs toggling a force of c * k * log 2 (the soft force at dist == dist_min)
+# in each of the S substeps, twice over:
+#   vel     <= 2 S (E-1) c k log2 sub_dt / m_min          pos <= vel bound * dt
+#   ang_vel <= 2 S (E-1) c k log2 lever sub_dt / I_min    rot <= ang_vel bound * dt
+# (lever = the largest circumscribed radius; agent force / torque: no contact term, tolerance
+# only).  ``max_bad_frac`` (default 0) additionally allows uncertified envs (kept for callers
+# that opt in; no test does).
 CUTOFF_TOL = 4e-6
+
+
+def cutoff_bound(world) -> Dict[str, float]:
+    """Per-field bound of a certified cut-off env's error (see CUTOFF_TOL)."""
+    ents = world.entities
+    dyn = [e for e in ents if e.movable or e.rotatable]
+    if not dyn:
+        return {}
+    f_jump = float(world._collision_force) * float(world._contact_margin) * math.log(2.0)
+    S, sdt = int(world._substeps), float(world._sub_dt)
+    dt = S * sdt
+    pairs = max(len(ents) - 1, 1)
+    m_min = min(float(e.mass) for e in dyn)
+    rot = [e for e in ents if e.rotatable]
+    i_min = min(float(e.moment_of_inertia) for e in rot) if rot else 1.0
+    lever = max(float(_circ_radius(e.shape)) for e in ents)
+    v = 2 * S * pairs * f_jump * sdt / m_min
+    w = 2 * S * pairs * f_jump * lever * sdt / i_min
+    return {"vel": v, "pos": v * dt, "ang_vel": w, "rot": w * dt, "force": 0.0, "torque": 0.0}
+
+
+def _circ_radius(shape) -> float:
+    k = _kind(shape)
+    if k == "Sphere":
+        return shape.radius
+    if k == "Box":
+        return math.sqrt((shape.length / 2) ** 2 + (shape.width / 2) ** 2)
+    return shape.length / 2
 
 
 def compare(a: Dict[int, dict], b: Dict[int, dict], world=None, atol_pos=1e-5, atol_vel=1e-4, rtol=1e-4,
             band=None, band_factor=4.0, max_bad_frac=0.0, cutoff=None, cutoff_tol=CUTOFF_TOL):
-    worst = {}
+    """Engine result ``a`` vs oracle result ``b`` under the stated tolerance (see CUTOFF_TOL).
+    ``cutoff`` (per-env margins) enables certification; a certified env must still stay within
+    ``cutoff_bound(world)`` + the tolerance.  The report carries the numbers a reader needs:
+    bad / uncertified envs, the largest cut-off margin among certified envs, the largest error of
+    a certified env as a fraction of its bound, max |diff| and the band's max per field."""
+    worst, band_max = {}, {}
     bad_envs = None
+    excess = []  # per field: (diff - tol) / bound per env, for the certification bound
+    bound = cutoff_bound(world) if (world is not None and cutoff is not None) else {}
     for i in a:
         for k, va in a[i].items():
             vb = b[i][k].to(va.device)
@@ -949,9 +991,17 @@ def compare(a: Dict[int, dict], b: Dict[int, dict], world=None, atol_pos=1e-5, a
             tol = (atol_pos if k in ("pos", "rot") else atol_vel) + rtol * vb.abs()
             if band is not None:
                 tol = tol + band_factor * band[i][k]
-            bad = (diff > tol) | torch.isnan(va).ne(torch.isnan(vb))
+                band_max[k] = max(band_max.get(k, 0.0), float(band[i][k].max()) if band[i][k].numel() else 0.0)
+            nan_mis = torch.isnan(va).ne(torch.isnan(vb))
+            bad = (diff > tol) | nan_mis
             bad = bad.reshape(bad.shape[0], -1).any(-1)
             bad_envs = bad if bad_envs is None else (bad_envs | bad)
+            if bound:
+                over = (diff - tol).clamp_min(0.0).nan_to_num(float("inf"))
+                over = torch.where(nan_mis, torch.full_like(over, float("inf")), over)
+                over = over.reshape(over.shape[0], -1).amax(-1)
+                bk = bound.get(k, 0.0)
+                excess.append(over / bk if bk > 0 else torch.where(over > 0, float("inf"), 0.0))
             m = float(diff.nan_to_num(0.0).max()) if diff.numel() else 0.0
             name = world.entities[i].name if world is not None else str(i)
             if m > worst.get(k, (0.0, ""))[0]:
@@ -960,28 +1010,37 @@ def compare(a: Dict[int, dict], b: Dict[int, dict], world=None, atol_pos=1e-5, a
     n_env = int(bad_envs.numel()) if bad_envs is not None else 1
     rep = {"bad_envs": n_bad, "n_envs": n_env}
     uncertified = n_bad
+    rep["certified_envs"] = 0
     if n_bad and cutoff is not None:
         idx = bad_envs.nonzero().flatten()
         margins = cutoff[idx]
-        cert = margins <= cutoff_tol
+        frac = torch.stack(excess).amax(0)[idx] if excess else torch.zeros(len(idx))
+        cert = (margins <= cutoff_tol) & (frac <= 1.0)
         uncertified = int((~cert).sum())
+        rep["certified_envs"] = int(cert.sum())
         rep["bad_env_cutoff_margins"] = [(int(i), float(m)) for i, m in zip(idx[:16], margins[:16])]
+        if bool(cert.any()):
+            rep["certified_max_margin"] = float(margins[cert].max())
+            rep["certified_max_bound_frac"] = float(frac[cert].max())
     rep["uncertified_envs"] = uncertified
     rep["ok"] = uncertified <= max_bad_frac * n_env
     rep["max_abs"] = {k: v[0] for k, v in worst.items()}
     rep["where"] = {k: v[1] for k, v in worst.items()}
+    if band_max:
+        rep["band_max"] = band_max
     return rep
 
 
-def compare_one_step(world, broadphase: str = "batch", with_band: bool = True, **tol):
-    """Teacher-forced one-step parity: native engine vs this oracle from the same state."""
+def compare_one_step(world, broadphase: str = "batch", with_band: bool = True, certify: bool = True, **tol):
+    """Teacher-forced one-step parity: native engine vs this oracle from the same state.
+    certify=False: no cut-off certification (a strict run: every env must be within tolerance)."""
     snap = snapshot(world)
     expected, ow = oracle_step(world, snap, broadphase)
     band = sensitivity_band(world, snap, expected, broadphase) if with_band else None
     world.broadphase = broadphase
     world.step()
     got = snapshot(world)
-    rep = compare(got, expected, world, band=band, cutoff=ow.cutoff_margin, **tol)
+    rep = compare(got, expected, world, band=band, cutoff=ow.cutoff_margin if certify else None, **tol)
     rep["iterations"] = getattr(world.engine, "last_iterations", None)
     rep["active_pairs_per_substep"] = [len(x) for x in ow.active_log]
     return rep

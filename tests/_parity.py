@@ -28,14 +28,49 @@ def make(name, kw, substeps, device, num_envs, seed):
     return env
 
 
-def step_parity(env, n_steps, broadphase="batch", max_bad_frac=0.0):
-    """Free-run the engine on random actions; after each step compare one teacher-forced step."""
+def step_parity(env, n_steps, broadphase="batch", max_bad_frac=0.0, certify=True):
+    """Free-run the engine on random actions; after each step compare one teacher-forced step.
+    certify=False: no cut-off certification (every env outside the tolerance counts as bad)."""
     reports = []
     for _ in range(n_steps):
         env.step(env.get_random_actions())
-        rep = O.compare_one_step(env.world, broadphase=broadphase, max_bad_frac=max_bad_frac)
+        rep = O.compare_one_step(env.world, broadphase=broadphase, max_bad_frac=max_bad_frac, certify=certify)
         reports.append(rep)
     return reports
+
+
+# Parity numbers of this session, printed as one "PARITY {json}" line per config at the end of
+# the run (tests/conftest.py pytest_terminal_summary), so that they land in the driver's log tail.
+SUMMARY = []
+
+
+def summarize(config, env, reps, lidar=None):
+    """Fold the per-step reports of one config into one record (and keep it for the summary)."""
+    w = env.world
+    eng = getattr(w, "engine", None)
+    src = eng.jit_source() if (eng is not None and eng.kernel_name == "k_world") else ""
+    rec = {
+        "config": config,
+        "device": str(w.device),
+        "kernel": getattr(eng, "kernel_name", None),
+        "math": ("relaxed" if "VMAS_PHYS_RELAXED" in src else "exact") if src else "exact",
+        "envs": reps[0]["n_envs"] if reps else 0,
+        "steps": len(reps),
+        "substeps": w._substeps,
+        "bad_envs": sum(r["bad_envs"] for r in reps),
+        "certified_envs": sum(r.get("certified_envs", 0) for r in reps),
+        "uncertified_envs": sum(r["uncertified_envs"] for r in reps),
+        "certified_max_margin": max((r.get("certified_max_margin", 0.0) for r in reps), default=0.0),
+        "certified_max_bound_frac": max((r.get("certified_max_bound_frac", 0.0) for r in reps), default=0.0),
+        "max_abs": {k: max(r["max_abs"].get(k, 0.0) for r in reps) for k in reps[0]["max_abs"]} if reps else {},
+        "band_max": {k: max(r.get("band_max", {}).get(k, 0.0) for r in reps) for k in reps[0].get("band_max", {})}
+        if reps else {},
+        "passes": [r.get("iterations") for r in reps],
+    }
+    if lidar is not None:
+        rec["lidar"] = {k: lidar[k] for k in ("rows", "bad_rows", "uncertified_rows", "max_abs")}
+    SUMMARY.append(rec)
+    return rec
 
 
 # ray perturbations that certify a LIDAR mismatch as a hit/miss boundary case: the engine's value

@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from oracle import vmas_oracle as O
-from tests._parity import make, step_parity
+from tests._parity import make, step_parity, summarize
 
 
 def _check_comm(env):
@@ -63,7 +63,9 @@ def test_sub_dt_attribute_host():
 @pytest.mark.gpu
 def test_features_full_size_gpu(gpu_device):
     env = make("features", dict(n_agents=8), None, gpu_device, num_envs=16384, seed=0)
-    for rep in step_parity(env, n_steps=2):
+    reps = step_parity(env, n_steps=2)
+    summarize("features 16384 envs n_agents=8", env, reps)
+    for rep in reps:
         assert rep["ok"], rep
     assert env.world.engine.kernel_name == "k_world", env.world.engine.jit_error
     _check_comm(env)

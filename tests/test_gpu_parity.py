@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import vmas_oracle as O
-from tests._parity import SCENARIOS, distance_parity, lidar_parity, make, step_parity
+from tests._parity import SCENARIOS, distance_parity, lidar_parity, make, step_parity, summarize
 
 pytestmark = pytest.mark.gpu
 
@@ -25,7 +25,9 @@ def _native_loaded():
 @pytest.mark.parametrize("name,kw,substeps", SCENARIOS, ids=[s[0] for s in SCENARIOS])
 def test_step_parity_gpu(gpu_device, name, kw, substeps):
     env = make(name, kw, substeps, gpu_device, num_envs=200, seed=0)
-    for rep in step_parity(env, n_steps=4):
+    reps = step_parity(env, n_steps=4)
+    summarize(f"{name} 200 envs", env, reps)
+    for rep in reps:
         assert rep["ok"], rep
     assert _native_loaded()
     assert env.world.engine._dev_index == 0
@@ -45,7 +47,9 @@ def test_lidar_distance_parity_gpu(gpu_device, name, kw, substeps):
 def test_balance_full_size_gpu(gpu_device):
     """C2 at full size: 32 768 envs, n_agents=4, 10 substeps."""
     env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=32768, seed=0)
-    for rep in step_parity(env, n_steps=2):
+    reps = step_parity(env, n_steps=2)
+    summarize("C2 balance 32768 envs n_agents=4 substeps=10", env, reps)
+    for rep in reps:
         assert rep["ok"], rep
 
 
@@ -93,7 +97,27 @@ def test_baseline_configs_full_size_gpu(gpu_device, name, kw, envs):
     """BASELINE.json configs C3-C5 at their full per-GPU sizes: teacher-forced step parity and
     LIDAR parity against the oracle (only certified cut-off envs may differ)."""
     env = make(name, kw, None, gpu_device, num_envs=envs, seed=0)
-    for rep in step_parity(env, n_steps=2):
+    reps = step_parity(env, n_steps=2)
+    lid = lidar_parity(env)
+    summarize(f"{name} {envs} envs {kw}", env, reps, lidar=lid)
+    for rep in reps:
         assert rep["ok"], rep
-    rep = lidar_parity(env)
-    assert rep["ok"], rep
+    assert lid["ok"], lid
+
+
+@pytest.mark.parametrize("name,kw,substeps,envs", [
+    ("balance", dict(n_agents=4), 10, 1024),
+    ("transport", dict(n_agents=4), None, 1024),
+    ("discovery", dict(n_agents=8, use_agent_lidar=True), None, 1024),
+    ("flocking", dict(n_agents=8), None, 1024),
+    ("features", dict(n_agents=4), None, 1024),
+], ids=["balance", "transport", "discovery", "flocking", "features"])
+def test_exact_math_strict_gpu(gpu_device, monkeypatch, name, kw, substeps, envs):
+    """VMAS_JIT_MATH=exact (IEEE div / sqrt, ocml transcendentals) with NO cut-off waiver: every
+    env of every step within the stated tolerance (atol/rtol + 4x the 1-ulp band)."""
+    monkeypatch.setenv("VMAS_JIT_MATH", "exact")
+    env = make(name, kw, substeps, gpu_device, num_envs=envs, seed=5)
+    reps = step_parity(env, n_steps=3, certify=False)
+    rec = summarize(f"{name} {envs} envs exact-math strict", env, reps)
+    assert rec["math"] == "exact"
+    assert rec["bad_envs"] == 0, [r for r in reps if r["bad_envs"]]

@@ -147,28 +147,39 @@ def test_fixed_point_no_convergence_poisons_outputs_gpu(gpu_device, monkeypatch)
 
 
 @pytest.mark.gpu
-def test_fixed_point_with_cus_held_by_another_stream_gpu(gpu_device):
+@pytest.mark.parametrize("envs,cap,held", [(32768, None, 224), (2048, None, 250), (32768, "16", 250)],
+                         ids=["32768envs-224cus", "2048envs-250cus", "grid16-250cus"])
+def test_fixed_point_with_cus_held_by_another_stream_gpu(gpu_device, monkeypatch, envs, cap, held):
     """A kernel on a second stream holds most of the chip's wave slots for 0.5 s while the step
     launches: part of the step's grid cannot become resident until it ends.  Workgroups only wait
     for groups that running workgroups have claimed, so the step completes exactly (oracle parity,
-    no error bit; the resident workgroups steal the groups of the absent ones)."""
+    no error bit; the resident workgroups steal the groups of the absent ones).  Small grids
+    (<= 32 workgroups: one workgroup per start shard) and a capped grid are included: the final
+    decider must wait for the late workgroups' starts before advancing the epoch, or a late
+    workgroup would run the NEXT step's pass on stale inputs -- so the step after the held one is
+    checked too."""
     from vectorizedmultiagentsimulator_amd import _native as N
 
-    env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=32768, seed=0)
+    if cap is not None:
+        monkeypatch.setenv("VMAS_JIT_GRID_CAP", cap)
+    env = make("balance", dict(n_agents=4), 10, gpu_device, num_envs=envs, seed=0)
     env.step(env.get_random_actions())
     w = env.world
-    snap = O.snapshot(w)
-    expected, ow = O.oracle_step(w, snap)
-    band = O.sensitivity_band(w, snap, expected)
-    side = torch.cuda.Stream()
-    torch.cuda.synchronize()
-    N.check_aux(N.load_library().vmas_test_hold(0, 224, 500_000, ctypes.c_void_p(side.cuda_stream)),
-                "vmas_test_hold")
-    w.step()
-    torch.cuda.synchronize()
-    w.engine.check_device_errors()
-    rep = O.compare(O.snapshot(w), expected, w, band=band, cutoff=ow.cutoff_margin)
-    assert rep["ok"], rep
+    for held_step in (True, False):
+        snap = O.snapshot(w)
+        expected, ow = O.oracle_step(w, snap)
+        band = O.sensitivity_band(w, snap, expected)
+        if held_step:
+            side = torch.cuda.Stream()
+            torch.cuda.synchronize()
+            N.check_aux(N.load_library().vmas_test_hold(0, held, 500_000, ctypes.c_void_p(side.cuda_stream)),
+                        "vmas_test_hold")
+        w.step()
+        torch.cuda.synchronize()
+        w.engine.check_device_errors()
+        rep = O.compare(O.snapshot(w), expected, w, band=band, cutoff=ow.cutoff_margin)
+        assert rep["ok"], (held_step, rep)
+    assert w.engine.kernel_name == "k_world"
 
 
 @pytest.mark.gpu

@@ -3,13 +3,15 @@ CPU oracle: one teacher-forced World.step per check, LIDAR scans and distance qu
 Tolerances: oracle.vmas_oracle.compare (fp32 atol/rtol + 4x the system's 1-ulp sensitivity)."""
 import pytest
 
-from tests._parity import SCENARIOS, distance_parity, lidar_parity, make, step_parity
+from tests._parity import SCENARIOS, distance_parity, lidar_parity, make, step_parity, summarize
 
 
 @pytest.mark.parametrize("name,kw,substeps", SCENARIOS, ids=[s[0] for s in SCENARIOS])
 def test_step_parity_host(name, kw, substeps):
     env = make(name, kw, substeps, "cpu", num_envs=48, seed=0)
-    for rep in step_parity(env, n_steps=4):
+    reps = step_parity(env, n_steps=4)
+    summarize(f"{name} 48 envs (host backend)", env, reps)
+    for rep in reps:
         assert rep["ok"], rep
 
 

@@ -13,9 +13,15 @@ namespace vmas {
 #define __HIP_MEMORY_SCOPE_AGENT 4
 #endif
 
-// Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily).
-// (kGridErrStateTimeout belonged to an earlier spin-waiting launch; no code sets it.)
+// Sticky error bits of the device-side fixed point (vmas_jit.hip reads them back lazily):
+// kGridErrNoConverge -- the fixed point did not converge within max_pass passes;
+// kGridErrStateTimeout -- the final decider waited kGridStartWaitTicks for a workgroup of the
+// launch to be dispatched (grid_decide).  Both NaN-poison the step's outputs.
 constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
+// Bound of the final decider's wait for the dispatcher, in s_memrealtime ticks (100 MHz): 10 s.
+// Far above any real dispatch delay (a kernel of another stream holding the CUs for 0.5 s is
+// tested), low enough that a stuck dispatch fails the step instead of hanging it.
+constexpr unsigned long long kGridStartWaitTicks = 1000000000ull;
 
 // Device-side fixed point of the batch-global broadphase (core.py:2796) in ONE persistent launch
 // whose only cross-workgroup waits are for work that a RUNNING workgroup has claimed -- so nothing
@@ -52,10 +58,14 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 //     workgroups are resident (a workgroup that only becomes resident later finds every group
 //     claimed and the decisions published, and follows them to the exit).
 //   * The decider of the final pass then waits until every workgroup of the launch has read E
-//     (a start counter sharded like the completions, each shard at a multiple of its workgroups;
-//     a workgroup adds its start before its first wait for a decision -- off its critical path
-//     -- and the decider counts itself), advances E past the launch's passes and clears the mask
-//     if a re-run changed it.  The decision is published before that wait, so every other
+//     (a start counter sharded like the completions; a workgroup adds its start before its first
+//     wait for a decision -- off its critical path -- and the decider counts itself), advances E
+//     past the launch's passes and clears the mask if a re-run changed it.  The starts are
+//     cumulative over launches, so the wait is for an ABSOLUTE count: the sum of the shards equal
+//     to kGridStartBase (the starts of every earlier launch, advanced by each launch's final
+//     decider) + gridDim.x.  (A per-shard residue test cannot tell a shard nobody has started
+//     in from a full one.)  The wait is bounded (kGridStartWaitTicks): past it the step fails
+//     with kGridErrStateTimeout and NaN outputs instead of hanging.  The decision is published before that wait, so every other
 //     workgroup is leaving and the slots the remaining ones need are free: this wait is for the
 //     dispatcher, never for another workgroup's progress.
 // Memory order (MI355X_MICROARCH.md, the sc1 hand-off forms): every byte handed between
@@ -70,13 +80,14 @@ constexpr uint32_t kGridErrNoConverge = 2u, kGridErrStateTimeout = 4u;
 // decision that precedes the re-run.
 //
 // ctl (uint32 words; each 64-bit word on a 128-byte line of its own): [2] passes run by the last
-// step (u32, read by the host); u64 words: kGridEpoch (E), kGridCand (candidate word), kGridTop
+// step (u32, read by the host); u64 words: kGridEpoch (E), kGridStartBase (starts of every
+// earlier launch), kGridCand (candidate word), kGridTop
 // (top completion counter), kGridDone + 32 * k (completion shard k: groups g % 32 == k),
 // kGridDec + 2 * p (dec[p], contiguous), kGridStart + 32 * k (start shard k: workgroups
 // blockIdx % 32 == k).  Then the mask words and, from the next multiple of 32 words, the claim
 // words (u64, kClaimStride words apart).
 constexpr int kGridMaxPasses = 64, kGridShards = 32;
-constexpr int kGridEpoch = 32, kGridCand = 96, kGridTop = 128, kGridDone = 160;
+constexpr int kGridEpoch = 32, kGridStartBase = 64, kGridCand = 96, kGridTop = 128, kGridDone = 160;
 constexpr int kGridDec = kGridDone + 32 * kGridShards;
 constexpr int kGridStart = kGridDec + 2 * kGridMaxPasses;
 constexpr int kGridCtlWords = kGridStart + 32 * kGridShards;
@@ -200,17 +211,13 @@ __device__ __forceinline__ void grid_started(uint32_t* ctl) {
     (void)add64(&ctl[kGridStart + 32 * (int)(blockIdx.x % kGridShards)], 1ull);
 }
 
-// Every workgroup of the launch has counted its start -- but this one when `self` is false (wave
-// 0; every shard at a multiple of its workgroups, this workgroup's shard one short if not self).
-__device__ __forceinline__ bool grid_all_started(const uint32_t* ctl, bool self) {
+// Starts counted so far over every launch (the first 64 threads; wave-uniform result): the sum
+// of the start shards.
+__device__ __forceinline__ u64 grid_starts(const uint32_t* ctl) {
     const uint32_t nsh = gridDim.x < (uint32_t)kGridShards ? gridDim.x : (uint32_t)kGridShards;
-    bool ok = true;
-    if (threadIdx.x < nsh) {
-        const uint32_t k = threadIdx.x, n_k = (gridDim.x + kGridShards - 1u - k) / kGridShards;
-        const u64 want = (!self && k == blockIdx.x % kGridShards) ? (u64)(n_k - 1u) : 0ull;
-        ok = ld64(&ctl[kGridStart + 32 * (int)k]) % (u64)n_k == want;
-    }
-    return __ballot(!ok) == 0ull;
+    u64 v = threadIdx.x < nsh ? ld64(&ctl[kGridStart + 32 * (int)threadIdx.x]) : 0ull;
+    for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return __shfl(v, 0, 64);
 }
 
 // Completion of group g in global pass G (all threads; the group's row and outputs are stored).
@@ -302,9 +309,25 @@ __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, const u
     }
     if (!more) {  // the step's final pass: wait for every start, then advance E (see the header)
         const bool self = CUR->started != 0;
-        if (threadIdx.x < 64)
-            while (!grid_all_started(ctl, self)) __builtin_amdgcn_s_sleep(8);
+        if (threadIdx.x < 64) {
+            const u64 base = ld64(&ctl[kGridStartBase]);
+            const u64 want = base + (u64)gridDim.x - (self ? 0ull : 1ull);
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            bool late = false;
+            while (grid_starts(ctl) != want) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kGridStartWaitTicks) {
+                    late = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (threadIdx.x == 0) {
+                st64(&ctl[kGridStartBase], base + (u64)gridDim.x);
+                RED[nw2 + 1] = late ? 2u : (viol ? 1u : 0u);
+            }
+        }
         if (threadIdx.x == 0) {
+            if (RED[nw2 + 1] == 2u) report_err(err, herr, kGridErrStateTimeout);
             st64(&ctl[kGridEpoch], G + 1ull);
             if (!self) {
                 grid_started(ctl);
@@ -317,7 +340,7 @@ __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, const u
             for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], 0u);
     }
     __syncthreads();
-    return viol && !more;
+    return RED[nw2 + 1] == 2u || (viol && !more);
 }
 
 // Wait for the decision of global pass G (all threads): true when another pass follows.  The
