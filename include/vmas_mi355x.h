@@ -595,10 +595,13 @@ int32_t vmas_cast_rays_vjp(int32_t device, int32_t batch, int32_t n_rays, const 
 
 /* World-specialised step (csrc/vmas_jit.hip): same seam and semantics as vmas_world_create /
  * vmas_world_step (World.step, core.py:1971-2014), GPU only.  vmas_jit_world_create generates a
- * gfx950 kernel for this exact world (constants folded, per-wave straight-line pair/entity code)
- * and compiles it with hipRTC; it returns VMAS_E_INVALID for worlds beyond its argument-block or
- * LDS budget, in which case the caller uses vmas_world_step.  Results are bit-identical to
- * vmas_world_step. */
+ * gfx950 kernel for this exact world structure (shapes, pairs and flags folded, per-wave
+ * straight-line pair/entity code; parameter values are kernel arguments, see
+ * vmas_jit_world_set_params) and compiles it with hipRTC (an in-process cache of the most
+ * recently used code objects, keyed by the generated source, serves identical structures); it
+ * returns VMAS_E_INVALID for worlds beyond its argument-block or LDS budget, in which case the
+ * caller uses vmas_world_step.  With VMAS_JIT_MATH=exact (always for worlds with joints) results
+ * are bit-identical to vmas_world_step. */
 typedef struct VmasJitWorld VmasJitWorld;
 int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
                               const VmasPairDesc* pairs, const VmasJointDesc* joints,
@@ -612,6 +615,18 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* world);
  * is returned by vmas_jit_world_passes and by the next vmas_jit_world_step. */
 int32_t vmas_jit_world_step(VmasJitWorld* world, const VmasStepIO* io, void* stream,
                             int32_t* iterations);
+/* New parameter VALUES for a world of the same structure (the entity attributes a scenario may
+ * change between steps -- mass and inertia (ref scenarios/debug/het_mass.py:48-54 re-rolls them on
+ * every reset), drag, frictions, max_speed, v_range, force / torque limits; Entity setters,
+ * core.py:537-1085).  They are kernel arguments of the generated kernel, so no recompilation: the
+ * next vmas_jit_world_step uses them.  Returns VMAS_E_INVALID (and changes nothing) when anything
+ * else differs from the world's tables: shapes and dimensions, flags (which limits / frictions /
+ * gravity apply), slots, pairs, joints, world constants and the world's gravity / semidims (folded
+ * into the code; the caller then creates a new world), batch, device.  A graph that captured a
+ * step keeps the values it captured. */
+int32_t vmas_jit_world_set_params(VmasJitWorld* world, const VmasWorldConfig* cfg,
+                                  const VmasEntityDesc* entities, const VmasPairDesc* pairs,
+                                  const VmasJointDesc* joints);
 /* Error bits the kernel has reported so far, without waiting (VMAS_OK if none): how a launch
  * replayed from a HIP graph surfaces a device-side fixed-point failure. */
 int32_t vmas_jit_world_check(VmasJitWorld* world);
@@ -640,6 +655,10 @@ int32_t vmas_jit_compile_check(const VmasWorldConfig* cfg, const VmasEntityDesc*
  * with VMAS_JIT_PROFILE=<workgroup> set: [max_substeps*4 + 2][8 waves]; returns the count. */
 int32_t vmas_jit_world_profile(VmasJitWorld* world, uint64_t* out, int64_t cap);
 const char* vmas_jit_last_error(void);
+/* hipRTC compiles done by this process so far and the code objects held by the bounded cache
+ * (at most 32, VMAS_JIT_CACHE overrides).  Test / diagnostics entry point, no reference
+ * counterpart. */
+int32_t vmas_jit_stats(int64_t* compiles, int64_t* cached);
 
 #ifdef __cplusplus
 }

@@ -69,17 +69,19 @@ def _features(device, num_envs):
     return env
 
 
-def test_force_dicts_require_export():
+def test_force_dicts_by_default():
+    """Like the reference (core.py:1975-1992), every step leaves forces_dict / torques_dict; a
+    world with export_forces = False has none."""
     env = make("balance", dict(n_agents=2), None, "cpu", num_envs=4, seed=0)
-    env.step(env.get_random_actions())
-    with pytest.raises(AttributeError, match="export_forces"):
-        env.world.forces_dict
-    env.world.export_forces = True
     env.step(env.get_random_actions())
     fd = env.world.forces_dict
     assert set(fd) == set(env.world.entities)
     assert all(v.shape == (4, 2) for v in fd.values())
     assert all(v.shape == (4, 1) for v in env.world.torques_dict.values())
+    env.world.export_forces = False
+    env.step(env.get_random_actions())
+    with pytest.raises(AttributeError, match="export_forces"):
+        env.world.forces_dict
 
 
 @pytest.mark.parametrize("name,kw", [("features", dict(n_agents=4)), ("waterfall", dict(n_agents=5))])

@@ -209,3 +209,57 @@ def test_jit_nan_state_matches_oracle_gpu(gpu_device, name, kw, substeps):
         a.state.pos[17, 1] = float("nan")
     report = O.compare_one_step(env.world)
     assert report["ok"], report
+
+
+def _reroll(world, gen):
+    """New values for every mutable entity parameter (structure unchanged): masses (ref
+    het_mass.py:50-55), drags, and the world drag."""
+    for e in world.entities:
+        if e.movable:
+            e.mass = float(e.mass) * (0.5 + gen.random())
+            e._drag = 0.1 + 0.3 * gen.random()
+    world._drag = 0.2 + 0.1 * gen.random()
+
+
+def test_jit_source_is_independent_of_parameter_values():
+    """The generated kernel source (hence the code object) does not depend on mass / drag values:
+    only on the world's structure (CPU: generated + hipRTC-compiled without a device)."""
+    import random
+
+    env = make("balance", dict(n_agents=4), 10, "cpu", num_envs=64, seed=0)
+    src0 = env.world.engine.jit_compile_check()
+    _reroll(env.world, random.Random(0))
+    src1 = env.world.engine.jit_compile_check()
+    assert src0 == src1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_mutable_params_one_compile_gpu(gpu_device, graph):
+    """het_mass (ref scenarios/debug/het_mass.py:48-54) re-rolls the agents' masses on every
+    reset, and balance here re-rolls every movable entity's mass and drag (plus the world drag)
+    before each step: exactly one hipRTC compile per world structure, and every step at oracle
+    parity with the new values."""
+    import random
+
+    from vectorizedmultiagentsimulator_amd import _native as N
+    from vectorizedmultiagentsimulator_amd import make_env
+
+    gen = random.Random(1)
+    for name, kw, resets in (("het_mass", {}, 6), ("balance", dict(n_agents=4), 6)):
+        env = make_env(name, num_envs=256, device=gpu_device, seed=0, graph_step=graph, **kw)
+        env.step(env.get_random_actions())
+        c0, _ = N.jit_stats()
+        jit0 = env.world.engine._jit.value
+        for _ in range(resets):
+            env.reset()
+            if name == "balance":
+                _reroll(env.world, gen)
+            for _ in range(3):
+                env.step(env.get_random_actions())
+            rep = O.compare_one_step(env.world)
+            assert rep["ok"], (name, rep)
+        c1, cached = N.jit_stats()
+        assert c1 == c0, f"{name}: {c1 - c0} recompiles for parameter changes"
+        assert env.world.engine._jit.value == jit0  # the same world kernel object throughout
+        assert cached <= 32

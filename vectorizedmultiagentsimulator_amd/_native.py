@@ -94,6 +94,8 @@ EXPORTED_SYMBOLS = (
     "vmas_jit_world_passes",
     "vmas_jit_world_check",
     "vmas_jit_world_grid",
+    "vmas_jit_world_set_params",
+    "vmas_jit_stats",
     "vmas_jit_last_error",
 )
 
@@ -587,6 +589,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_jit_world_check.argtypes = [_vp]
     lib.vmas_jit_world_grid.restype = _i32
     lib.vmas_jit_world_grid.argtypes = [_vp]
+    lib.vmas_jit_world_set_params.restype = _i32
+    lib.vmas_jit_world_set_params.argtypes = [_vp, _vp, _vp, _vp, _vp]
+    lib.vmas_jit_stats.restype = _i32
+    lib.vmas_jit_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     lib.vmas_jit_last_error.restype = ctypes.c_char_p
     ver = lib.vmas_abi_version()
     if ver != VMAS_ABI_VERSION:
@@ -614,3 +620,10 @@ def check_aux(rc: int, what: str) -> None:
     if rc != 0:
         msg = load_library().vmas_aux_last_error().decode(errors="replace")
         raise NativeLibraryError(f"{what} failed ({rc}): {msg}")
+
+
+def jit_stats():
+    """(hipRTC compiles so far, code objects in the bounded cache) of this process."""
+    c, n = ctypes.c_int64(0), ctypes.c_int64(0)
+    load_library().vmas_jit_stats(ctypes.byref(c), ctypes.byref(n))
+    return c.value, n.value

@@ -144,6 +144,28 @@ constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (1
 
 // pointer-table sources of the kernel argument block
 enum Src { S_POS, S_VEL, S_ROT, S_ANG, S_GRAV, S_FORCE, S_TORQUE, S_JFIX };
+constexpr unsigned kPrmMaskDefault = 0x7FFu;
+// value fields of VmasEntityDesc passed as kernel arguments (Gen::value_fields)
+enum Prm { kPrmMass, kPrmInertia, kPrmDrag, kPrmLinFric, kPrmAngFric, kPrmMaxSpeed, kPrmVRange, kPrmMaxF, kPrmFRange,
+           kPrmMaxT, kPrmTRange };
+inline float prm_value(const VmasEntityDesc& d, int k) {
+    switch (k) {
+        case kPrmMass: return d.mass;
+        case kPrmInertia: return d.inertia;
+        case kPrmDrag: return d.one_minus_drag;
+        case kPrmLinFric: return d.lin_fric;
+        case kPrmAngFric: return d.ang_fric;
+        case kPrmMaxSpeed: return d.max_speed;
+        case kPrmVRange: return d.v_range;
+        case kPrmMaxF: return d.max_f;
+        case kPrmFRange: return d.f_range;
+        case kPrmMaxT: return d.max_t;
+        default: return d.t_range;
+    }
+}
+inline float prm_world_value(const VmasWorldConfig& c, int k) {
+    return k == 0 ? c.gravity_x : k == 1 ? c.gravity_y : k == 2 ? c.x_semidim : c.y_semidim;
+}
 
 struct Item {
     int pair, side, torque;
@@ -362,6 +384,7 @@ struct Gen {
         for (int p = 0; p < P; ++p)
             if (pd[p].cls == VMAS_PAIR_JOINT) ptr(S_JFIX, pd[p].joint), str(S_JFIX, 0, pd[p].joint);
         if (str_src.size() % 2) str_src.push_back({-1, 0});  // keep the int block 8-byte aligned
+        plan_params();
         if (arg_bytes() > kMaxArgBytes) {
             *why = "kernel argument block too large (" + it(arg_bytes()) + " B)";
             return false;
@@ -373,8 +396,9 @@ struct Gen {
     size_t n_out() const { return cfg.export_forces ? 8 : 6; }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
-        // (+4 ints: B, S, sdt, max_pass; the struct is padded to its 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4);
+        // (+4 ints: B, S, sdt, max_pass; then the value slots; padded to the 8-byte alignment)
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4) +
+                         4 * prm_src.size();
         return (n + 7) & ~(size_t)7;
     }
 
@@ -458,14 +482,85 @@ struct Gen {
                "] = " + v + ";\n";
     }
 
+    // The STRUCTURE of a dynamic entity (shape, flags, slots, dimensions) is constexpr; its
+    // VALUES (mass, inertia, drag, frictions, speed / force / torque limits) are zero here and
+    // come from the kernel arguments (a.prm, prm_slots), so a world whose values change (a mass
+    // re-rolled on every reset, ref scenarios/debug/het_mass.py:48-54) keeps its code object.
+    // Which values are kernel arguments: bit k = entity value field k (kPrm*), bit 11 = the
+    // world's gravity and semidims.  Default 0x7FF: every entity value an argument, the world's
+    // values folded -- as arguments they cost balance's k_world ~0.8 us (+2.4 %; a folded zero
+    // gravity component and semidim clamps simplify; interleaved A/B, profiles/r03/run8_prm_ab),
+    // and scenarios change world values far more rarely than entity masses (a change rebuilds).
+    // VMAS_JIT_PRM_MASK overrides (A/B).
+    unsigned prm_mask = kPrmMaskDefault;
     std::string desc(int e) const {
         const VmasEntityDesc& d = ed[e];
-        return "{" + it(d.shape) + ", " + it(d.flags) + "u, " + it(d.agent_index) + ", " + it(d.out_lin) + ", " +
-               it(d.out_rot) + ", " + it(d.out_force) + ", " + it(d.out_torque) + ", " + fl(d.radius) + ", " +
-               fl(d.half_length) + ", " + fl(d.half_width) + ", " + fl(d.mass) + ", " + fl(d.inertia) + ", " +
-               fl(d.one_minus_drag) + ", " + fl(d.lin_fric) + ", " + fl(d.ang_fric) + ", " + fl(d.max_speed) + ", " +
-               fl(d.v_range) + ", " + fl(d.max_f) + ", " + fl(d.f_range) + ", " + fl(d.max_t) + ", " +
-               fl(d.t_range) + "}";
+        auto v = [&](int k) { return (prm_mask >> k) & 1u ? std::string("0.f") : fl(prm_value(d, k)); };
+        std::string o = "{" + it(d.shape) + ", " + it(d.flags) + "u, " + it(d.agent_index) + ", " + it(d.out_lin) + ", " +
+                        it(d.out_rot) + ", " + it(d.out_force) + ", " + it(d.out_torque) + ", " + fl(d.radius) + ", " +
+                        fl(d.half_length) + ", " + fl(d.half_width);
+        for (int k = 0; k <= kPrmTRange; ++k) o += ", " + v(k);
+        return o + "}";
+    }
+    // the value fields a dynamic entity's code reads (by its flags), in VmasEntityDesc order
+    std::vector<int> value_fields(const VmasEntityDesc& d) const {
+        std::vector<int> f = value_fields_all(d), out;
+        for (int k : f)
+            if ((prm_mask >> k) & 1u) out.push_back(k);
+        return out;
+    }
+    static std::vector<int> value_fields_all(const VmasEntityDesc& d) {
+        std::vector<int> f;
+        const bool mov = d.flags & VMAS_F_MOVABLE, rotb = d.flags & VMAS_F_ROTATABLE;
+        if (mov) f.push_back(kPrmMass);
+        if (rotb) f.push_back(kPrmInertia);
+        if (mov || rotb) f.push_back(kPrmDrag);
+        if (d.flags & VMAS_F_LIN_FRIC) f.push_back(kPrmLinFric);
+        if (d.flags & VMAS_F_ANG_FRIC) f.push_back(kPrmAngFric);
+        if (d.flags & VMAS_F_MAX_SPEED) f.push_back(kPrmMaxSpeed);
+        if (d.flags & VMAS_F_V_RANGE) f.push_back(kPrmVRange);
+        if (d.flags & VMAS_F_MAX_F) f.push_back(kPrmMaxF);
+        if (d.flags & VMAS_F_F_RANGE) f.push_back(kPrmFRange);
+        if (d.flags & VMAS_F_MAX_T) f.push_back(kPrmMaxT);
+        if (d.flags & VMAS_F_T_RANGE) f.push_back(kPrmTRange);
+        return f;
+    }
+    static const char* field_name(int k) {
+        static const char* n[] = {"mass", "inertia", "one_minus_drag", "lin_fric", "ang_fric", "max_speed",
+                                  "v_range", "max_f", "f_range", "max_t", "t_range"};
+        return n[k];
+    }
+    // kernel-argument value slots: (entity, field) pairs, then the world's gravity x / y and
+    // semidims (kPrmWorld + 0..3); laid out once in plan()
+    std::vector<std::pair<int, int>> prm_src;
+    std::vector<int> prm_of;  // first slot of entity e's fields (-1 if none)
+    int prm_world = -1;
+    void plan_params() {
+        prm_src.clear();
+        prm_of.assign(E, -1);
+        for (int e = 0; e < E; ++e) {
+            if (!dyn[e]) continue;
+            prm_of[e] = (int)prm_src.size();
+            for (int k : value_fields(ed[e])) prm_src.push_back({e, k});
+        }
+        prm_world = (int)prm_src.size();
+        for (int k = 0; k < 4; ++k) prm_src.push_back({-1, k});
+    }
+    // prologue: the value slots into LDS, constant indices only (a loop indexing a.prm
+    // dynamically makes the compiler keep the whole by-value argument block addressable:
+    // balance static VALU +27 %)
+    std::string prm_copy() const {
+        std::string o = "    if (threadIdx.x == 0) {";
+        for (size_t i = 0; i < prm_src.size(); ++i) o += " PRM[" + it((long)i) + "] = a.prm[" + it((long)i) + "];";
+        return o + " }\n";
+    }
+    // the entity's runtime desc: the constexpr structure with its value fields from a.prm
+    std::string runtime_desc(int e, const std::string& I) const {
+        const std::string s = it(e);
+        std::string o = I + "VmasEntityDesc D" + s + " = D" + s + "c;\n";
+        int slot = prm_of[e];
+        for (int k : value_fields(ed[e])) o += I + "D" + s + "." + field_name(k) + " = PRM[" + it(slot++) + "];\n";
+        return o;
     }
 
     void publish(std::string& o, int e, const std::string& ind, bool with_pos, bool with_rot) const {
@@ -667,6 +762,8 @@ struct Gen {
             publish(o, e, "    ", true, true);
             // World.forces_dict / torques_dict: the totals of the last substep (core.py:1975-1992)
             if (cfg.export_forces) o += "    float lfx" + s + " = 0.f, lfy" + s + " = 0.f, ltq" + s + " = 0.f;\n";
+            // its parameter values, read from LDS once per group (registers for the substeps)
+            o += runtime_desc(e, "    ");
         }
         const std::string pro = it((long)cfg.max_substeps * 4);
         o += "    " + stamp(w, pro);
@@ -805,7 +902,9 @@ struct Gen {
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[" + it(n_out()) + "];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
-             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n};\n\n";
+             "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n"
+             "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
+             "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    if (s0 == 2 && s1 == 1) {\n"
              "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
@@ -813,12 +912,23 @@ struct Gen {
              "    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);\n}\n\n";
         o += "constexpr WorldK WK{" + fl(cfg.contact_margin) + ", " + fl(cfg.collision_force) + ", " +
              fl(cfg.joint_force) + ", " + fl(cfg.torque_constraint_force) + "};\n";
-        o += "constexpr float GX = " + fl(cfg.gravity_x) + ", GY = " + fl(cfg.gravity_y) + ";\n";
+        // world gravity and semidims: whether they apply is structure, their values are arguments
+        const std::string pw = it(prm_world);
+        // (the values are copied from the kernel arguments into LDS in the prologue and read from
+        // there where used: held in SGPRs for the whole launch they raised balance's SGPR
+        // spills 193 -> 289 and the static VALU count by 11 %)
+        o += "__shared__ float PRM[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n";
+        if ((prm_mask >> 11) & 1u) {
+            o += "#define GX PRM[" + pw + "]\n#define GY PRM[" + pw + " + 1]\n";
+            o += "#define XS PRM[" + pw + " + 2]\n#define YS PRM[" + pw + " + 3]\n";
+        } else {
+            o += "constexpr float GX = " + fl(cfg.gravity_x) + ", GY = " + fl(cfg.gravity_y) + ";\n";
+            o += "constexpr float XS = " + fl(cfg.x_semidim) + ", YS = " + fl(cfg.y_semidim) + ";\n";
+        }
         o += "constexpr bool HAS_G = " + bl(cfg.has_world_gravity) + ";\n";
-        o += "constexpr float XS = " + fl(cfg.x_semidim) + ", YS = " + fl(cfg.y_semidim) + ";\n";
         o += "constexpr bool HAS_XS = " + bl(cfg.has_x_semidim) + ", HAS_YS = " + bl(cfg.has_y_semidim) + ";\n";
         for (int e = 0; e < E; ++e)
-            if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + desc(e) + ";\n";
+            if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + "c" + desc(e) + ";\n";
         o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
              "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid);\n\n";
         for (int w = 0; w < nw; ++w) wave_body(o, w);
@@ -867,7 +977,8 @@ struct Gen {
              "    __shared__ GridCursor CUR;\n"
              "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0, 0, persistent ? ld64(&a.ctl[kGridEpoch]) : 0ull};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
-             "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n"
+             "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n" +
+             prm_copy() +
              "    __syncthreads();\n" +
              block_stamp(0, "__builtin_amdgcn_s_memrealtime()") + block_stamp(1, "__builtin_amdgcn_s_getreg(63492)") +
              block_stamp(2, "__builtin_amdgcn_s_getreg(30740)") +
@@ -928,6 +1039,7 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
     for (const auto& t : tries) {
         if (t.split && !allow_split) continue;
         std::unique_ptr<Gen> g(new Gen(cfg, ed, pd, jd));
+        if (const char* pm = getenv("VMAS_JIT_PRM_MASK")) g->prm_mask = (unsigned)strtoul(pm, nullptr, 0) & 0xFFFu;
         if ((size_t)cfg.max_substeps * g->W > 1024) {
             *why = "too many substeps x pairs";
             return nullptr;
@@ -990,9 +1102,17 @@ bool relaxed_math(const VmasWorldConfig& cfg) {
     return !(m && std::string(m) == "exact") && cfg.n_joints == 0;
 }
 
-// hipRTC compile with an in-process cache (identical worlds share one code object)
+// hipRTC compile with an in-process cache (identical world structures share one code object;
+// parameter values are kernel arguments, so a world whose masses / drags / limits change keeps
+// its entry).  Bounded: the kCodeCacheMax most recently used code objects (VMAS_JIT_CACHE).
 std::mutex g_cache_mu;
-std::unordered_map<std::string, std::vector<char>> g_code_cache;
+std::unordered_map<std::string, std::pair<std::vector<char>, uint64_t>> g_code_cache;  // src -> (code, last use)
+uint64_t g_cache_tick = 0;
+constexpr size_t kCodeCacheMax = 32;
+size_t code_cache_max() {
+    const char* c = getenv("VMAS_JIT_CACHE");
+    return c ? (size_t)std::max(1, atoi(c)) : kCodeCacheMax;
+}
 
 std::string module_dir() {
     Dl_info info{};
@@ -1004,12 +1124,15 @@ std::string module_dir() {
     return ".";
 }
 
+int64_t g_jit_compiles = 0;  // hipRTC compiles so far (vmas_jit_stats)
+
 int32_t compile(const std::string& src, std::vector<char>* code) {
     {
         std::lock_guard<std::mutex> lk(g_cache_mu);
         auto f = g_code_cache.find(src);
         if (f != g_code_cache.end()) {
-            *code = f->second;
+            *code = f->second.first;
+            f->second.second = ++g_cache_tick;
             return VMAS_OK;
         }
     }
@@ -1052,7 +1175,14 @@ int32_t compile(const std::string& src, std::vector<char>* code) {
     hiprtcGetCode(prog, code->data());
     hiprtcDestroyProgram(&prog);
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    g_code_cache[src] = *code;
+    ++g_jit_compiles;
+    while (!g_code_cache.empty() && g_code_cache.size() >= code_cache_max()) {  // evict the least recently used
+        auto lru = g_code_cache.begin();
+        for (auto it2 = g_code_cache.begin(); it2 != g_code_cache.end(); ++it2)
+            if (it2->second.second < lru->second.second) lru = it2;
+        g_code_cache.erase(lru);
+    }
+    g_code_cache[src] = {*code, ++g_cache_tick};
     return VMAS_OK;
 }
 
@@ -1064,7 +1194,8 @@ struct VmasJitWorld {
     std::vector<VmasPairDesc> pd;
     std::vector<VmasJointDesc> jd;
     std::string src;
-    std::vector<std::pair<int, int>> ptr_src, str_src;
+    std::vector<std::pair<int, int>> ptr_src, str_src, prm_src;
+    unsigned prm_mask = kPrmMaskDefault;  // value fields passed as arguments (the others are folded in)
     size_t arg_bytes = 0;
     int W = 1, nblk = 0, nw = kNW;
     hipModule_t mod = nullptr;
@@ -1097,6 +1228,13 @@ struct VmasJitWorld {
 extern "C" {
 
 const char* vmas_jit_last_error(void) { return g_jit_err.c_str(); }
+
+int32_t vmas_jit_stats(int64_t* compiles, int64_t* cached) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    if (compiles) *compiles = g_jit_compiles;
+    if (cached) *cached = (int64_t)g_code_cache.size();
+    return VMAS_OK;
+}
 
 int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
     if (!W) return VMAS_OK;
@@ -1174,6 +1312,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
     W->src = g.src;
     W->ptr_src = g.ptr_src;
     W->str_src = g.str_src;
+    W->prm_src = g.prm_src;
+    W->prm_mask = g.prm_mask;
     W->arg_bytes = g.arg_bytes();
     W->W = g.W;
     W->nw = g.nw;
@@ -1359,6 +1499,11 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     const int max_it = batch_bp ? io->substeps + 2 : 1;
     const int max_pass = std::min(W->max_passes > 0 ? std::min(W->max_passes, max_it) : max_it, vmas::kGridMaxPasses);
     put_i32(persistent ? max_pass : max_it);
+    for (const auto& q : W->prm_src) {
+        const float v = q.first >= 0 ? prm_value(W->ed[q.first], q.second) : prm_world_value(W->cfg, q.second);
+        memcpy(p, &v, 4);
+        p += 4;
+    }
     size_t size = ((size_t)(p - buf.data()) + 7) & ~(size_t)7;
     if (size > buf.size()) return jfail(VMAS_E_INVALID, "kernel argument block overflow");
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
@@ -1441,6 +1586,48 @@ int32_t vmas_jit_world_passes(VmasJitWorld* W, int32_t* passes) {
     if (err)
         return jfail(err & vmas::kGridErrNoConverge ? VMAS_E_NOCONVERGE : VMAS_E_HIP,
                      "device-side broadphase fixed point failed (error bits 0x%x)", err);
+    return VMAS_OK;
+}
+
+int32_t vmas_jit_world_set_params(VmasJitWorld* W, const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
+                                  const VmasPairDesc* pairs, const VmasJointDesc* joints) {
+    if (!W || !cfg || !entities || (cfg->n_pairs && !pairs) || (cfg->n_joints && !joints))
+        return jfail(VMAS_E_INVALID, "null argument");
+    const VmasWorldConfig& c = W->cfg;
+    if (cfg->n_entities != c.n_entities || cfg->n_agents != c.n_agents || cfg->n_pairs != c.n_pairs ||
+        cfg->n_joints != c.n_joints || cfg->batch != c.batch || cfg->device != c.device ||
+        cfg->n_out_lin != c.n_out_lin || cfg->n_out_rot != c.n_out_rot || cfg->n_out_force != c.n_out_force ||
+        cfg->n_out_torque != c.n_out_torque || cfg->contact_margin != c.contact_margin ||
+        cfg->collision_force != c.collision_force || cfg->joint_force != c.joint_force ||
+        cfg->torque_constraint_force != c.torque_constraint_force || cfg->has_world_gravity != c.has_world_gravity ||
+        cfg->has_x_semidim != c.has_x_semidim || cfg->has_y_semidim != c.has_y_semidim ||
+        cfg->max_substeps != c.max_substeps || cfg->export_forces != c.export_forces)
+        return jfail(VMAS_E_INVALID, "set_params: the world configuration differs in structure");
+    for (int e = 0; e < c.n_entities; ++e) {
+        const VmasEntityDesc &a = W->ed[e], &b = entities[e];
+        if (a.shape != b.shape || a.flags != b.flags || a.agent_index != b.agent_index || a.out_lin != b.out_lin ||
+            a.out_rot != b.out_rot || a.out_force != b.out_force || a.out_torque != b.out_torque ||
+            a.radius != b.radius || a.half_length != b.half_length || a.half_width != b.half_width)
+            return jfail(VMAS_E_INVALID, "set_params: entity %d differs in structure", e);
+        for (int k = 0; k <= kPrmTRange; ++k)  // (fields folded into the code: VMAS_JIT_PRM_MASK)
+            if (!((W->prm_mask >> k) & 1u) && prm_value(a, k) != prm_value(b, k))
+                return jfail(VMAS_E_INVALID, "set_params: entity %d field %d is folded into the code", e, k);
+    }
+    if (!((W->prm_mask >> 11) & 1u))
+        for (int k = 0; k < 4; ++k)
+            if (prm_world_value(c, k) != prm_world_value(*cfg, k))
+                return jfail(VMAS_E_INVALID, "set_params: the world values are folded into the code");
+    // pairs (classes, order, broadphase radii, d_min) and joints (anchors, dist, fixed rotation)
+    // are folded into the code
+    if (c.n_pairs && memcmp(pairs, W->pd.data(), sizeof(VmasPairDesc) * (size_t)c.n_pairs) != 0)
+        return jfail(VMAS_E_INVALID, "set_params: the pair table differs");
+    if (c.n_joints && memcmp(joints, W->jd.data(), sizeof(VmasJointDesc) * (size_t)c.n_joints) != 0)
+        return jfail(VMAS_E_INVALID, "set_params: the joint table differs");
+    W->ed.assign(entities, entities + c.n_entities);
+    W->cfg.gravity_x = cfg->gravity_x;
+    W->cfg.gravity_y = cfg->gravity_y;
+    W->cfg.x_semidim = cfg->x_semidim;
+    W->cfg.y_semidim = cfg->y_semidim;
     return VMAS_OK;
 }
 

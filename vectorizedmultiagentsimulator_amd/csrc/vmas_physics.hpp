@@ -458,7 +458,17 @@ VHD Real friction1(Real v, Real coeff, Real mass, Real sdt) {
     const Real speed = fabsf(v);
     const Real ffc = coeff * mass;
     const Real den = (speed == 0.f) ? 1e-8f : speed;
+#ifdef VMAS_PHYS_RELAXED
+    // v / |v| is exactly +-1 in IEEE arithmetic for every finite v != 0, denormals included.
+    // The relaxed build's division is x * v_rcp_f32(y), and v_rcp_f32 of a denormal is inf: an
+    // angular velocity that friction has brought to a denormal residue would make the torque
+    // inf (measured: features world, 16 384 envs).  So the sign is taken directly (NaN and 0
+    // keep the division, whose result is the same there).
+    const Real dir = (speed == 0.f || speed != speed) ? v / den : copysignf(1.f, v);
+    Real f = -dir * tmin(ffc, (fabsf(v) / sdt) * mass);
+#else
     Real f = -(v / den) * tmin(ffc, (fabsf(v) / sdt) * mass);
+#endif
     if (speed == 0.f) f = 0.f;
     return f;
 }

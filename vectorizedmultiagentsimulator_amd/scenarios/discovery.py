@@ -476,9 +476,13 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
                                                       ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
                 "vmas_spawn_targets")
     h = mx.tolist()  # the step's one host wait
+    # the generator is left where the tries it consumed put it, also when an env found no free
+    # position (the reference warns and keeps trying forever, utils.py:285-317; here the kernels
+    # stop after VMAS_SPAWN_MAX_TRIES tries and the call raises, with the targets of the resolved
+    # envs moved and the generator consistent with the tries drawn)
+    gen.set_offset(io.offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc.value)
     if h[T]:
         raise RuntimeError(
             f"find_random_pos_for_entity: {h[T]} env(s) found no free position within {N.VMAS_SPAWN_MAX_TRIES} "
             "tries; make sure the bounds or the min_dist_between_entities are not too tight to fit all entities")
-    gen.set_offset(io.offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc.value)
     return mx

@@ -371,12 +371,19 @@ class PhysicsEngine:
             self.lib.vmas_world_destroy(self._handle)
         self._handle = handle
         # GPU worlds: the world-specialised kernel (csrc/vmas_jit.hip) when it applies, with the
-        # generic k_step as the fallback (both native; VMAS_JIT=0 forces the generic kernel)
-        if self._jit is not None:
+        # generic k_step as the fallback (both native; VMAS_JIT=0 forces the generic kernel).
+        # Only parameter VALUES changed (a mass re-rolled at reset, het_mass.py:48-54; a drag, a
+        # limit): the world kernel takes them as arguments -- no new code object, no compile.
+        keep_jit = (self._jit is not None and max_substeps == self._max_substeps and
+                    self.lib.vmas_jit_world_set_params(self._jit, ctypes.byref(cfg), ed, pd, jd) == 0)
+        if self._jit is not None and not keep_jit:
             self.lib.vmas_jit_world_destroy(self._jit)
             self._jit = None
-        self.jit_error = None
-        if self._dev_index >= 0 and os.environ.get("VMAS_JIT", "1") != "0":
+        if not keep_jit:
+            self.jit_error = None
+        if keep_jit:
+            pass
+        elif self._dev_index >= 0 and os.environ.get("VMAS_JIT", "1") != "0":
             jh = ctypes.c_void_p()
             rc = self.lib.vmas_jit_world_create(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(jh))
             if rc == 0:
@@ -589,6 +596,12 @@ class PhysicsEngine:
         dev = self._dev
         B = w.batch_dim
         _GRAD_OK = grad_ok
+        try:
+            return self._launch_body(w, dev, B)
+        finally:
+            _GRAD_OK = False
+
+    def _launch_body(self, w, dev, B) -> torch.Tensor:
         # pointer tables: only tensors that are not the objects seen last step are re-read
         seen = self._ent_seen
         for i, e in enumerate(self.entities):
@@ -636,9 +649,10 @@ class PhysicsEngine:
         fd = None
         if self._cfg.export_forces:
             # World.forces_dict / torques_dict rows ([E][B][2] | [E][B]); entities that neither move
-            # nor rotate are not written by the kernels (zeros, or their friction: _static_forces)
+            # nor rotate are not written by the kernels (their rows are set when the dicts are
+            # first read: zeros, or their friction -- _static_forces)
             E = len(self.entities)
-            fd = torch.zeros(E * B * 3, device=dev, dtype=torch.float32)
+            fd = torch.empty(E * B * 3, device=dev, dtype=torch.float32)
             io.out_fdict, io.out_tdict = fd.data_ptr(), fd.data_ptr() + 4 * E * B * 2
         else:
             io.out_fdict = io.out_tdict = 0
@@ -650,16 +664,18 @@ class PhysicsEngine:
             N.check(self.lib.vmas_world_step(self._handle, ctypes.byref(io), self._stream(dev),
                                              ctypes.byref(iters)), "vmas_world_step")
         self._last_iterations = iters.value
-        if fd is not None:
-            self._publish_force_dicts(fd, B)
+        # the dicts are built from the buffer when first read (World.forces_dict); a step that did
+        # not export leaves none (stale dicts of an earlier step must not be read as this one's)
+        w._force_buf = (fd, B, self) if fd is not None else None
+        w._forces_dict = w._torques_dict = None
         self.steps += 1
-        _GRAD_OK = False
         self._last_keep = keep
         return out
 
-    def _publish_force_dicts(self, fd: torch.Tensor, B: int) -> None:
-        """World.forces_dict / torques_dict (ref core.py:1975-1992): per entity, views of the step's
-        last-substep force [B,2] and torque [B,1] totals."""
+    def force_dicts(self, fd: torch.Tensor, B: int):
+        """World.forces_dict / torques_dict (ref core.py:1975-1992) of the step that wrote ``fd``:
+        per entity, views of its last-substep force [B,2] and torque [B,1] totals; the rows of
+        entities that neither move nor rotate are set here (the kernels do not write them)."""
         w = self.world
         E = len(self.entities)
         f2 = fd[: E * B * 2].view(E, B, 2)
@@ -668,8 +684,10 @@ class PhysicsEngine:
         for i, e in enumerate(self.entities):
             forces[e], torques[e] = f2[i], f1[i]
             if not (e.movable or e.rotatable):
+                f2[i].zero_()
+                f1[i].zero_()
                 self._static_forces(e, f2[i], f1[i], w)
-        w._forces_dict, w._torques_dict = forces, torques
+        return forces, torques
 
     @staticmethod
     def _static_forces(e, f, t, w) -> None:
@@ -943,6 +961,9 @@ class _StepFn(torch.autograd.Function):
         ctx.eng = eng
         ctx.tables = (eng._eio.copy(), eng._aio.copy(), eng._jio.copy(), eng._io.substeps, eng._io.sub_dt,
                       eng._io.broadphase)
+        # the world tables of THIS forward (a parameter or entity change before the backward
+        # rebuilds the engine's own; the VJP must differentiate the step that ran)
+        ctx.world_tables = (eng._cfg, eng._tables, eng._out_off, list(eng.entities), list(eng.agents))
         ctx.keep = ([list(k) if k is not None else None for k in eng._ent_keep],
                     [tuple(k) if k is not None else None for k in eng._agent_keep], eng._last_keep)
         # the backward re-runs the step on the forward's input values: inputs that require grad
@@ -959,19 +980,20 @@ class _StepFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         inputs = [s if s is not None else c for s, c in zip(saved, ctx.consts)]
         eio, aio, jio, substeps, sub_dt, bp = ctx.tables
+        cfg, (ed, pd, jd), out_off, entities, agents = ctx.world_tables
         eio, aio = eio.copy(), aio.copy()
         dev = eng._dev
         B = eng.world.batch_dim
         keep = []
-        for i in range(len(eng.entities)):  # the rows point at the forward's input values
+        for i in range(len(entities)):  # the rows point at the forward's input values
             pos, vel, rot, ang = (eng._prep(t.detach(), dev) for t in inputs[4 * i: 4 * i + 4])
             keep += [pos, vel, rot, ang]
             eio["pos"][i], eio["vel"][i], eio["rot"][i], eio["ang"][i] = pos.data_ptr(), vel.data_ptr(), rot.data_ptr(), ang.data_ptr()
             eio["pos_s0"][i], eio["pos_s1"][i] = pos.stride()
             eio["vel_s0"][i], eio["vel_s1"][i] = vel.stride()
             eio["rot_s0"][i], eio["ang_s0"][i] = rot.stride(0), ang.stride(0)
-        off = 4 * len(eng.entities)
-        for i in range(len(eng.agents)):
+        off = 4 * len(entities)
+        for i in range(len(agents)):
             f, t = (eng._prep(x.detach(), dev) for x in inputs[off + 2 * i: off + 2 * i + 2])
             keep += [f, t]
             aio["force"][i], aio["torque"][i] = f.data_ptr(), t.data_ptr()
@@ -983,10 +1005,10 @@ class _StepFn(torch.autograd.Function):
         g = gout.to(device=dev, dtype=torch.float32).contiguous()
         base = g.data_ptr()
         go = N.VmasStepIO()
-        o_pos, o_vel, o_rot, o_ang, o_force, o_torque = eng._out_off
+        o_pos, o_vel, o_rot, o_ang, o_force, o_torque = out_off
         go.out_pos, go.out_vel, go.out_rot = base + 4 * o_pos, base + 4 * o_vel, base + 4 * o_rot
         go.out_ang_vel, go.out_force, go.out_torque = base + 4 * o_ang, base + 4 * o_force, base + 4 * o_torque
-        E, A = len(eng.entities), len(eng.agents)
+        E, A = len(entities), len(agents)
         grads = []
         ptrs = {k: (ctypes.c_void_p * max(E, 1))() for k in ("pos", "vel", "rot", "ang")}
         ptrs.update({k: (ctypes.c_void_p * max(A, 1))() for k in ("force", "torque")})
@@ -1001,8 +1023,7 @@ class _StepFn(torch.autograd.Function):
                 grads.append(t)
                 ptrs[key][i] = t.data_ptr()
         gio = N.VmasGradIO(*(ctypes.cast(ptrs[k], ctypes.c_void_p) for k in ("pos", "vel", "rot", "ang", "force", "torque")))
-        ed, pd, jd = eng._tables
-        N.check_aux(eng.lib.vmas_world_step_vjp(ctypes.byref(eng._cfg), ed, pd, jd, ctypes.byref(io), ctypes.byref(go),
+        N.check_aux(eng.lib.vmas_world_step_vjp(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(io), ctypes.byref(go),
                                                 ctypes.byref(gio), eng._stream(dev) if eng._dev_index >= 0 else None),
                     "vmas_world_step_vjp")
         out = []

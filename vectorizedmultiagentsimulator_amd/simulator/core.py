@@ -12,6 +12,7 @@ arithmetic on host threads for ``device="cpu"``) instead of hundreds of PyTorch 
 from __future__ import annotations
 
 import math
+import os
 import typing
 from abc import ABC, abstractmethod
 from typing import Callable, List, Sequence, Tuple, Union
@@ -919,11 +920,16 @@ class World(TorchVectorizedObject):
         ]
         self.entity_index_map = {}
         self.broadphase = "batch"
-        # World.forces_dict / torques_dict (core.py:1975-1992) are exported by the step only when
-        # asked for: each dynamic entity's last-substep totals (12 B per entity and env)
-        self.export_forces = False
+        # World.forces_dict / torques_dict (core.py:1975-1992): the step exports each dynamic
+        # entity's last-substep totals (12 B per entity and env).  On by default for CPU worlds
+        # (the reference's behaviour); opt-in on GPU worlds, where the exporting kernel keeps 3
+        # more live registers per entity (balance C2: k_world 34.4 -> 38.3 us, profiles/r03/
+        # run4_bisect).  VMAS_EXPORT_FORCES=0/1 overrides the default.
+        env_default = os.environ.get("VMAS_EXPORT_FORCES")
+        self.export_forces = (env_default != "0") if env_default is not None else torch.device(device).type == "cpu"
         self._forces_dict = None
         self._torques_dict = None
+        self._force_buf = None
         self._engine = None
 
     def add_agent(self, agent: Agent):
@@ -1046,19 +1052,28 @@ class World(TorchVectorizedObject):
     # ---- the step (core.py:1970-2014) -------------------------------------------------------------
     @property
     def forces_dict(self):
-        """{entity: [B, 2]} force totals of the last step's last substep (core.py:1975-2198)."""
+        """{entity: [B, 2]} force totals of the last step's last substep (core.py:1975-2198), as the
+        reference leaves them after every step.  The step writes them into one buffer (the
+        kernels' last-substep totals, ``export_forces``, on by default); the dict of views is
+        built on first read."""
         if self._forces_dict is None:
-            raise AttributeError("forces_dict is exported by the step only with world.export_forces = True "
-                                 "(set it before the step)")
+            self._build_force_dicts()
         return self._forces_dict
 
     @property
     def torques_dict(self):
         """{entity: [B, 1]} torque totals of the last step's last substep (core.py:1984-2198)."""
         if self._torques_dict is None:
-            raise AttributeError("torques_dict is exported by the step only with world.export_forces = True "
-                                 "(set it before the step)")
+            self._build_force_dicts()
         return self._torques_dict
+
+    def _build_force_dicts(self):
+        buf = getattr(self, "_force_buf", None)
+        if buf is None:
+            raise AttributeError("forces_dict: no step has exported force totals yet (world.export_forces "
+                                 "was False at the last step, or no step ran)")
+        fd, B, engine = buf
+        self._forces_dict, self._torques_dict = engine.force_dicts(fd, B)
 
     def step(self):
         self.entity_index_map = {e: i for i, e in enumerate(self.entities)}

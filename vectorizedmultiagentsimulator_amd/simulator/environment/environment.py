@@ -550,10 +550,12 @@ class Environment(TorchVectorizedObject):
             if type(ur) not in (float, int):
                 return None
             sig.append((a, act, ur, a.silent, a.action_size, a.batch_dim))
-        return (self.world.dim_c, sig)
+        # the device the plan draws on (env.to(...) moves the world and its agents)
+        return (self.world.dim_c, sig, self.world.device, self.world.batch_dim)
 
     def _uniform_same(self, sig) -> bool:
-        if sig is None or sig[0] != self.world.dim_c or len(sig[1]) != len(self.agents):
+        if (sig is None or sig[0] != self.world.dim_c or len(sig[1]) != len(self.agents)
+                or sig[2] != self.world.device or sig[3] != self.world.batch_dim):
             return False
         for a, (ag, act, ur, sil, asz, bd) in zip(self.agents, sig[1]):
             if (a is not ag or a.action is not act or act.u_range is not ur or a.silent is not sil
@@ -922,3 +924,4 @@ class Environment(TorchVectorizedObject):
         device = torch.device(device)
         self.scenario.to(device)
         super().to(device)
+        self._uniform_cache = None  # (the fused random-action plan holds device buffers)
