@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define VMAS_ABI_VERSION 1
+#define VMAS_ABI_VERSION 2
 
 /* error codes */
 #define VMAS_OK 0
@@ -314,6 +314,15 @@ typedef struct VmasUniformColumn {
     int64_t stride;      /* elements between consecutive draws */
     float from, to;      /* f32(low), f32(high) as torch casts them */
     uint64_t offset;     /* set by the library */
+    /* Optional second output (u_out != NULL): the drawn value x as the step's action kernel
+     * applies it (vmas_apply_actions: x clamped to +-u_range when u_clamp, times u_mult; the same
+     * fp32 operations), at u_out[i * u_stride] -- the random actions of a graph-mode step drawn
+     * and applied in one launch (environment.py:615-709 on values that pass its checks by
+     * construction: uniform draws in [-u_range, u_range]). */
+    float* u_out;
+    int64_t u_stride;
+    float u_range, u_mult;
+    int32_t u_clamp, pad;
 } VmasUniformColumn;
 
 int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformColumn* cols,

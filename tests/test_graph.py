@@ -334,3 +334,38 @@ def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
     assert env.graph_status == "eager", env.graph_reason
     expect = "Python-side state" if kind == "python_counter" else "host RNG"
     assert expect in env.graph_reason, env.graph_reason
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps", [("balance", dict(n_agents=4), 10), ("flocking", dict(n_agents=4), None)],
+                         ids=["balance", "flocking"])
+def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substeps):
+    """env.step(env.get_random_actions()) in graph mode: the draw kernel also writes the applied
+    actions into the graph's action buffer, and the step launches no action kernel.  Bit-identical
+    to the eager step on the same draws; an in-place edit of the drawn tensors, or other tensors,
+    take the normal action path."""
+    eager, graph = _twin_envs(gpu_device, name, **kw)
+    for env in (eager, graph):
+        if substeps:
+            env.world._substeps = substeps
+            env.world._sub_dt = env.world._dt / substeps
+    for t in range(12):
+        s = _rng_save()
+        a_e = eager.get_random_actions()
+        _rng_load(s)
+        a_g = graph.get_random_actions()
+        _assert_same(a_e, a_g, f"draws step {t}")
+        if t == 8:  # an in-place edit of a drawn tensor: the step applies the edited values
+            for a in (a_e, a_g):
+                a[0][:5] = 0.25
+        if t == 9:  # other tensors than the draw's
+            a_g = [a.clone() for a in a_g]
+        s = _rng_save()
+        out_e = eager.step(a_e)
+        _rng_load(s)
+        out_g = graph.step(a_g)
+        _assert_same(out_e, out_g, f"{name} outputs step {t}")
+        _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
+        _assert_same([a.action.u for a in eager.agents], [a.action.u for a in graph.agents], f"u step {t}")
+    assert graph.graph_status == "graph", graph.graph_reason
+    assert graph.preapplied_steps >= 5

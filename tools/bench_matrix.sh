@@ -20,7 +20,7 @@ run() {  # run <name> <bench args...>
 run c2_balance_sub10
 run c2_balance_sub1 --substeps 1
 run c2_balance_sub10_envbp --broadphase env
-run c3_transport --scenario transport --substeps 0
-run c4_discovery --scenario discovery --envs 16384 --n-agents 8 --substeps 0 --kw '{"use_agent_lidar": true}'
-run c5_flocking --scenario flocking --n-agents 8 --substeps 0
+run c3_transport --scenario transport
+run c4_discovery --scenario discovery
+run c5_flocking --scenario flocking
 echo done

@@ -16,7 +16,10 @@ from vectorizedmultiagentsimulator_amd import make_env  # noqa: E402
 scenario = sys.argv[1] if len(sys.argv) > 1 else "balance"
 n_envs = int(sys.argv[2]) if len(sys.argv) > 2 else 32768
 n_agents = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, n_agents=n_agents, graph_step=True)
+import os  # noqa: E402
+
+graph = os.environ.get("STEP_GRAPH", "1") != "0"  # STEP_GRAPH=0: the eager step (the graph's body)
+env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, n_agents=n_agents, graph_step=graph)
 if scenario == "balance":
     env.world._substeps = 10
     env.world._sub_dt = env.world._dt / 10

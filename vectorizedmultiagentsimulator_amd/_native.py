@@ -18,7 +18,7 @@ LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
-VMAS_ABI_VERSION = 1
+VMAS_ABI_VERSION = 2
 VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
 (
     VMAS_PAIR_JOINT,
@@ -461,8 +461,10 @@ ACTION_APPLY_REF_DTYPE = np.dtype(
         ("pad", "<i4"),
     ]
 )
-UNIFORM_COLUMN_DTYPE = np.dtype([("out", "<u8"), ("stride", "<i8"), ("from_", "<f4"), ("to", "<f4"), ("offset", "<u8")])
-assert UNIFORM_COLUMN_DTYPE.itemsize == 32
+UNIFORM_COLUMN_DTYPE = np.dtype([("out", "<u8"), ("stride", "<i8"), ("from_", "<f4"), ("to", "<f4"), ("offset", "<u8"),
+                                 ("u_out", "<u8"), ("u_stride", "<i8"), ("u_range", "<f4"), ("u_mult", "<f4"),
+                                 ("u_clamp", "<i4"), ("pad", "<i4")])
+assert UNIFORM_COLUMN_DTYPE.itemsize == 64
 assert ACTION_REF_DTYPE.itemsize == 40
 assert ACTION_APPLY_REF_DTYPE.itemsize == 56
 assert ENTITY_IO_DTYPE.itemsize == 72

@@ -214,7 +214,12 @@ __global__ void __launch_bounds__(kUniformThreads) k_uniform_columns(UniformArgs
             if (li < a.numel) {
                 const float r = unit_float(vv[k], fused_unit);
                 const float val = fused_affine ? __builtin_fmaf(r, range, from) : r * range + from;
-                col.out[li * col.stride] = val == to ? from : val;  // (0, 1] -> [from, to)
+                const float x = val == to ? from : val;  // (0, 1] -> [from, to)
+                col.out[li * col.stride] = x;
+                if (col.u_out) {  // apply_one's operations on the same value
+                    const float v = col.u_clamp ? fminf(fmaxf(x, -col.u_range), col.u_range) : x;
+                    col.u_out[li * col.u_stride] = v * col.u_mult;
+                }
             }
         }
     }

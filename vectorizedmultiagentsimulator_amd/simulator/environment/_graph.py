@@ -373,6 +373,9 @@ class StepGraph:
         the eager step orders it): tensors re-bound by the caller are copied into the captured
         ones, carried state is copied forward.  (A tracked tensor may alias the action buffer --
         a holonomic agent's force is a view of u -- so the fresh actions must land last.)"""
+        # (copied: this call wrote tracked tensors, which may alias the persistent action buffer:
+        # random actions applied into it by their draw are then stale -- Environment._take_preapplied)
+        self.copied = False
         if self.graph is None:
             return
         self.env.world.engine.check_device_errors()
@@ -388,7 +391,9 @@ class StepGraph:
                 with torch.no_grad():
                     t.copy_(cur)
                 d[k] = t
+                self.copied = True
         if not self._first_replay and not self._carry_current():
+            self.copied = True
             self._post = None
             with torch.no_grad():
                 if self._carry_dst:

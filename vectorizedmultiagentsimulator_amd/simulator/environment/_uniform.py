@@ -64,7 +64,7 @@ def mode(device: torch.device, B: int) -> Optional[int]:
             out = torch.empty(B, len(_PROBE_BOUNDS), device=device, dtype=torch.float32)
             cols = np.zeros(len(_PROBE_BOUNDS), dtype=N.UNIFORM_COLUMN_DTYPE)
             for i, (lo, hi) in enumerate(_PROBE_BOUNDS):
-                cols[i] = (out.data_ptr() + 4 * i, len(_PROBE_BOUNDS), lo, hi, 0)
+                cols[i] = (out.data_ptr() + 4 * i, len(_PROBE_BOUNDS), lo, hi, 0, 0, 0, 0, 0, 0, 0)
             launch(idx, B, cols, m, gen)
             if all(torch.equal(out[:, i], r) for i, r in enumerate(ref)) and torch.equal(gen.get_state(), after):
                 found = m

@@ -132,6 +132,9 @@ class Environment(TorchVectorizedObject):
         self._spec_keep = None  # action tensors a speculative action launch reads
         self._draw_plans = {}  # agent -> cached column plan of its random actions
         self._uniform_cache = None  # see _fused_random_actions
+        self._preapply = None  # see _preapply_columns
+        self._drawn = None  # the last draw whose applied values are in the persistent buffer
+        self.preapplied_steps = 0  # graph steps whose actions were applied by their draw
         self._raw_outputs = False  # set while a step is captured (outputs are cloned after replay)
         self.terminated_truncated = terminated_truncated
         observations = self._reset(seed=seed)
@@ -277,6 +280,11 @@ class Environment(TorchVectorizedObject):
                         # rolls the step back (StepGraph.replay_speculative) and the eager check
                         # below raises the reference's AssertionError
                         g.backup(self._u_persist[1])
+                        if self._take_preapplied(actions):  # drawn + applied by get_random_actions
+                            out = g.replay_speculative(lambda: True)
+                            if out is not None:
+                                return out
+                            raise RuntimeError("a step of pre-applied random actions was rolled back")
                         seq = self._apply_continuous_actions(actions, persistent=True, speculative=True)
                         if seq:
                             out = g.replay_speculative(lambda: self._speculative_flags_ok(seq))
@@ -540,6 +548,78 @@ class Environment(TorchVectorizedObject):
         self._uniform_cache = (c[0], c[1], self._uniform_sig())
         return self._uniform_draw(c[1])
 
+    # ---- random actions drawn and applied in one launch (graph mode) -----------------------------
+    def _preapply_columns(self, st):
+        """When the next step will replay a captured graph with the speculative action path, the
+        draw kernel also writes every column as the action kernel would apply it (clamp to
+        u_range, times u_multiplier) into the persistent action buffer the graph reads.  A step
+        given exactly these tensors, unmodified, then needs no action launch: uniform draws from
+        [-u_range, u_range] pass the NaN / range checks by construction (environment.py:621-655).
+        Sets (or clears) the columns' second outputs; returns whether they are set."""
+        cols = st[1]
+        g = self._graph
+        ok = (g is not None and g.graph is not None and self._can_speculate())
+        if ok:
+            c = self._apply_cache
+            refs, sizes = c[1][0], c[1][4]
+            widths = st[2]
+            ok = list(widths) == list(sizes)
+        if ok:
+            key = (id(c), self._u_persist[1].data_ptr())
+            pre = self._preapply
+            if pre is None or pre[0] != key:
+                pre = None
+                vals = []
+                for ag in self.agents:  # host copies of u_range / u_multiplier (once per apply plan)
+                    r = ag.action.u_range_tensor.detach().cpu().tolist()
+                    m = ag.action.u_multiplier_tensor.detach().cpu().tolist()
+                    vals.append((r, m))
+                base = self._u_persist[1].data_ptr()
+                u_out, u_rng, u_mul = [], [], []
+                k = 0
+                good = True
+                for i, ag in enumerate(self.agents):
+                    r, m = vals[i]
+                    for j in range(sizes[i]):
+                        lo, hi = float(cols[k]["from_"]), float(cols[k]["to"])
+                        good &= (lo == -np.float32(r[j]) and hi == np.float32(r[j]))
+                        u_out.append(base + 4 * (int(refs[i]["out_offset"]) + j))
+                        u_rng.append(r[j])
+                        u_mul.append(m[j])
+                        k += 1
+                if good:
+                    pre = (key, np.array(u_out, dtype=np.uint64), np.array(u_rng, dtype=np.float32),
+                           np.array(u_mul, dtype=np.float32), np.array(sizes, dtype=np.int64).repeat(sizes))
+                self._preapply = pre if pre is not None else (key, None)
+            ok = self._preapply[1] is not None
+        if ok:
+            _, u_out, u_rng, u_mul, strides = self._preapply
+            cols["u_out"], cols["u_stride"], cols["u_range"], cols["u_mult"] = u_out, strides, u_rng, u_mul
+            cols["u_clamp"] = int(bool(self.clamp_action))
+        elif cols["u_out"].any():
+            cols["u_out"] = 0
+        return ok
+
+    def _take_preapplied(self, actions) -> bool:
+        """The step's actions are the last draw's tensors, unmodified, and that draw also wrote
+        their applied values into the persistent action buffer: bind every agent's u to it (the
+        speculative path's state after its action launch) and return True."""
+        d = self._drawn
+        self._drawn = None
+        if (d is None or len(actions) != len(d[0]) or self._u_persist is None or d[3] is not self._u_persist[1]
+                or getattr(self._graph, "copied", True)):
+            return False
+        for a, t, ptr, ver in zip(actions, d[0], d[1], d[2]):
+            if a is not t or a.data_ptr() != ptr or a._version != ver:
+                return False
+        us = self._u_persist[2]
+        if us is None:
+            return False
+        for i, ag in enumerate(self.agents):
+            ag.action.u = us[i]
+        self.preapplied_steps += 1
+        return True
+
     def _uniform_sig(self):
         """What _column_plan's keys depend on, compared by identity (None when a u_range is a
         mutable sequence: then the plans are rebuilt every call)."""
@@ -580,7 +660,10 @@ class Environment(TorchVectorizedObject):
                     f_out[k] = base + 4 * j
                     k += 1
                 outs.append(out)
+        pre = self._preapply_columns(st)
         _uniform.launch(idx, B, cols, mode, gen, cols_addr)
+        self._drawn = (tuple(outs), tuple(o.data_ptr() for o in outs), tuple(o._version for o in outs),
+                       self._u_persist[1]) if pre else None
         return outs
 
     @local_seed(vmas_random_state)
@@ -701,6 +784,7 @@ class Environment(TorchVectorizedObject):
         (or False) and the caller checks the flags later with _finish_speculative_actions."""
         agents = self.agents
         n = len(agents)
+        self._drawn = None  # (the persistent buffer is rewritten: a draw's applied values are stale)
         if n == 0:
             return False
         for a in actions:

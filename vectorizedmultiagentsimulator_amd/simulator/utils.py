@@ -284,8 +284,8 @@ class ScenarioUtils:
                     cols = np.zeros(2 * (k1 - k0), dtype=N.UNIFORM_COLUMN_DTYPE)
                     for k in range(k0, k1):
                         j = 2 * (k - k0)
-                        cols[j] = (base + 4 * (2 * k) * batch_size, 1, x0, x1, 0)
-                        cols[j + 1] = (base + 4 * (2 * k + 1) * batch_size, 1, y0, y1, 0)
+                        cols[j] = (base + 4 * (2 * k) * batch_size, 1, x0, x1, 0, 0, 0, 0, 0, 0, 0)
+                        cols[j + 1] = (base + 4 * (2 * k + 1) * batch_size, 1, y0, y1, 0, 0, 0, 0, 0, 0, 0)
                     _uniform.launch(dev_index, batch_size, cols, m, gen)
             else:
                 for k in range(n):
