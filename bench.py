@@ -115,7 +115,7 @@ def program_bytes_per_env_step(env) -> int:
     4 B per ray) and the done flag (1 B)."""
     world = env.world
     out = 20 * len(world.entities) + 1
-    for a in world.agents:
+    for a in env.agents:  # (the policy agents: those the environment asks for observations)
         obs = env.scenario.observation(a)
         out += 4 * sum(int(o.shape[-1]) for o in (obs.values() if isinstance(obs, dict) else [obs])) + 4
     return out
@@ -129,7 +129,8 @@ def time_program(env, n: int):
     is not counted.  Returns (ms per step, timer description); eager events if the calls cannot
     be captured."""
     world = env.world
-    a0 = world.agents[0]
+    pol = getattr(world, "policy_agents", None) or world.agents
+    a0 = pol[0]  # (the programs launch at the first policy agent's calls)
 
     def calls():
         env.scenario.reward(a0)

@@ -345,6 +345,13 @@ int32_t vmas_assert_publish(VmasDeviceAssert* ch, int32_t slot, const uint8_t* c
                             void* stream);
 int32_t vmas_assert_wait(VmasDeviceAssert* ch, int32_t slot, uint32_t seq, int32_t* violated,
                          void* stream);
+/* The scripted-action range check itself (Agent.action_callback, core.py:977-980:
+ * ((u / u_multiplier).abs() <= u_range).all(), u [batch, n] fp32 with element strides s0 / s1,
+ * u_multiplier / u_range [n] fp32 device arrays) evaluated, reduced and published into `slot` by
+ * one kernel, as vmas_assert_publish publishes a precomputed condition. */
+int32_t vmas_assert_publish_range(VmasDeviceAssert* ch, int32_t slot, const float* u, int64_t s0,
+                                  int64_t s1, int32_t batch, int32_t n, const float* mult,
+                                  const float* range, void* stream);
 
 /* Distance queries; out has B floats, or B bytes of 0/1 (torch.bool) for VMAS_OVERLAP_PAIR. */
 int32_t vmas_distance(int32_t device, int32_t batch, int32_t kind, const VmasShapeRef* a,
@@ -454,7 +461,10 @@ typedef struct VmasFlockingIO {
                                                         the mean's sum order (vmas_scenarios.hip ordered_sum) */
     float min_collision_distance, collision_reward, desired_distance, dist_shaping_factor;
     float max_range, pad0;
-    int32_t collide_reward_on, pad1;       /* the scenario's `collision_reward != 0` */
+    int32_t collide_reward_on;             /* the scenario's `collision_reward != 0` */
+    int32_t fast_lidar;                    /* 1: one thread per (env, agent), direct ray-sphere
+                                              form (k_flocking_fast; LIDAR within the parity
+                                              tolerance); 0: bit-identical to k_cast_rays */
     VmasShapeRef agents[VMAS_FLOCK_MAX_AGENTS]; /* world.agents, in order (spheres) */
     int32_t scripted[VMAS_FLOCK_MAX_AGENTS];    /* action_script is not None */
     int32_t policy[VMAS_FLOCK_MAX_AGENTS];      /* world.policy_agents[p] = agents[policy[p]] */
@@ -473,6 +483,11 @@ typedef struct VmasFlockingIO {
     float* lidar[VMAS_FLOCK_MAX_AGENTS];         /* [B, n_rays] fresh (OBS): Lidar._last_measurement */
 } VmasFlockingIO;
 int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* stream);
+/* flocking's scripted target (flocking.py:81-87 action_script): u[b] = (cos(t[b] / period),
+ * sin(t[b] / period)) written into u [batch, 2] (contiguous), the division as torch computes a
+ * tensor / Python-scalar division (t * f32(1 / period)). */
+int32_t vmas_flocking_target_action(int32_t device, const float* t, int32_t batch, float period, float* u,
+                                    void* stream);
 
 /* transport (reference vmas/scenarios/transport.py:130-190): replaces Scenario.reward (for the
  * first agent: per package dist_to_goal, on_goal = is_overlapping(package, goal), the colour,

@@ -79,9 +79,11 @@ def summarize(config, env, reps, lidar=None):
 _RAY_CERT_DELTAS = (-1e-6, -3e-7, 3e-7, 1e-6)
 
 
-def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0):
+def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0, measured=False):
     """Every agent sensor: engine measure() vs the oracle's cast_rays on the same state/angles.
-    A (env, ray) outside atol/rtol passes only when certified as a boundary case (see above)."""
+    A (env, ray) outside atol/rtol passes only when certified as a boundary case (see above).
+    measured=True: check each sensor's last measurement (what the step's observation program
+    produced, e.g. a fused scenario program's LIDAR) instead of a fresh measure()."""
     w = env.world
     snap = O.snapshot(w)
     ow = O.OracleWorld(w, snap)
@@ -89,7 +91,7 @@ def lidar_parity(env, atol=2e-5, rtol=2e-5, max_bad_frac=0.0):
     for agent in w.agents:
         ai = w.entities.index(agent)
         for sensor in agent.sensors:
-            got = sensor.measure().detach().cpu()
+            got = (sensor._last_measurement if measured else sensor.measure()).detach().cpu()
             angles = sensor._angles.detach().cpu() + snap[ai]["rot"]
             exp = ow.cast_rays(ai, angles, sensor._max_range, sensor.entity_filter)
             diff = (got - exp).abs()

@@ -65,7 +65,8 @@ def _attrs(env, names):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps,attrs", FUSED, ids=[c[0] for c in FUSED])
-def test_fused_program_matches_torch_program_gpu(gpu_device, name, kw, substeps, attrs):
+def test_fused_program_matches_torch_program_gpu(gpu_device, monkeypatch, name, kw, substeps, attrs):
+    monkeypatch.setattr(_fused, "EXACT_LIDAR", True)  # (LIDAR bit-identical to World.cast_rays)
     envs = {}
     for mode in ("torch", "fused", "graph"):
         saved = _rng_save()
@@ -131,3 +132,49 @@ def test_reduce_order_probe_finds_torch_mean_order_gpu(gpu_device, n):
     """The fused kernels' mean over n contiguous values reproduces torch's .mean(-1) on the device
     bit for bit in one of the ordered_sum modes (else the scenario would keep its torch program)."""
     assert _fused.reduce_order(torch.device(gpu_device), n) is not None
+
+
+# (scenario, kwargs, observation columns that are LIDAR rays, per policy agent)
+FAST_LIDAR = [
+    ("flocking", dict(n_agents=5), lambda env, a: slice(6, None)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,lidar_cols", FAST_LIDAR, ids=[c[0] for c in FAST_LIDAR])
+def test_fast_lidar_program_gpu(gpu_device, name, kw, lidar_cols):
+    """The default fused programs (fast LIDAR): every output but the LIDAR rays is bit-identical to
+    the scenario's torch program; the rays match the CPU oracle's World.cast_rays on the same state
+    within the LIDAR tolerance, a ray outside it only at a hit / miss boundary (certified,
+    tests/_parity.py lidar_parity)."""
+    from tests._parity import lidar_parity
+
+    envs = {}
+    for mode in ("torch", "fused"):
+        saved = _rng_save()
+        with _Torch() if mode == "torch" else _NullCtx():
+            envs[mode] = make_env(name, num_envs=4096, device=gpu_device, seed=3, **kw)
+        if mode == "torch":
+            _rng_load(saved)
+    ref, fus = envs["torch"], envs["fused"]
+    worst = 0.0
+    for t in range(8):
+        actions = ref.get_random_actions()
+        outs = {}
+        for mode, env in envs.items():
+            s = _rng_save()
+            with _Torch() if mode == "torch" else _NullCtx():
+                outs[mode] = env.step([a.clone() for a in actions])
+            if mode == "torch":
+                _rng_load(s)
+        obs_t, obs_f = outs["torch"][0], outs["fused"][0]
+        for a, ot, of in zip(fus.world.policy_agents, obs_t, obs_f):
+            keep = torch.ones(ot.shape[-1], dtype=torch.bool)
+            keep[lidar_cols(fus, a)] = False
+            assert torch.equal(ot[:, keep], of[:, keep]), (t, a.name)
+        _assert_same(outs["torch"][1:], outs["fused"][1:], f"{name} rewards / dones / infos step {t}")
+        _assert_same(_state(ref), _state(fus), f"{name} state step {t}")
+        rep = lidar_parity(fus, measured=True)
+        assert rep["ok"], (t, rep)
+        worst = max(worst, rep["bad_rows"] / max(rep["rows"], 1))
+    assert worst < 1e-3  # boundary rays are rare

@@ -62,6 +62,8 @@ EXPORTED_SYMBOLS = (
     "vmas_distance_vjp",
     "vmas_cast_rays_vjp",
     "vmas_flocking_outputs",
+    "vmas_flocking_target_action",
+    "vmas_assert_publish_range",
     "vmas_transport_outputs",
     "vmas_discovery_outputs",
     "vmas_world_create",
@@ -342,7 +344,7 @@ class VmasFlockingIO(ctypes.Structure):
         ("target", _i32), ("n_rays", _i32), ("n_ray_targets", _i32), ("sum_mode", _i32),
         ("min_collision_distance", _f32), ("collision_reward", _f32), ("desired_distance", _f32),
         ("dist_shaping_factor", _f32), ("max_range", _f32), ("pad0", _f32),
-        ("collide_reward_on", _i32), ("pad1", _i32),
+        ("collide_reward_on", _i32), ("fast_lidar", _i32),
         ("agents", VmasShapeRef * _FA), ("scripted", _i32 * _FA), ("policy", _i32 * _FA),
         ("vel", VmasVec * _FA), ("rot", VmasVec * _FA), ("angles", _vp * _FA),
         ("ang_s0", _i32 * _FA), ("ang_s1", _i32 * _FA),
@@ -557,6 +559,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_assert_publish.argtypes = [_vp, _i32, _vp, ctypes.c_int64, _vp]
     lib.vmas_assert_wait.restype = _i32
     lib.vmas_assert_wait.argtypes = [_vp, _i32, ctypes.c_uint32, ctypes.POINTER(_i32), _vp]
+    lib.vmas_assert_publish_range.restype = _i32
+    lib.vmas_assert_publish_range.argtypes = [_vp, _i32, _vp, ctypes.c_int64, ctypes.c_int64, _i32, _i32, _vp, _vp, _vp]
+    lib.vmas_flocking_target_action.restype = _i32
+    lib.vmas_flocking_target_action.argtypes = [_i32, _vp, _i32, _f32, _vp, _vp]
     lib.vmas_distance.restype = _i32
     lib.vmas_distance.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _vp]
     lib.vmas_spawn_resolve.restype = _i32

@@ -160,7 +160,10 @@ __global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int
     __syncthreads();
     bool mine = false;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) mine |= cond[i] == 0;
-    if ((threadIdx.x & 63) == 0 && __any(mine)) atomicOr(&bad, 1u);
+    // (the vote outside the lane-0 branch: a short-circuit `lane == 0 && __any(..)` would vote
+    // with lane 0 alone)
+    const bool wave_bad = __any(mine);
+    if ((threadIdx.x & 63) == 0 && wave_bad) atomicOr(&bad, 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t e = *epoch + 1u;
@@ -168,6 +171,47 @@ __global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int
         *epoch = e;
         __hip_atomic_store(hsig, ((uint64_t)e << 32) | bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// A scripted agent's action range check (core.py:977-980: ((u / u_multiplier).abs() <= u_range)
+// .all()) evaluated and published in one kernel: the element-wise test, the AND over the batch
+// and the publish of k_assert_publish (instead of torch's divide / abs / compare / all-reduce
+// kernels and a publish).  Workgroups OR their verdict into the slot's work line and arrive on
+// its counter; the last one publishes and clears the line for the next launch.  (One 1024-thread
+// workgroup over the 65 536 elements of flocking's target took 30 us.)
+constexpr int kRangeThreads = 256, kRangePerThread = 8;
+__global__ void __launch_bounds__(kRangeThreads) k_assert_range(const float* u, int64_t s0, int64_t s1, int batch, int n,
+                                                                const float* mult, const float* range, uint32_t* epoch,
+                                                                uint64_t* hsig, uint32_t* work) {
+    __shared__ uint32_t bad;
+    __shared__ bool last;
+    if (threadIdx.x == 0) bad = 0u;
+    __syncthreads();
+    bool mine = false;
+    const int64_t total = (int64_t)batch * n, step = (int64_t)gridDim.x * kRangeThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kRangeThreads + threadIdx.x; i < total; i += step) {
+        const int64_t b = i / n;
+        const int c = (int)(i - b * n);
+        const float x = u[b * s0 + (int64_t)c * s1];
+        mine |= !(fabsf(x / mult[c]) <= range[c]);  // (NaN fails, as torch's comparison)
+    }
+    const bool wave_bad = __any(mine);  // (every lane takes part in the vote)
+    if ((threadIdx.x & 63) == 0 && wave_bad) atomicOr(&bad, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (bad) (void)__hip_atomic_fetch_or(&work[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);  // the verdict has landed before the arrival
+        last = __hip_atomic_fetch_add(&work[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    const uint32_t v = __hip_atomic_load(&work[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&work[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t e = *epoch + 1u;
+    if (e == 0u) e = 1u;
+    *epoch = e;
+    __hip_atomic_store(hsig, ((uint64_t)e << 32) | (v ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- random actions: every agent's uniform_ columns in one launch ------------------------------
@@ -236,6 +280,7 @@ struct VmasDeviceAssert {
     int device = 0;
     int n_slots = 0;
     uint32_t* epoch = nullptr;  // [n_slots] device epochs
+    uint32_t* work = nullptr;   // [n_slots][32] per-slot line: arrival counter, verdict (k_assert_range)
     uint64_t* hsig = nullptr;   // [n_slots] mapped, coherent pinned words
     uint64_t* dsig = nullptr;   // their device address
 };
@@ -360,6 +405,8 @@ int32_t vmas_assert_create(int32_t device, int32_t n_slots, VmasDeviceAssert** o
     ch->n_slots = n_slots;
     hipError_t e = hipMalloc((void**)&ch->epoch, 4 * (size_t)n_slots);
     if (e == hipSuccess) e = hipMemset(ch->epoch, 0, 4 * (size_t)n_slots);
+    if (e == hipSuccess) e = hipMalloc((void**)&ch->work, 128 * (size_t)n_slots);
+    if (e == hipSuccess) e = hipMemset(ch->work, 0, 128 * (size_t)n_slots);
     if (e == hipSuccess) e = hipHostMalloc((void**)&ch->hsig, 8 * (size_t)n_slots, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ch->dsig, ch->hsig, 0);
     if (e == hipSuccess) e = hipDeviceSynchronize();  // the epoch memset has landed before any capture
@@ -377,6 +424,7 @@ int32_t vmas_assert_create(int32_t device, int32_t n_slots, VmasDeviceAssert** o
 int32_t vmas_assert_destroy(VmasDeviceAssert* ch) {
     if (!ch) return VMAS_OK;
     if (ch->epoch) (void)hipFree(ch->epoch);
+    if (ch->work) (void)hipFree(ch->work);
     if (ch->hsig) (void)hipHostFree(ch->hsig);
     delete ch;
     return VMAS_OK;
@@ -387,6 +435,19 @@ int32_t vmas_assert_publish(VmasDeviceAssert* ch, int32_t slot, const uint8_t* c
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_assert_publish: bad arguments");
     hipLaunchKernelGGL(k_assert_publish, dim3(1), dim3(256), 0, (hipStream_t)stream, cond, n, ch->epoch + slot,
                        ch->dsig + slot);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
+int32_t vmas_assert_publish_range(VmasDeviceAssert* ch, int32_t slot, const float* u, int64_t s0, int64_t s1,
+                                  int32_t batch, int32_t n, const float* mult, const float* range, void* stream) {
+    if (!ch || !u || !mult || !range || slot < 0 || slot >= ch->n_slots || batch <= 0 || n <= 0)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_assert_publish_range: bad arguments");
+    const int64_t total = (int64_t)batch * n;
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (total + kRangeThreads * kRangePerThread - 1) /
+                                                                          (kRangeThreads * kRangePerThread)));
+    hipLaunchKernelGGL(k_assert_range, dim3(gx), dim3(kRangeThreads), 0, (hipStream_t)stream, u, s0, s1, batch, n, mult,
+                       range, ch->epoch + slot, ch->dsig + slot, ch->work + 32 * slot);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

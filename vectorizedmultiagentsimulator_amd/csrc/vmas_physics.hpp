@@ -580,6 +580,20 @@ VHD Real ray_sphere(V2 o, Real dc, Real ds, V2 sp, Real r, Real max_range) {
     return (inter && front) ? d : max_range;
 }
 
+// The same distance in its direct form (the fused scenario programs' fast LIDAR): u = centre -
+// origin, t = u . dir (the foot point's distance along the ray; the reference's |cp - o| and its
+// `front` test udot > 0), dn^2 = |u|^2 - t^2 (the reference's |sp - cp|^2), d = t - sqrt(r^2 - dn^2)
+// on a hit.  Mathematically the reference's value; in fp32 within the LIDAR parity tolerance,
+// and at a tangent ray or the front boundary the hit / miss decision can flip (certified by a
+// ray turned by ~1e-6 rad, tests/_parity.py lidar_parity).  `u` is the centre relative to the
+// origin, `r2` the squared radius.
+VHD Real ray_sphere_fast(V2 u, Real dc, Real ds, Real r2, Real max_range) {
+    const Real t = u.x * dc + u.y * ds;
+    const Real a = r2 - (u.x * u.x + u.y * u.y - t * t);
+    const Real m = sqrtf(a > 0.f ? a : 1e-8f);
+    return (a > 0.f && t > 0.f) ? t - m : max_range;
+}
+
 VHD Real ray_line(V2 o, Real dc, Real ds, V2 lp, Real lrot, Real L, Real max_range) {
     const V2 r = mk(cosf(lrot) * L, sinf(lrot) * L);
     const V2 s = mk(dc, ds);

@@ -127,35 +127,27 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
 // of p's LIDAR (one (env, agent, ray) per thread: a thread per (env, agent) casting all 12 rays
 // left the chip latency-bound at 3 waves per SIMD, 95 us per step at 32 768 envs x 8 agents).
 // Positions are loaded up front with independent loads (unrolled over the static bounds).
-__global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
-    constexpr int MA = VMAS_FLOCK_MAX_AGENTS, MT = VMAS_SCN_MAX_RAY_TARGETS;
-    const int b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= io.batch) return;
-    const int parts = (io.what & VMAS_SCN_OBS) ? 1 + io.n_rays : 1;
-    const int p = blockIdx.y / parts, part = blockIdx.y - p * parts, k = io.policy[p], na = io.n_all;
-    const V2 pk = ref_pos(io.agents[k], b);
+// Part 0 of policy agent p in env b: the reward block (REWARD) and the first six observation
+// entries (OBS).
+struct FlockHead {
+    float v[6];
+};
+// IO: the argument block by value, or (k_flocking_fast) read in place through the kernel
+// argument segment pointer -- structs copied out before use, see k_flocking_fast.
+template <class IO>
+__device__ __forceinline__ FlockHead flock_part0(IO& io, int b, int p, bool ret = false) {
+    FlockHead h{};
+    constexpr int MA = VMAS_FLOCK_MAX_AGENTS;
+    const int k = io.policy[p], na = io.n_all;
+    const VmasShapeRef ak = io.agents[k];
+    const V2 pk = ref_pos(ak, b);
     const int W = 6 + io.n_rays;
-    if (part > 0) {  // LIDAR ray r: Lidar.measure = World.cast_rays(angles + agent rot) (cast_one)
-        const int r = part - 1, nt = io.n_ray_targets;
-        V2 T[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            const VmasRayTarget& x = io.ray_targets[t];
-            T[t] = t < nt ? mk(x.pos[(long)b * x.pos_s0], x.pos[(long)b * x.pos_s0 + x.pos_s1]) : mk(0.f, 0.f);
-        }
-        const float a = io.angles[p][(long)b * io.ang_s0[p] + (long)r * io.ang_s1[p]] + ld_vec1(io.rot[p], b);
-        const float dc = cosf(a), ds = sinf(a);
-        float best = io.max_range;
-#pragma unroll
-        for (int t = 0; t < MT; ++t)  // (sphere targets: checked by the host entry point)
-            if (t < nt) best = tmin(best, ray_sphere(pk, dc, ds, T[t], io.ray_targets[t].radius, io.max_range));
-        io.lidar[p][(long)b * io.n_rays + r] = best;
-        io.obs[p][(long)b * W + 6 + r] = best;
-        return;
-    }
     V2 P[MA];
 #pragma unroll
-    for (int j = 0; j < MA; ++j) P[j] = j < na ? ref_pos(io.agents[j], b) : mk(0.f, 0.f);
+    for (int j = 0; j < MA; ++j) {
+        const VmasShapeRef aj = io.agents[j];
+        P[j] = j < na ? ref_pos(aj, b) : mk(0.f, 0.f);
+    }
     if (io.what & VMAS_SCN_REWARD) {
         if (p == 0) io.t[b] = io.t[b] + 1.f;  // self.t += 1 (first policy agent's call)
         // collision rewards: pairs (i < j) of world.agents in loop order; agent k meets them
@@ -206,19 +198,168 @@ __global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
         io.rewards[p][b] = cr + dr;
     }
     if (io.what & VMAS_SCN_OBS) {
-        const V2 v = ld_vec2(io.vel[p], b);
+        const VmasVec vp = io.vel[p];
+        const V2 v = ld_vec2(vp, b);
         V2 tp = mk(0.f, 0.f);
 #pragma unroll
         for (int j = 0; j < MA; ++j)
             if (j == io.target) tp = P[j];
-        float* o = io.obs[p] + (long)b * W;
-        o[0] = pk.x;
-        o[1] = pk.y;
-        o[2] = v.x;
-        o[3] = v.y;
-        o[4] = pk.x - tp.x;
-        o[5] = pk.y - tp.y;
+        h = FlockHead{{pk.x, pk.y, v.x, v.y, pk.x - tp.x, pk.y - tp.y}};
+        if (!ret) {
+            float* o = io.obs[p] + (long)b * W;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) o[i] = h.v[i];
+        }
     }
+    return h;
+}
+
+// flocking.py:149-206 (restated in scenarios/flocking.py), LIDAR bit-identical to k_cast_rays
+// (io.fast_lidar == 0).  Grid: x = 64-env groups, y = (policy agent p, part): part 0 is p's
+// reward and the first six observation entries, part 1 + r is ray r of p's LIDAR (one (env,
+// agent, ray) per thread: a thread per (env, agent) casting all 12 rays with the exact ray code
+// left the chip latency-bound at 3 waves per SIMD, 95 us per step at 32 768 envs x 8 agents).
+// Positions are loaded up front with independent loads (unrolled over the static bounds).
+__global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
+    constexpr int MT = VMAS_SCN_MAX_RAY_TARGETS;
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= io.batch) return;
+    const int parts = (io.what & VMAS_SCN_OBS) ? 1 + io.n_rays : 1;
+    const int p = blockIdx.y / parts, part = blockIdx.y - p * parts, k = io.policy[p];
+    if (part == 0) {
+        flock_part0(io, b, p);
+        return;
+    }
+    // LIDAR ray r: Lidar.measure = World.cast_rays(angles + agent rot) (cast_one)
+    const V2 pk = ref_pos(io.agents[k], b);
+    const int W = 6 + io.n_rays;
+    const int r = part - 1, nt = io.n_ray_targets;
+    V2 T[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const VmasRayTarget& x = io.ray_targets[t];
+        T[t] = t < nt ? mk(x.pos[(long)b * x.pos_s0], x.pos[(long)b * x.pos_s0 + x.pos_s1]) : mk(0.f, 0.f);
+    }
+    const float a = io.angles[p][(long)b * io.ang_s0[p] + (long)r * io.ang_s1[p]] + ld_vec1(io.rot[p], b);
+    const float dc = cosf(a), ds = sinf(a);
+    float best = io.max_range;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)  // (sphere targets: checked by the host entry point)
+        if (t < nt) best = tmin(best, ray_sphere(pk, dc, ds, T[t], io.ray_targets[t].radius, io.max_range));
+    io.lidar[p][(long)b * io.n_rays + r] = best;
+    io.obs[p][(long)b * W + 6 + r] = best;
+}
+
+// The same program with the fast LIDAR (io.fast_lidar, the default): the ray-sphere distance in
+// its direct form (ray_sphere_fast), hardware sin / cos / sqrt.  Grid: x = 64-env groups, y =
+// groups of 4 policy agents; a wave per (64 envs, agent): its reward / head (flock_part0) and all
+// of its rays (angles and targets loaded up front), the observation rows staged in LDS and
+// written out as contiguous blocks (a lane per env writes 4-byte values 4 * W bytes apart
+// otherwise: twice the output bytes reached HBM).  History (32 768 envs x 8 agents): a thread per
+// ray of the exact program, 53 us; a thread per (env, agent) with ocml sincosf and per-ray angle
+// loads, 89 us; waves over ray subsets with wave 0 also doing the reward, 48 us.
+constexpr int kFlockFastRays = 16, kFlockFastTargets = 8, kFlockFastW = 6 + kFlockFastRays;
+#ifdef __HIP_DEVICE_COMPILE__
+typedef const VmasFlockingIO __attribute__((address_space(4))) KFlockingIO;  // (the device pass)
+#else
+typedef const VmasFlockingIO KFlockingIO;  // (the host pass only parses the kernel)
+#endif
+__global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
+    constexpr int RM = kFlockFastRays, TM = kFlockFastTargets;
+    // The argument block read in place (s_load from the kernel argument segment): indexed by the
+    // wave's agent, the by-value parameter was copied to scratch (3.5 KiB per lane)
+#ifdef __HIP_DEVICE_COMPILE__
+    KFlockingIO& io = *(KFlockingIO*)__builtin_amdgcn_kernarg_segment_ptr();
+    (void)io_arg;
+#else
+    KFlockingIO& io = io_arg;
+#endif
+    __shared__ float S[4][64 * kFlockFastW];
+    const int lane = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
+    // (p made wave-uniform for the compiler: indexing the argument block's arrays with a per-lane
+    // index copies the whole 3.5 KiB block to scratch)
+    const int g0 = (int)blockIdx.x * 64, b = g0 + lane;
+    const int p = __builtin_amdgcn_readfirstlane((int)blockIdx.y * 4 + w);
+    if (p >= io.n_policy) return;  // (wave-uniform; no workgroup barrier below)
+    const bool valid = b < io.batch;
+    const int nr = io.n_rays, nt = io.n_ray_targets, W = 6 + nr;
+    const int bb = valid ? b : io.batch - 1;
+    const int row = lane * W;
+    if (io.what & VMAS_SCN_OBS) {
+        // loads first (independent): angles, rotation, position, targets
+        const float* ang = io.angles[p] + (long)bb * io.ang_s0[p];
+        const int as1 = io.ang_s1[p];
+        float A[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) A[r] = r < nr ? ang[(long)r * as1] : 0.f;
+        const VmasVec rv = io.rot[p];
+        const float rot = ld_vec1(rv, bb);
+        const VmasShapeRef ak = io.agents[io.policy[p]];
+        const V2 pk = ref_pos(ak, bb);
+        V2 T[TM];
+        float R2[TM];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+            const float* xp = io.ray_targets[t].pos;
+            const int s0 = io.ray_targets[t].pos_s0, s1 = io.ray_targets[t].pos_s1;
+            const float rad = io.ray_targets[t].radius;
+            T[t] = t < nt ? mk(xp[(long)bb * s0], xp[(long)bb * s0 + s1]) - pk : mk(0.f, 0.f);
+            R2[t] = t < nt ? rad * rad : 0.f;
+        }
+        if (valid) {
+            const FlockHead h = flock_part0(io, b, p, true);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) S[w][row + i] = h.v[i];
+        }
+        // (loops fully unrolled with guarded bodies, never `break`: a partly unrolled loop indexes
+        // A / T dynamically, which puts them in scratch)
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+            if (r >= nr) continue;
+            const float a = A[r] + rot;
+            // hardware sin / cos (v_sin / v_cos_f32: a few 1e-7 rad at these angles, within the
+            // LIDAR certification's 1e-6 rad) instead of ocml's range-reduced sincosf; large
+            // angles keep sincosf
+            float ds, dc;
+            if (fabsf(a) < 256.f) {
+                ds = __sinf(a);
+                dc = __cosf(a);
+            } else {
+                sincosf(a, &ds, &dc);
+            }
+            float best = io.max_range;
+#pragma unroll
+            for (int t = 0; t < TM; ++t) {
+                if (t >= nt) continue;
+                // ray_sphere_fast with the hardware square root
+                const float tt = T[t].x * dc + T[t].y * ds;
+                const float q = R2[t] - (T[t].x * T[t].x + T[t].y * T[t].y - tt * tt);
+                const float m = __builtin_amdgcn_sqrtf(q > 0.f ? q : 1e-8f);
+                best = tmin(best, (q > 0.f && tt > 0.f) ? tt - m : io.max_range);
+            }
+            S[w][row + 6 + r] = best;
+        }
+        // the wave's rows out as contiguous blocks: obs [64 x W], the LIDAR [64 x nr]
+        const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
+        float* obs = io.obs[p] + (long)g0 * W;
+        for (int i = lane; i < nv * W; i += 64) obs[i] = S[w][i];
+        float* lid = io.lidar[p] + (long)g0 * nr;
+        for (int i = lane; i < nv * nr; i += 64) {
+            const int e = i / nr;
+            lid[i] = S[w][e * W + 6 + (i - e * nr)];
+        }
+    } else if (valid) {
+        flock_part0(io, b, p);
+    }
+}
+
+// flocking's scripted target: u = stack([cos(t / period), sin(t / period)], dim=1) (the division
+// by a Python scalar as torch's divide kernel computes it: t * (1 / period) in fp32).
+__global__ void __launch_bounds__(256) k_flocking_target(const float* t, int batch, float inv, float* u) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= batch) return;
+    const float x = t[b] * inv;
+    reinterpret_cast<float2*>(u)[b] = make_float2(cosf(x), sinf(x));
 }
 
 // transport.py:130-190 (restated in scenarios/transport.py).  Grid: x = 64-env groups, y = part:
@@ -411,6 +552,16 @@ int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stre
     return VMAS_OK;
 }
 
+int32_t vmas_flocking_target_action(int32_t device, const float* t, int32_t batch, float period, float* u,
+                                    void* stream) {
+    if (device < 0 || !t || !u || batch <= 0 || period == 0.f)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_flocking_target_action: bad arguments");
+    const float inv = 1.0f / period;
+    hipLaunchKernelGGL(k_flocking_target, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, t, batch, inv, u);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
+
 int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* stream) {
     if (!io || device < 0 || io->batch <= 0 || io->n_all < 2 || io->n_all > VMAS_FLOCK_MAX_AGENTS || io->n_policy < 1 ||
         io->n_policy > io->n_all || io->target < 0 || io->target >= io->n_all || io->n_rays < 0 ||
@@ -427,7 +578,12 @@ int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* st
     VMAS_AUX_HIP(hipSetDevice(device));
     static_assert(sizeof(VmasFlockingIO) <= 4096, "kernel argument block");
     const int parts = (io->what & VMAS_SCN_OBS) ? 1 + io->n_rays : 1;
-    hipLaunchKernelGGL(k_flocking, dim3((io->batch + 63) / 64, io->n_policy * parts), dim3(64), 0, (hipStream_t)stream, *io);
+    if (io->fast_lidar && io->n_rays <= kFlockFastRays && io->n_ray_targets <= kFlockFastTargets)
+        hipLaunchKernelGGL(k_flocking_fast, dim3((io->batch + 63) / 64, (io->n_policy + 3) / 4), dim3(256), 0,
+                           (hipStream_t)stream, *io);
+    else
+        hipLaunchKernelGGL(k_flocking, dim3((io->batch + 63) / 64, io->n_policy * parts), dim3(64), 0, (hipStream_t)stream,
+                           *io);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

@@ -63,6 +63,14 @@ class Scenario(BaseScenario):
 
     def action_script_creator(self):
         def action_script(agent, world):
+            if _fused.enabled(world) and self.t.dtype is torch.float32 and self.t.is_contiguous():
+                # one native launch for the same values (vmas_flocking_target_action)
+                u = torch.empty(world.batch_dim, 2, device=self.t.device, dtype=torch.float32)
+                _fused.check(_fused.lib().vmas_flocking_target_action(
+                    _fused.device_index(world), self.t.data_ptr(), world.batch_dim, 30.0, u.data_ptr(),
+                    _fused.stream(world)), "vmas_flocking_target_action")
+                agent.action.u = u
+                return
             t = self.t / 30
             agent.action.u = torch.stack([torch.cos(t), torch.sin(t)], dim=1)
 
@@ -209,6 +217,7 @@ class Scenario(BaseScenario):
         io.desired_distance = float(self.desired_distance)
         io.dist_shaping_factor = float(self.dist_shaping_factor)
         io.collide_reward_on = 1 if self.collision_reward != 0 else 0
+        io.fast_lidar = 0 if _fused.EXACT_LIDAR else 1
         io.max_range = float(pol[0].sensors[0]._max_range)
         for i, a in enumerate(agents):
             io.agents[i] = _fused.ref(w, a, keep, 0)

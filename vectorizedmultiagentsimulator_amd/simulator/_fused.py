@@ -24,6 +24,10 @@ import torch
 from .. import _native as N
 
 _ON = os.environ.get("VMAS_FUSED_SCENARIOS", "1") != "0"
+# The programs' LIDAR: fast (default; the direct ray-sphere form, within the LIDAR parity
+# tolerance of the oracle, tests/test_fused.py) or, with VMAS_FUSED_EXACT_LIDAR=1, bit-identical
+# to World.cast_rays (k_cast_rays) and so to the scenario's torch program.
+EXACT_LIDAR = os.environ.get("VMAS_FUSED_EXACT_LIDAR", "0") == "1"
 
 
 _OFF_DEPTH = [0]

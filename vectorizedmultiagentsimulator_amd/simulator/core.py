@@ -771,8 +771,13 @@ class Agent(Entity):
         assert self._action.u.shape[1] == self.action_size, (
             f"Scripted action of agent {self.name} has wrong shape"
         )
-        ok = ((self._action.u / self.action.u_multiplier_tensor).abs() <= self.action.u_range_tensor).all()
         sink = world._assert_sink
+        rsink = getattr(world, "_assert_range_sink", None)
+        if sink is not None and rsink is not None and rsink(self._action.u, self.action.u_multiplier_tensor,
+                                                            self.action.u_range_tensor,
+                                                            f"Scripted physical action of {self.name} is out of range"):
+            return  # (graph mode: the check evaluated and published by one native kernel)
+        ok = ((self._action.u / self.action.u_multiplier_tensor).abs() <= self.action.u_range_tensor).all()
         if sink is None:
             assert ok, f"Scripted physical action of {self.name} is out of range"
         else:  # graph mode: checked on the device, raised from the same step() (environment/_graph.py)

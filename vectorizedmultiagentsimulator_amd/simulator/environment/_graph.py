@@ -250,6 +250,24 @@ class _DeviceAsserts:
         self.keep.append(ok)
         self.msgs.append(msg)
 
+    def capture_range(self, u: Tensor, mult: Tensor, rng: Tensor, msg: str) -> bool:
+        """A scripted action's range check ((u / mult).abs() <= rng).all(), evaluated and
+        published by one captured kernel (vmas_assert_publish_range); False (nothing done) when
+        the operands are not the fp32 [B, n] / [n] device tensors it takes."""
+        if len(self.msgs) >= self.MAX_SLOTS:
+            raise GraphUnsupported("too many device asserts in the captured step")
+        if (u.dim() != 2 or any(t.dtype is not torch.float32 or t.device != u.device for t in (u, mult, rng))
+                or mult.shape != (u.shape[1],) or rng.shape != (u.shape[1],) or not mult.is_contiguous()
+                or not rng.is_contiguous()):
+            return False
+        stream = ctypes.c_void_p(torch.cuda.current_stream(u.device).cuda_stream)
+        self.N.check_aux(self.lib.vmas_assert_publish_range(self.h, len(self.msgs), u.data_ptr(), u.stride(0),
+                                                            u.stride(1), u.shape[0], u.shape[1], mult.data_ptr(),
+                                                            rng.data_ptr(), stream), "vmas_assert_publish_range")
+        self.keep += [u, mult, rng]
+        self.msgs.append(msg)
+        return True
+
     def after_replay(self, dev, raise_: bool = True):
         """Waits for this replay's words; raises the first violated assert (raise_) or only keeps
         the sequence in step (a replay that is rolled back for another reason)."""
@@ -540,6 +558,7 @@ class StepGraph:
         segs = _Segments(side)
         try:
             env.world._assert_sink = asserts.capture_sink
+            env.world._assert_range_sink = asserts.capture_range
             env.world._hole_sink = segs.hole
             torch.cuda.synchronize(dev)
             with torch.cuda.stream(side), consts:
@@ -586,6 +605,7 @@ class StepGraph:
                 gc.enable()
             env._raw_outputs = False
             env.world._assert_sink = None
+            env.world._assert_range_sink = None
             env.world._hole_sink = None
         del contents
         self.graph = g
