@@ -385,12 +385,13 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
  * o_i + k * per_try and for y at o_i + k * per_try + inc, per_try = 2 * inc, with inc, the element
  * to (philox subsequence, offset) mapping and the float mapping (`mode`, vmas_uniform_columns) of
  * PyTorch's distribution kernel; o_0 = offset and o_{i+1} = o_i + consumed_i * per_try, consumed_i
- * = 1 if every env accepts try 0, else max accepted try + 2 (the reference loop).  One kernel per
- * target, chained on `stream` through max_accepted (device int32 [n_targets], written by the
- * call): no host wait inside.  The caller reads max_accepted once afterwards and advances the
- * generator by sum_i consumed_i * per_try (*increment returns inc).  max_accepted[n_targets]
- * counts envs that found no position within VMAS_SPAWN_MAX_TRIES tries (the reference would loop
- * on; the caller raises). */
+ * = 1 if every env accepts try 0, else max accepted try + 2 (the reference loop).  ONE launch on
+ * `stream` (workgroups claim (target, 64 envs) items in order; target i's items start once target
+ * i - 1's are done), no host wait inside.  The caller reads max_accepted once afterwards and
+ * advances the generator by sum_i consumed_i * per_try (*increment returns inc).
+ * max_accepted[n_targets] counts envs that found no position within VMAS_SPAWN_MAX_TRIES tries
+ * (the reference would loop on; the caller raises), max_accepted[VMAS_SPAWN_ERR_WORD] is
+ * nonzero when the launch's bounded wait timed out (the caller raises). */
 #define VMAS_SPAWN_MAX_TARGETS 16
 #define VMAS_SPAWN_MAX_TRIES 65536
 typedef struct VmasSpawnTargetsIO {
@@ -403,8 +404,12 @@ typedef struct VmasSpawnTargetsIO {
     int32_t cov_s0, cov_s1;
     float min_dist, x_lo, x_hi, y_lo, y_hi, pad1;
     uint64_t seed, offset;
-    int32_t* max_accepted;                /* [n_targets + 1] device int32 */
+    int32_t* max_accepted;                /* VMAS_SPAWN_WORDS(n_targets) device int32: [0, T) per-target max
+                                             accepted try, [T] envs with no position found, [64] 1 when the
+                                             launch's bounded wait timed out (the rest: its counters) */
 } VmasSpawnTargetsIO;
+#define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets))
+#define VMAS_SPAWN_ERR_WORD 64
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream);
 
 /* ---- fused scenario programs (csrc/vmas_scenarios.hip) -------------------
@@ -537,6 +542,8 @@ typedef struct VmasDiscoveryIO {
     float covering_range, covering_rew_coeff, time_penalty;
     int32_t agents_per_target, shared_reward, n_entities, n_lidars;
     int32_t time_int;             /* time_rew is int64 (torch.full of a python int), value time_penalty_i */
+    int32_t fast_lidar;           /* 1: OBS with the direct ray-sphere form (k_discovery_obs_fast; within
+                                     the LIDAR parity tolerance); 0: bit-identical to k_cast_rays */
     int64_t time_penalty_i;
     int32_t agent_entity[VMAS_DISC_MAX_AGENTS];  /* table index of agent i */
     int32_t target_entity[VMAS_DISC_MAX_TARGETS]; /* table index of target j (scenario order) */

@@ -137,11 +137,13 @@ def test_reduce_order_probe_finds_torch_mean_order_gpu(gpu_device, n):
 # (scenario, kwargs, observation columns that are LIDAR rays, per policy agent)
 FAST_LIDAR = [
     ("flocking", dict(n_agents=5), lambda env, a: slice(6, None)),
+    ("discovery", dict(n_agents=5), lambda env, a: slice(4, None)),
+    ("discovery", dict(n_agents=8, n_targets=7, use_agent_lidar=True), lambda env, a: slice(4, None)),
 ]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,kw,lidar_cols", FAST_LIDAR, ids=[c[0] for c in FAST_LIDAR])
+@pytest.mark.parametrize("name,kw,lidar_cols", FAST_LIDAR, ids=[f"{c[0]}{i}" for i, c in enumerate(FAST_LIDAR)])
 def test_fast_lidar_program_gpu(gpu_device, name, kw, lidar_cols):
     """The default fused programs (fast LIDAR): every output but the LIDAR rays is bit-identical to
     the scenario's torch program; the rays match the CPU oracle's World.cast_rays on the same state

@@ -60,7 +60,7 @@ def test_spawn_matches_reference_loop_gpu(gpu_device, b, n_occ, min_dist):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("b,a,t,min_dist", [(1, 3, 2, 0.2), (16384, 8, 7, 0.2), (4096, 5, 7, 0.45), (333, 4, 16, 0.2)])
+@pytest.mark.parametrize("b,a,t,min_dist", [(1, 3, 2, 0.2), (16384, 8, 7, 0.2), (4096, 5, 7, 0.45), (333, 4, 16, 0.2), (131072, 8, 7, 0.2)])
 def test_respawn_targets_matches_reference_loop_gpu(gpu_device, b, a, t, min_dist):
     """Discovery's respawn loop (discovery.py:237-252: per target, find_random_pos_for_entity over
     the agents and every other target, then where(covered)) as ONE stream-ordered native call

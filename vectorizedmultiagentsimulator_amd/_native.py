@@ -244,6 +244,13 @@ VMAS_SPAWN_MAX_TARGETS = 16
 VMAS_SPAWN_MAX_TRIES = 65536
 
 
+VMAS_SPAWN_ERR_WORD = 64
+
+
+def spawn_words(n_targets: int) -> int:  # VMAS_SPAWN_WORDS
+    return 96 + 32 * n_targets
+
+
 class VmasSpawnTargetsIO(ctypes.Structure):
     _fields_ = [
         ("batch", _i32), ("n_agents", _i32), ("n_targets", _i32), ("mode", _i32),
@@ -381,7 +388,7 @@ class VmasDiscoveryIO(ctypes.Structure):
         ("batch", _i32), ("n_agents", _i32), ("n_targets", _i32), ("what", _i32),
         ("covering_range", _f32), ("covering_rew_coeff", _f32), ("time_penalty", _f32),
         ("agents_per_target", _i32), ("shared_reward", _i32), ("n_entities", _i32), ("n_lidars", _i32),
-        ("time_int", _i32), ("time_penalty_i", ctypes.c_int64),
+        ("time_int", _i32), ("fast_lidar", _i32), ("time_penalty_i", ctypes.c_int64),
         ("agent_entity", _i32 * _DA), ("target_entity", _i32 * _DT),
         ("pos", VmasVec * _DE), ("radius", _f32 * _DE), ("vel", VmasVec * _DA), ("rot", VmasVec * _DA),
         ("n_rays", _i32 * _DL), ("max_range", _f32 * _DL), ("mask", ctypes.c_uint32 * _DL),

@@ -594,6 +594,32 @@ VHD Real ray_sphere_fast(V2 u, Real dc, Real ds, Real r2, Real max_range) {
     return (a > 0.f && t > 0.f) ? t - m : max_range;
 }
 
+// ray_sphere_fast without compares (the fused programs' inner loop: 6 VALU + the hardware square
+// root per (ray, sphere) instead of ~26 with the compares, selects and the NaN-propagating min as
+// divergent branches).  c = r^2 - |u|^2 per sphere; returns t - sqrt(min(a, t * 1e30)), a = t^2 + c
+// = r^2 - dn^2: NaN on a miss (a < 0, or t < 0 making the root's argument negative), which the
+// caller's fminf drops (IEEE minNum keeps the other operand) -- so the running minimum starts at
+// max_range and never becomes NaN, as the reference's where(hit, d, max_range) before its min
+// (non-finite positions fail its comparisons: max_range; here: NaN, dropped).  Differs from
+// ray_sphere_fast only on the measure-zero boundaries a == 0 and t == 0 (and t * 1e30 < a, t below
+// ~1e-32), the hit / miss flips the LIDAR certification covers.
+VHD float ray_sphere_fast_nan(float ux, float uy, float c, float dc, float ds) {
+    const float t = __builtin_fmaf(ux, dc, uy * ds);
+    const float a = __builtin_fmaf(t, t, c);
+    return t - __builtin_amdgcn_sqrtf(__builtin_fminf(a, t * 1e30f));
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+// v_min_f32 as is (IEEE mode: a quiet NaN operand yields the other one).  fminf makes the compiler
+// quieten a running minimum that crosses a basic block (v_max_f32 x, x) on every update.
+__device__ __forceinline__ float min_drop_nan(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+#else
+VHD float min_drop_nan(float a, float b) { return fminf(a, b); }
+#endif
+
 VHD Real ray_line(V2 o, Real dc, Real ds, V2 lp, Real lrot, Real L, Real max_range) {
     const V2 r = mk(cosf(lrot) * L, sinf(lrot) * L);
     const V2 s = mk(dc, ds);

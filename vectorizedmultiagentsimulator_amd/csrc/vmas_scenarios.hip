@@ -313,10 +313,18 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
         }
         // (loops fully unrolled with guarded bodies, never `break`: a partly unrolled loop indexes
         // A / T dynamically, which puts them in scratch)
+        float C[TM];
 #pragma unroll
-        for (int r = 0; r < RM; ++r) {
-            if (r >= nr) continue;
-            const float a = A[r] + rot;
+        for (int t = 0; t < TM; ++t) C[t] = R2[t] - (T[t].x * T[t].x + T[t].y * T[t].y);
+        // rays in a rolled loop, targets unrolled inside (see k_discovery_obs_fast)
+        // (the angles wait in the rays' own LDS slots: a register array indexed at run time goes to
+        // scratch)
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+            if (r < nr) S[w][row + 6 + r] = A[r] + rot;
+#pragma unroll 1
+        for (int r = 0; r < nr; ++r) {
+            const float a = S[w][row + 6 + r];
             // hardware sin / cos (v_sin / v_cos_f32: a few 1e-7 rad at these angles, within the
             // LIDAR certification's 1e-6 rad) instead of ocml's range-reduced sincosf; large
             // angles keep sincosf
@@ -331,11 +339,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
 #pragma unroll
             for (int t = 0; t < TM; ++t) {
                 if (t >= nt) continue;
-                // ray_sphere_fast with the hardware square root
-                const float tt = T[t].x * dc + T[t].y * ds;
-                const float q = R2[t] - (T[t].x * T[t].x + T[t].y * T[t].y - tt * tt);
-                const float m = __builtin_amdgcn_sqrtf(q > 0.f ? q : 1e-8f);
-                best = tmin(best, (q > 0.f && tt > 0.f) ? tt - m : io.max_range);
+                best = min_drop_nan(best, ray_sphere_fast_nan(T[t].x, T[t].y, C[t], dc, ds));
             }
             S[w][row + 6 + r] = best;
         }
@@ -535,6 +539,190 @@ __global__ void __launch_bounds__(64) k_discovery_obs(VmasDiscoveryIO io) {
     o[col + r] = best;
 }
 
+#ifdef __HIP_DEVICE_COMPILE__
+typedef const VmasDiscoveryIO __attribute__((address_space(4))) KDiscoveryIO;  // (see k_flocking_fast)
+#define VMAS_KARG(T, name) T& io = *(T*)__builtin_amdgcn_kernarg_segment_ptr(); (void)name
+#else
+typedef const VmasDiscoveryIO KDiscoveryIO;
+#define VMAS_KARG(T, name) T& io = name
+#endif
+
+// REWARD with a wave per agent (k_discovery_reward has one thread per env: 256 waves for 16 384
+// envs, 31.5 us): lane = env of the workgroup's 64, wave i = agent i.  The agents' in-range bits
+// meet in LDS for the per-target counts; wave 0 sums the covering rewards in agent order (the
+// reference's loop order: bit-identical); the [64 x A x T] distances and the stacks are staged in
+// LDS and written out as contiguous blocks.
+constexpr int kDiscFastAgents = 16, kDiscFastTargets = 16;
+__global__ void __launch_bounds__(1024) k_discovery_reward_fast(VmasDiscoveryIO io_arg) {
+    VMAS_KARG(KDiscoveryIO, io_arg);
+    constexpr int MT = kDiscFastTargets;
+    __shared__ float D[64 * kDiscFastAgents * kDiscFastTargets];  // dists rows of the 64 envs (64 KiB)
+    __shared__ uint32_t IN[kDiscFastAgents][64];                  // agent i's in-range target bits
+    __shared__ float CR[kDiscFastAgents][64];                     // agent i's covering reward
+    __shared__ float SH[64];
+    const int lane = (int)(threadIdx.x & 63u);
+    const int i = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int A = io.n_agents, T = io.n_targets, g0 = (int)blockIdx.x * 64, b = g0 + lane;
+    const bool valid = b < io.batch;
+    const int bb = valid ? b : io.batch - 1;
+    const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
+    V2 PT[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+        const VmasVec pv = io.pos[io.target_entity[j < T ? j : 0]];
+        PT[j] = j < T ? ld_vec2(pv, bb) : mk(0.f, 0.f);
+    }
+    const VmasVec av = io.pos[io.agent_entity[i]];
+    const V2 pa = ld_vec2(av, bb);
+    // torch.cdist (p = 2): sqrt(fl(fl(d0^2) + fl(d1^2))); agent i's distances and in-range bits
+    uint32_t in = 0u;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+        if (j >= T) continue;
+        const float d0 = pa.x - PT[j].x, d1 = pa.y - PT[j].y;
+        const float d = sqrtf(d0 * d0 + d1 * d1);
+        D[(lane * A + i) * T + j] = d;
+        in |= (d < io.covering_range) ? (1u << j) : 0u;
+    }
+    IN[i][lane] = in;
+    __syncthreads();
+    // per target: the count of agents in range, covered when >= agents_per_target
+    uint32_t covm = 0u;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+        if (j >= T) continue;
+        int cnt = 0;
+        for (int k = 0; k < A; ++k) cnt += (IN[k][lane] >> j) & 1u;
+        covm |= cnt >= io.agents_per_target ? (1u << j) : 0u;
+        if (i == 0 && valid) {
+            io.per_target[(long)b * T + j] = (int64_t)cnt;
+            io.covered[(long)b * T + j] = cnt >= io.agents_per_target ? 1 : 0;
+        }
+    }
+    // agent i's covering reward: (count of covered targets in range) * coeff
+    const float covr = 0.f + (float)__builtin_popcount(in & covm) * io.covering_rew_coeff;
+    CR[i][lane] = covr;
+    if (valid) {
+        io.covering[i][b] = covr;
+        io.collision[i][b] = 0.f;  // collision_rew[:] = 0 (penalty 0: nothing added)
+    }
+    __syncthreads();
+    if (i == 0) {  // shared[:] = 0; += each agent's covering reward in agent order; halved where nonzero
+        float shared = 0.f;
+        for (int k = 0; k < A; ++k) shared = shared + CR[k][lane];
+        if (shared != 0.f) shared = shared / 2.f;
+        SH[lane] = shared;
+        if (valid) {
+            io.shared[b] = shared;
+            if (io.time_int) reinterpret_cast<int64_t*>(io.time_rew)[b] = io.time_penalty_i;  // torch.full(int)
+            else reinterpret_cast<float*>(io.time_rew)[b] = io.time_penalty;
+        }
+    }
+    __syncthreads();
+    if (valid) {
+        const float cv = io.shared_reward ? SH[lane] : covr;
+        io.rewards[i][b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
+    }
+    // the stacks and the distances as contiguous blocks of the workgroup's envs
+    const int tid = (int)threadIdx.x, nth = (int)blockDim.x;
+    float* dists = io.dists + (long)g0 * A * T;
+    for (int k = tid; k < nv * A * T; k += nth) dists[k] = D[k];
+    float2* ap = reinterpret_cast<float2*>(io.agents_pos) + (long)g0 * A;
+    float2* tp = reinterpret_cast<float2*>(io.targets_pos) + (long)g0 * T;
+    for (int k = tid; k < nv * A; k += nth) {
+        const int e = k / A, a = k - e * A;
+        const VmasVec v = io.pos[io.agent_entity[a]];
+        ap[k] = make_float2(v.p[(long)(g0 + e) * v.s0], v.p[(long)(g0 + e) * v.s0 + v.s1]);
+    }
+    for (int k = tid; k < nv * T; k += nth) {
+        const int e = k / T, j = k - e * T;
+        const VmasVec v = io.pos[io.target_entity[j]];
+        tp[k] = make_float2(v.p[(long)(g0 + e) * v.s0], v.p[(long)(g0 + e) * v.s0 + v.s1]);
+    }
+}
+
+// OBS with the fast LIDAR (io.fast_lidar): a wave per (64 envs, agent), every ray of its LIDARs
+// from the entity positions loaded once, the direct ray-sphere form with hardware sin / cos /
+// sqrt (as k_flocking_fast), the observation rows staged in LDS and written as contiguous blocks.
+constexpr int kDiscFastEntities = 16, kDiscFastRays = 16;  // per LIDAR
+constexpr int kDiscFastW = 4 + VMAS_DISC_MAX_LIDARS * kDiscFastRays;
+__global__ void __launch_bounds__(256) k_discovery_obs_fast(VmasDiscoveryIO io_arg) {
+    VMAS_KARG(KDiscoveryIO, io_arg);
+    constexpr int ME = kDiscFastEntities, RM = kDiscFastRays;
+    __shared__ float S[4][64 * kDiscFastW];
+    const int lane = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
+    const int a = __builtin_amdgcn_readfirstlane((int)blockIdx.y * 4 + w);
+    if (a >= io.n_agents) return;  // (wave-uniform; no workgroup barrier below)
+    const int g0 = (int)blockIdx.x * 64, b = g0 + lane;
+    const bool valid = b < io.batch;
+    const int bb = valid ? b : io.batch - 1;
+    const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
+    const int self = io.agent_entity[a], ne = io.n_entities;
+    int rays = 0;
+    for (int s = 0; s < io.n_lidars; ++s) rays += io.n_rays[s];
+    const int W = 4 + rays, row = lane * W;
+    const VmasVec sp = io.pos[self], vv = io.vel[a], rv = io.rot[a];
+    const V2 p = ld_vec2(sp, bb), v = ld_vec2(vv, bb);
+    const float rot = ld_vec1(rv, bb);
+    V2 T[ME];
+    float R2[ME];
+#pragma unroll
+    for (int e = 0; e < ME; ++e) {
+        const VmasVec ev = io.pos[e < ne ? e : 0];
+        const float rad = io.radius[e < ne ? e : 0];
+        T[e] = e < ne ? ld_vec2(ev, bb) - p : mk(0.f, 0.f);
+        R2[e] = rad * rad;
+    }
+    S[w][row + 0] = p.x;
+    S[w][row + 1] = p.y;
+    S[w][row + 2] = v.x;
+    S[w][row + 3] = v.y;
+    float C[ME];
+#pragma unroll
+    for (int e = 0; e < ME; ++e) C[e] = R2[e] - (T[e].x * T[e].x + T[e].y * T[e].y);
+    int col = 4;
+    for (int s = 0; s < io.n_lidars; ++s) {
+        const uint32_t mask = io.mask[s] & ~(1u << self);  // World.cast_rays skips the entity itself
+        const int nr = io.n_rays[s];
+        const float mr = io.max_range[s];
+        const float* ang = io.angles[s][a] + (long)bb * io.ang_s0[s][a];
+        const int as1 = io.ang_s1[s][a];
+        // rays in a rolled loop (entities unrolled inside, a uniform branch on the LIDAR's mask):
+        // the fully unrolled rays x entities body was ~35 KiB of straight-line code, each wave
+        // streaming it through the instruction cache once
+        // (the angles, loaded together up front, wait in the rays' own LDS slots)
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+            if (r < nr) S[w][row + col + r] = ang[(long)r * as1] + rot;
+#pragma unroll 1
+        for (int r = 0; r < nr; ++r) {
+            const float th = S[w][row + col + r];
+            float dc, ds;
+            if (fabsf(th) < 256.f) {
+                ds = __sinf(th);
+                dc = __cosf(th);
+            } else {
+                sincosf(th, &ds, &dc);
+            }
+            float best = mr;
+#pragma unroll
+            for (int e = 0; e < ME; ++e) {
+                if (e >= ne || !((mask >> e) & 1u)) continue;
+                best = min_drop_nan(best, ray_sphere_fast_nan(T[e].x, T[e].y, C[e], dc, ds));
+            }
+            S[w][row + col + r] = best;
+        }
+        float* lid = io.lidar[s][a] + (long)g0 * nr;
+        for (int k = lane; k < nv * nr; k += 64) {
+            const int e = k / nr;
+            lid[k] = S[w][e * W + col + (k - e * nr)];
+        }
+        col += nr;
+    }
+    float* obs = io.obs[a] + (long)g0 * W;
+    for (int k = lane; k < nv * W; k += 64) obs[k] = S[w][k];
+}
+
 }  // namespace
 
 extern "C" {
@@ -622,10 +810,22 @@ int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* 
     VMAS_AUX_HIP(hipSetDevice(device));
     static_assert(sizeof(VmasDiscoveryIO) <= 4096, "kernel argument block");
     const unsigned gx = (unsigned)((io->batch + 63) / 64);
-    if (io->what & VMAS_SCN_REWARD)
-        hipLaunchKernelGGL(k_discovery_reward, dim3(gx), dim3(64), 0, (hipStream_t)stream, *io);
-    if (io->what & VMAS_SCN_OBS)
-        hipLaunchKernelGGL(k_discovery_obs, dim3(gx, io->n_agents * (1 + rays)), dim3(64), 0, (hipStream_t)stream, *io);
+    if (io->what & VMAS_SCN_REWARD) {
+        if (io->n_agents <= kDiscFastAgents && io->n_targets <= kDiscFastTargets && io->n_targets >= 1)
+            hipLaunchKernelGGL(k_discovery_reward_fast, dim3(gx), dim3(64 * io->n_agents), 0, (hipStream_t)stream, *io);
+        else
+            hipLaunchKernelGGL(k_discovery_reward, dim3(gx), dim3(64), 0, (hipStream_t)stream, *io);
+    }
+    if (io->what & VMAS_SCN_OBS) {
+        bool fast = io->fast_lidar && io->n_entities <= kDiscFastEntities;
+        for (int s = 0; s < io->n_lidars; ++s) fast = fast && io->n_rays[s] <= kDiscFastRays;
+        if (fast)
+            hipLaunchKernelGGL(k_discovery_obs_fast, dim3(gx, (io->n_agents + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                               *io);
+        else
+            hipLaunchKernelGGL(k_discovery_obs, dim3(gx, io->n_agents * (1 + rays)), dim3(64), 0, (hipStream_t)stream,
+                               *io);
+    }
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }

@@ -208,82 +208,145 @@ __device__ __forceinline__ bool near(float ox, float oy, float x, float y, float
     return d0 * d0 + d1 * d1 < d2_min;
 }
 
-// Target i of the respawn loop.  A workgroup of kSpawnWaves waves takes 64 envs; wave w tries
-// k = w, w + kSpawnWaves, ... for its lane's env and stops at the first accepted try or once
-// another wave has accepted an earlier one (the per-lane minimum in LDS): the first accepted try
-// of each env, as the reference's loop keeps it, with a kSpawnWaves times shorter serial chain.
-// The occupied positions are staged in LDS.  (One wave per 64 envs, the occupied set in
-// scratch: 37 us per target at 16 384 envs; 4 waves, the set in registers: the same.)  The
-// generator offset of the target's first try follows from the earlier targets' max accepted
-// tries (stream order: their kernels have completed).
+// The respawn loop of every target in ONE launch.  Work item (i, g) = target i for the 64 envs of
+// group g: a workgroup of kSpawnWaves waves, wave w tries k = w, w + kSpawnWaves, ... for its lane's
+// env and stops at the first accepted try or once another wave has accepted an earlier one (the
+// per-lane minimum in LDS): the first accepted try of each env, as the reference's loop keeps it,
+// with a kSpawnWaves times shorter serial chain.  The occupied positions are staged in LDS.
+//
+// Target i's generator offset follows from the earlier targets' max accepted tries over ALL envs,
+// and its occupied set holds the earlier targets' new positions: item (i, g) starts once every
+// item of target i - 1 is done.  Workgroups claim items in order from a counter and wait for the
+// previous target's done count -- every item they wait for was claimed earlier by a running
+// workgroup, so the launch needs no co-residency (the k_world claim pattern); the wait is bounded
+// (kSpawnWaitTicks, then the error word and every workgroup leaves).  Before: a launch per target,
+// 7 x 14.7 us at 16 384 envs.
+//
+// The grid is at most one workgroup per env group, so at most that many workgroups poll one done
+// counter; each counter has a 128-byte line of its own (polls are sc1 loads served beyond the
+// L2: on a shared line they delay the claims and the maxima -- 29 us per target when every
+// word sat on one line and 1024 workgroups polled it).
+//
+// max_accepted words: [0, T) per-target max accepted try, [T] unresolved envs, [32] the claim
+// counter, [64] error (1: a wait timed out), [96 + 32 i] target i's done items.
 constexpr int kSpawnWaves = 8;
 constexpr int kSpawnMaxOcc = 32 + VMAS_SPAWN_MAX_TARGETS - 1;  // agents + the other targets
+constexpr unsigned long long kSpawnWaitTicks = 100000000ull;   // s_memrealtime (100 MHz): 1 s
 
-__global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_target(VmasSpawnTargetsIO io, DrawGrid g, int i,
-                                                                 float d2_min) {
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
+                                                                  int n_groups) {
     __shared__ int best[64];
-    __shared__ float2 occ[kSpawnMaxOcc][64];  // the occupied positions of the workgroup's 64 envs
+    __shared__ int item_s;
+    __shared__ unsigned long long off_s;
+    __shared__ float2 occ[kSpawnMaxOcc][64];  // the occupied positions of the item's 64 envs
     __shared__ float2 won[kSpawnWaves][64];   // each wave's accepted position (at most one per lane)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b = blockIdx.x * 64 + lane;
-    const bool valid = b < io.batch;
-    const int bb = valid ? b : io.batch - 1;
-    // (read early: wave 0 applies the accepted position where the target was covered)
-    const bool cov = wave == 0 && valid && io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1];
-    if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+    const int T = io.n_targets, n_items = T * n_groups;
+    int32_t* const W = io.max_accepted;
+    int32_t* const claim = W + 32;
+    int32_t* const err = W + 64;
+    int32_t* const done = W + 96;  // target i's counter at done[32 * i]
     const unsigned long long per_try = 2ull * g.inc;
-    unsigned long long off = io.offset;
-    for (int j = 0; j < i; ++j) {
-        const int m = io.max_accepted[j];
-        off += (unsigned long long)(m == 0 ? 1 : m + 2) * per_try;
-    }
-    // occupied: the agents, then every other target (earlier ones already moved)
-    const int n_occ = io.n_agents + io.n_targets - 1;
-    for (int m = wave; m < n_occ; m += kSpawnWaves) {
-        const float* p;
-        int s1;
-        if (m < io.n_agents) {
-            p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
-            s1 = io.ag_s2;
-        } else {
-            const int j = m - io.n_agents + (m - io.n_agents >= i ? 1 : 0);
-            p = io.pos[j] + (long)bb * io.pos_s0[j];
-            s1 = io.pos_s1[j];
-        }
-        occ[m][lane] = make_float2(p[0], p[s1]);
-    }
-    __syncthreads();
-    if (valid) {
-        for (int k = wave; k < VMAS_SPAWN_MAX_TRIES; k += kSpawnWaves) {
-            if (k >= __hip_atomic_load(&best[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            const unsigned long long o = off + (unsigned long long)k * per_try;
-            const float x = uniform_at(io.seed, o, g, b, io.x_lo, io.x_hi, io.mode);
-            const float y = uniform_at(io.seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
-            bool hit = false;
-            for (int m = 0; m < n_occ; ++m) {
-                const float2 o2 = occ[m][lane];
-                hit = hit || near(o2.x, o2.y, x, y, d2_min);
+    const int n_occ = io.n_agents + T - 1;
+    // (thread 0) the claim of the coming item, taken one item ahead so that the claim's round trip
+    // overlaps the current item; still deadlock-free: the smallest unfinished item is always some
+    // workgroup's current one, and it waits only for smaller items
+    int next = threadIdx.x == 0 ? atomicAdd(claim, 1) : 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            int it = next;
+            if (it < n_items) next = atomicAdd(claim, 1);
+            if (it < n_items && it >= n_groups) {  // wait for every item of the previous target
+                const int* dp = done + 32 * (it / n_groups - 1);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (ld_agent(dp) < n_groups) {
+                    if (ld_agent(err) || __builtin_amdgcn_s_memrealtime() - t0 > kSpawnWaitTicks) {
+                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        it = n_items;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
             }
-            if (!hit) {
-                won[wave][lane] = make_float2(x, y);
-                atomicMin(&best[lane], k);
-                break;
+            item_s = it;
+            if (it < n_items) {  // target i's generator offset, from the earlier targets' maxima
+                const int i = it / n_groups;
+                int mv[VMAS_SPAWN_MAX_TARGETS];
+#pragma unroll
+                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j) mv[j] = j < i ? ld_agent(W + j) : 0;  // (one round trip)
+                unsigned long long off = io.offset;
+#pragma unroll
+                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j)
+                    if (j < i) off += (unsigned long long)(mv[j] == 0 ? 1 : mv[j] + 2) * per_try;
+                off_s = off;
             }
         }
-    }
-    __syncthreads();
-    if (wave != 0) return;
-    const int k = valid ? best[lane] : 0;
-    const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
-    if (unresolved) atomicAdd(&io.max_accepted[io.n_targets], 1);  // (the word after the maxima)
-    int km = unresolved ? 0 : k;  // one atomic per wave
-    for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
-    if (lane == 0 && km > 0) atomicMax(&io.max_accepted[i], km);
-    if (cov && !unresolved) {  // try k was drawn and accepted by wave k % kSpawnWaves
-        const float2 xy = won[k % kSpawnWaves][lane];
-        float* p = io.pos[i] + (long)b * io.pos_s0[i];
-        p[0] = xy.x;
-        p[io.pos_s1[i]] = xy.y;
+        __syncthreads();
+        const int it = item_s;
+        if (it >= n_items) return;
+        const int i = it / n_groups, grp = it - i * n_groups;
+        const int b = grp * 64 + lane;
+        const bool valid = b < io.batch;
+        const int bb = valid ? b : io.batch - 1;
+        const bool cov = wave == 0 && valid && io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1];
+        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+        const unsigned long long off = off_s;
+        // occupied: the agents, then every other target (earlier ones already moved, by items that
+        // may have run on another XCD: loaded with agent-scope atomics, sc1, as they were stored)
+        for (int m = wave; m < n_occ; m += kSpawnWaves) {
+            if (m < io.n_agents) {
+                const float* p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
+                occ[m][lane] = make_float2(p[0], p[io.ag_s2]);
+            } else {
+                const int j = m - io.n_agents + (m - io.n_agents >= i ? 1 : 0);
+                const float* p = io.pos[j] + (long)bb * io.pos_s0[j];
+                occ[m][lane] = make_float2(ld_agent(p), ld_agent(p + io.pos_s1[j]));
+            }
+        }
+        __syncthreads();
+        if (valid) {
+            for (int k = wave; k < VMAS_SPAWN_MAX_TRIES; k += kSpawnWaves) {
+                if (k >= __hip_atomic_load(&best[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                const unsigned long long o = off + (unsigned long long)k * per_try;
+                const float x = uniform_at(io.seed, o, g, b, io.x_lo, io.x_hi, io.mode);
+                const float y = uniform_at(io.seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
+                bool hit = false;
+                for (int m = 0; m < n_occ; ++m) {
+                    const float2 o2 = occ[m][lane];
+                    hit = hit || near(o2.x, o2.y, x, y, d2_min);
+                }
+                if (!hit) {
+                    won[wave][lane] = make_float2(x, y);
+                    atomicMin(&best[lane], k);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const int k = valid ? best[lane] : 0;
+            const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
+            if (unresolved) atomicAdd(&W[T], 1);
+            int km = unresolved ? 0 : k;  // one atomic per wave
+            for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
+            if (lane == 0 && km > 0) atomicMax(&W[i], km);
+            if (cov && !unresolved) {  // try k was drawn and accepted by wave k % kSpawnWaves
+                const float2 xy = won[k % kSpawnWaves][lane];
+                float* p = io.pos[i] + (long)b * io.pos_s0[i];
+                __hip_atomic_store(p, xy.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(p + io.pos_s1[i], xy.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // the positions and the maxima have landed before the completion (the sc1 hand-off of
+            // vmas_jit_ops.hpp: no agent fence, 1.7-6.5 us each)
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) atomicAdd(&done[32 * i], 1);
+        }
+        // (item_s is rewritten only after every wave has passed the barrier above)
     }
 }
 
@@ -371,12 +434,15 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     int cur = -1;
     VMAS_AUX_HIP(hipGetDevice(&cur));
     if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
-    static int max_blocks[64] = {0};
+    static int max_blocks[64] = {0}, resident[64] = {0};
     if (!max_blocks[device]) {
         hipDeviceProp_t prop;
         VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
         max_blocks[device] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / kUniformThreads);
         if (max_blocks[device] <= 0) return vmas_aux::fail(VMAS_E_HIP, "vmas_spawn_targets: device properties");
+        int per_cu = 0;
+        VMAS_AUX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spawn_targets, 64 * kSpawnWaves, 0));
+        resident[device] = prop.multiProcessorCount * std::max(per_cu, 1);
     }
     // torch's distribution-kernel grid and per-call philox increment on B elements (as
     // vmas_uniform_columns)
@@ -385,12 +451,11 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     DrawGrid g{kUniformThreads * gx, (unsigned long long)((B - 1) / (kUniformThreads * gx * 4) + 1) * 4};
     const float d2_min = spawn_d2_min(io->min_dist);
     hipStream_t st = (hipStream_t)stream;
-    VMAS_AUX_HIP(hipMemsetAsync(io->max_accepted, 0, sizeof(int32_t) * (io->n_targets + 1), st));
-    for (int i = 0; i < io->n_targets; ++i) {
-        hipLaunchKernelGGL(k_spawn_target, dim3((unsigned)((B + 63) / 64)), dim3(64 * kSpawnWaves), 0, st, *io, g, i,
-                           d2_min);
-        VMAS_AUX_HIP(hipGetLastError());
-    }
+    const int T = io->n_targets, n_groups = (int)((B + 63) / 64);
+    VMAS_AUX_HIP(hipMemsetAsync(io->max_accepted, 0, sizeof(int32_t) * VMAS_SPAWN_WORDS(T), st));
+    const long long grid = std::min<long long>(n_groups, resident[device]);
+    hipLaunchKernelGGL(k_spawn_targets, dim3((unsigned)grid), dim3(64 * kSpawnWaves), 0, st, *io, g, d2_min, n_groups);
+    VMAS_AUX_HIP(hipGetLastError());
     *increment = g.inc;
     return VMAS_OK;
 }
