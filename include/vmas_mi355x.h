@@ -407,10 +407,36 @@ typedef struct VmasSpawnTargetsIO {
     int32_t* max_accepted;                /* VMAS_SPAWN_WORDS(n_targets) device int32: [0, T) per-target max
                                              accepted try, [T] envs with no position found, [64] 1 when the
                                              launch's bounded wait timed out (the rest: its counters) */
+    struct VmasSpawnChannel* channel;     /* optional (vmas_spawn_channel_create): the launch reads seed and
+                                             offset from it at run time (a captured launch replays with the
+                                             generator state armed before each replay) and publishes its
+                                             maxima there; seed / offset above are then ignored */
 } VmasSpawnTargetsIO;
-#define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets))
+#define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets) + 32 * 32)
 #define VMAS_SPAWN_ERR_WORD 64
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream);
+/* Spawn channel: mapped pinned host words between the host and a (captured) vmas_spawn_targets
+ * launch, so that a graph-mode step keeps the respawn inside its one graph: the host arms the
+ * channel with the generator state before each replay, the launch reads it at run time, and its
+ * last workgroup publishes the per-target maxima, the unresolved count and the error word with one
+ * final system-scope sequence word; the host waits on that word once per step (after the rest of
+ * the step is queued) and advances the generator.  Replaces the graph-mode host hole (a graph
+ * break, a device->host read and a second graph launch in the middle of every discovery step). */
+typedef struct VmasSpawnChannel VmasSpawnChannel;
+int32_t vmas_spawn_channel_create(int32_t device, VmasSpawnChannel** out);
+int32_t vmas_spawn_channel_destroy(VmasSpawnChannel* ch);
+/* the generator state the next launch through the channel reads; seq != 0, new per launch */
+int32_t vmas_spawn_channel_arm(VmasSpawnChannel* ch, uint64_t seed, uint64_t offset, uint32_t seq);
+/* waits (host spin, checking `stream` for errors) for the launch armed with seq; words[0, T) the
+ * maxima, [T] unresolved envs, [T + 1] error word (nonzero: the launch's bounded wait timed out;
+ * the launch then publishes nothing and this returns VMAS_E_HIP once the stream has drained) */
+int32_t vmas_spawn_channel_wait(VmasSpawnChannel* ch, uint32_t seq, int32_t* words, int32_t n_targets, void* stream);
+
+/* Probe support: with VMAS_SPAWN_PROFILE=1 in the environment, vmas_spawn_targets records per
+ * (target, 64-env group) item six u64 words (s_memrealtime when claimed, wait over, occupied
+ * positions loaded, tries done, completion added; the workgroup); this copies up to n words of
+ * the last launch's record to host memory and returns the count (0: none recorded). */
+int32_t vmas_spawn_profile(uint64_t* out, int64_t n);
 
 /* ---- fused scenario programs (csrc/vmas_scenarios.hip) -------------------
  * One launch computes a benchmark scenario's per-step observation / reward / done tensor program

@@ -57,13 +57,22 @@ CASES = [
     ("balance", dict(n_agents=4), 10, "graph"),
     ("transport", dict(n_agents=4), None, "graph"),
     ("flocking", dict(n_agents=4), None, "graph"),     # scripted agent: range assert on the device
-    ("discovery", dict(n_agents=4), None, "graph"),    # spawn sampler: host holes between graphs
+    ("discovery", dict(n_agents=4), None, "graph"),    # spawn sampler: inside the graph (spawn channel)
+    ("discovery-hole", dict(n_agents=4), None, "graph"),  # the segmented form: a host hole, two graphs
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps,expect", CASES, ids=[c[0] for c in CASES])
-def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
+def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, substeps, expect):
+    if name == "discovery-hole":
+        from vectorizedmultiagentsimulator_amd.scenarios import discovery
+
+        monkeypatch.setattr(discovery, "DEFERRED_RESPAWN", False)
+        name = "discovery"
+        hole = True
+    else:
+        hole = False
     envs = []
     for graph in (False, True):
         saved = _rng_save()
@@ -101,9 +110,10 @@ def test_graph_replay_matches_eager_gpu(gpu_device, name, kw, substeps, expect):
     assert graph.graph_status == expect, graph.graph_reason
     if expect == "graph":
         assert graph._graph.replays >= 5
-    if name == "discovery":  # the 7 targets' respawn is one native call: one host hole, two graphs
+    if name == "discovery":  # the targets' respawn is one native call: inside the one graph with
+        # its host side after the replay (a spawn channel), or one host hole between two graphs
         n_holes, n_segments = len(graph._graph._holes), len(graph._graph._segments)
-        assert (n_holes, n_segments) == (1, 2)
+        assert (n_holes, n_segments, len(graph._graph._deferred)) == ((1, 2, 0) if hole else (0, 1, 1))
 
 
 def _twin_envs(gpu_device, name, **kw):
@@ -161,10 +171,14 @@ def test_scripted_action_assert_raised_from_step_gpu(gpu_device):
 
 
 @pytest.mark.gpu
-def test_failed_segmented_capture_restores_state_gpu(gpu_device):
+@pytest.mark.parametrize("deferred", [False, True], ids=["hole", "channel"])
+def test_failed_segmented_capture_restores_state_gpu(gpu_device, monkeypatch, deferred):
     """A capture that fails after host holes already ran the graphs before them (discovery's
     spawn sampler) restores the world and the generator, and the env continues eagerly with the
     eager twin's results."""
+    from vectorizedmultiagentsimulator_amd.scenarios import discovery
+
+    monkeypatch.setattr(discovery, "DEFERRED_RESPAWN", deferred)
     eager, graph = _twin_envs(gpu_device, "discovery", n_agents=4)
     orig = graph.scenario.info
 

@@ -20,7 +20,7 @@ if len(sys.argv) > 3:
     kw["n_agents"] = int(sys.argv[3])
 elif "n_agents" in preset:
     kw["n_agents"] = preset["n_agents"]
-env = make_env(name, num_envs=envs, device="cuda:0", seed=0, **kw)
+env = make_env(name, num_envs=envs, device="cuda:0", seed=0, graph_step=os.environ.get("GRAPH", "1") == "1", **kw)
 for _ in range(30):
     env.step(env.get_random_actions())
 torch.cuda.synchronize()

@@ -14,7 +14,8 @@ from pathlib import Path
 import numpy as np
 
 LIB_NAME = "libvmas_mi355x.so"
-LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+# VMAS_LIB_PATH: another build of the same sources (tools/asan_host.sh: the host-sanitized one)
+LIB_PATH = Path(os.environ.get("VMAS_LIB_PATH") or Path(__file__).resolve().parent / LIB_NAME)
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
@@ -58,6 +59,11 @@ EXPORTED_SYMBOLS = (
     "vmas_balance_outputs",
     "vmas_copy_spans",
     "vmas_spawn_targets",
+    "vmas_spawn_channel_create",
+    "vmas_spawn_channel_destroy",
+    "vmas_spawn_channel_arm",
+    "vmas_spawn_channel_wait",
+    "vmas_spawn_profile",
     "vmas_world_step_vjp",
     "vmas_distance_vjp",
     "vmas_cast_rays_vjp",
@@ -248,7 +254,7 @@ VMAS_SPAWN_ERR_WORD = 64
 
 
 def spawn_words(n_targets: int) -> int:  # VMAS_SPAWN_WORDS
-    return 96 + 32 * n_targets
+    return 96 + 32 * n_targets + 32 * 32
 
 
 class VmasSpawnTargetsIO(ctypes.Structure):
@@ -259,7 +265,7 @@ class VmasSpawnTargetsIO(ctypes.Structure):
         ("pos_s1", _i32 * VMAS_SPAWN_MAX_TARGETS),
         ("covered", _vp), ("cov_s0", _i32), ("cov_s1", _i32),
         ("min_dist", _f32), ("x_lo", _f32), ("x_hi", _f32), ("y_lo", _f32), ("y_hi", _f32), ("pad1", _f32),
-        ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp),
+        ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp), ("channel", _vp),
     ]
 
 
@@ -527,6 +533,16 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_world_step_vjp.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.vmas_spawn_targets.restype = _i32
     lib.vmas_spawn_targets.argtypes = [_i32, _vp, ctypes.POINTER(ctypes.c_uint64), _vp]
+    lib.vmas_spawn_channel_create.restype = _i32
+    lib.vmas_spawn_channel_create.argtypes = [_i32, ctypes.POINTER(_vp)]
+    lib.vmas_spawn_channel_destroy.restype = _i32
+    lib.vmas_spawn_channel_destroy.argtypes = [_vp]
+    lib.vmas_spawn_channel_arm.restype = _i32
+    lib.vmas_spawn_channel_arm.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+    lib.vmas_spawn_channel_wait.restype = _i32
+    lib.vmas_spawn_channel_wait.argtypes = [_vp, ctypes.c_uint32, ctypes.POINTER(_i32), _i32, _vp]
+    lib.vmas_spawn_profile.restype = _i32
+    lib.vmas_spawn_profile.argtypes = [_vp, ctypes.c_int64]
     lib.vmas_copy_spans.restype = _i32
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_stream_abort_capture.restype = _i32

@@ -163,8 +163,12 @@ struct DrawGrid {
 __device__ __forceinline__ uint4 philox10(uint4 c, uint2 k) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const unsigned int hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const unsigned int hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        // (the 64-bit products: one v_mad_u64_u32 each instead of v_mul_hi_u32 + v_mul_lo_u32, both
+        // quarter rate)
+        const unsigned long long p0 = (unsigned long long)c.x * 0xD2511F53u;
+        const unsigned long long p1 = (unsigned long long)c.z * 0xCD9E8D57u;
+        const unsigned int hi0 = (unsigned int)(p0 >> 32), lo0 = (unsigned int)p0;
+        const unsigned int hi1 = (unsigned int)(p1 >> 32), lo1 = (unsigned int)p1;
         c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
         k.x += 0x9E3779B9u;
         k.y += 0xBB67AE85u;
@@ -228,9 +232,11 @@ __device__ __forceinline__ bool near(float ox, float oy, float x, float y, float
 // word sat on one line and 1024 workgroups polled it).
 //
 // max_accepted words: [0, T) per-target max accepted try, [T] unresolved envs, [32] the claim
-// counter, [64] error (1: a wait timed out), [96 + 32 i] target i's done items.
-constexpr int kSpawnWaves = 8;
+// counter, [64] error (1: a wait timed out), [96 + 32 i] target i's done items, then
+// (k_spawn_targets_resident) kSpawnReplicas 64-bit words 128 bytes apart.
+constexpr int kSpawnWaves = 16;
 constexpr int kSpawnMaxOcc = 32 + VMAS_SPAWN_MAX_TARGETS - 1;  // agents + the other targets
+constexpr int kSpawnReplicas = 32;  // (k_spawn_targets_resident) the published tries, one line each
 constexpr unsigned long long kSpawnWaitTicks = 100000000ull;   // s_memrealtime (100 MHz): 1 s
 
 template <typename T>
@@ -238,11 +244,49 @@ __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Spawn channel (vmas_spawn_channel_*): mapped pinned host words.  in: [0] seed, [1] offset, [2] seq.
+// out: int32 [0, 16) maxima, [16] unresolved, [17] error; u64 word 12 (byte 96): seq << 32 | 1,
+// stored last.
+constexpr int kChanOutSeqWord = 12;
+struct ChanArgs {
+    const uint64_t* in;  // (device pointer of the mapped host words; null: no channel)
+    uint64_t* out;
+};
+
+// Generator state of a launch: the channel's (read at run time) or the arguments'.
+__device__ __forceinline__ void launch_rng(const VmasSpawnTargetsIO& io, const ChanArgs& ch, unsigned long long* seed,
+                                           unsigned long long* off, unsigned long long* seq) {
+    if (ch.in) {
+        *seed = __hip_atomic_load(ch.in + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *off = __hip_atomic_load(ch.in + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *seq = __hip_atomic_load(ch.in + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        *seed = io.seed;
+        *off = io.offset;
+        *seq = 0;
+    }
+}
+
+// (the last workgroup done with the last target, one wave) the launch's words to the channel: every
+// maximum and unresolved count has landed (each workgroup's before its completion)
+__device__ __forceinline__ void publish_channel(const ChanArgs& ch, const int32_t* W, int T, unsigned long long seq) {
+    const int lane = threadIdx.x & 63;
+    int32_t* o = reinterpret_cast<int32_t*>(ch.out);
+    if (lane < T) __hip_atomic_store(o + lane, ld_agent(W + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 16) __hip_atomic_store(o + 16, ld_agent(W + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 17) __hip_atomic_store(o + 17, ld_agent(W + 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0)
+        __hip_atomic_store(ch.out + kChanOutSeqWord, (seq << 32) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
-                                                                  int n_groups) {
+                                                                  int n_groups, unsigned long long* prof,
+                                                                  ChanArgs ch) {
     __shared__ int best[64];
     __shared__ int item_s;
-    __shared__ unsigned long long off_s;
+    __shared__ int abort_s;
+    __shared__ unsigned long long off_s, t_claim_s, rng_s[3];
     __shared__ float2 occ[kSpawnMaxOcc][64];  // the occupied positions of the item's 64 envs
     __shared__ float2 won[kSpawnWaves][64];   // each wave's accepted position (at most one per lane)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -253,38 +297,13 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
     int32_t* const done = W + 96;  // target i's counter at done[32 * i]
     const unsigned long long per_try = 2ull * g.inc;
     const int n_occ = io.n_agents + T - 1;
-    // (thread 0) the claim of the coming item, taken one item ahead so that the claim's round trip
-    // overlaps the current item; still deadlock-free: the smallest unfinished item is always some
-    // workgroup's current one, and it waits only for smaller items
-    int next = threadIdx.x == 0 ? atomicAdd(claim, 1) : 0;
+    if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);  // (read before the first barrier)
+    // (Claiming one item ahead, to overlap the claim's round trip, made it slower: a workgroup
+    // could hold two items of one target, serialising them -- 137 -> 218 us per call.)
     for (;;) {
         if (threadIdx.x == 0) {
-            int it = next;
-            if (it < n_items) next = atomicAdd(claim, 1);
-            if (it < n_items && it >= n_groups) {  // wait for every item of the previous target
-                const int* dp = done + 32 * (it / n_groups - 1);
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while (ld_agent(dp) < n_groups) {
-                    if (ld_agent(err) || __builtin_amdgcn_s_memrealtime() - t0 > kSpawnWaitTicks) {
-                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        it = n_items;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-            }
-            item_s = it;
-            if (it < n_items) {  // target i's generator offset, from the earlier targets' maxima
-                const int i = it / n_groups;
-                int mv[VMAS_SPAWN_MAX_TARGETS];
-#pragma unroll
-                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j) mv[j] = j < i ? ld_agent(W + j) : 0;  // (one round trip)
-                unsigned long long off = io.offset;
-#pragma unroll
-                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j)
-                    if (j < i) off += (unsigned long long)(mv[j] == 0 ? 1 : mv[j] + 2) * per_try;
-                off_s = off;
-            }
+            item_s = atomicAdd(claim, 1);
+            if (prof) t_claim_s = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
         const int it = item_s;
@@ -293,28 +312,68 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
         const int b = grp * 64 + lane;
         const bool valid = b < io.batch;
         const int bb = valid ? b : io.batch - 1;
+        // what does not depend on the earlier targets, loaded before the wait: the covered flag and
+        // the agents' positions
         const bool cov = wave == 0 && valid && io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1];
-        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
-        const unsigned long long off = off_s;
-        // occupied: the agents, then every other target (earlier ones already moved, by items that
-        // may have run on another XCD: loaded with agent-scope atomics, sc1, as they were stored)
-        for (int m = wave; m < n_occ; m += kSpawnWaves) {
-            if (m < io.n_agents) {
-                const float* p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
-                occ[m][lane] = make_float2(p[0], p[io.ag_s2]);
-            } else {
-                const int j = m - io.n_agents + (m - io.n_agents >= i ? 1 : 0);
-                const float* p = io.pos[j] + (long)bb * io.pos_s0[j];
-                occ[m][lane] = make_float2(ld_agent(p), ld_agent(p + io.pos_s1[j]));
+        for (int m = wave; m < io.n_agents; m += kSpawnWaves) {
+            const float* p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
+            occ[m][lane] = make_float2(p[0], p[io.ag_s2]);
+        }
+        if (threadIdx.x == 0) {
+            bool ok = true;
+            if (it >= n_groups) {  // wait for every item of the previous target
+                const int* dp = done + 32 * (i - 1);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (ld_agent(dp) < n_groups) {
+                    if (ld_agent(err) || __builtin_amdgcn_s_memrealtime() - t0 > kSpawnWaitTicks) {
+                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            abort_s = ok ? 0 : 1;
+            if (prof) {
+                prof[(long)it * 6 + 0] = t_claim_s;
+                prof[(long)it * 6 + 1] = __builtin_amdgcn_s_memrealtime();
+                prof[(long)it * 6 + 5] = blockIdx.x;
             }
         }
         __syncthreads();
-        if (valid) {
-            for (int k = wave; k < VMAS_SPAWN_MAX_TRIES; k += kSpawnWaves) {
-                if (k >= __hip_atomic_load(&best[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        if (abort_s) return;
+        if (threadIdx.x == 0) {  // target i's generator offset, from the earlier targets' maxima
+            int mv[VMAS_SPAWN_MAX_TARGETS];
+#pragma unroll
+            for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j) mv[j] = j < i ? ld_agent(W + j) : 0;  // (one round trip)
+            unsigned long long off = rng_s[1];
+#pragma unroll
+            for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j)
+                if (j < i) off += (unsigned long long)(mv[j] == 0 ? 1 : mv[j] + 2) * per_try;
+            off_s = off;
+        }
+        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+        // the other targets (earlier ones already moved, by items that may have run on another XCD:
+        // loaded with agent-scope atomics, sc1, as they were stored), with the maxima's round trip
+        for (int m = io.n_agents + wave; m < n_occ; m += kSpawnWaves) {
+            const int j = m - io.n_agents + (m - io.n_agents >= i ? 1 : 0);
+            const float* p = io.pos[j] + (long)bb * io.pos_s0[j];
+            occ[m][lane] = make_float2(ld_agent(p), ld_agent(p + io.pos_s1[j]));
+        }
+        __syncthreads();
+        const unsigned long long off = off_s, seed = rng_s[0];
+        if (prof && threadIdx.x == 0) prof[(long)it * 6 + 2] = __builtin_amdgcn_s_memrealtime();
+        // rounds of kSpawnWaves tries, wave w drawing try base + w for the lanes still open; the
+        // workgroup agrees after each round whether another is needed (one round unless an env
+        // rejects 16 tries in a row).  (Without the rounds' barrier a wave whose try was rejected
+        // went on to its next try before seeing another wave's earlier acceptance: 8 us per item
+        // instead of one round's ~3.)
+        for (int base = 0; base < VMAS_SPAWN_MAX_TRIES; base += kSpawnWaves) {
+            const int k = base + wave;
+            if (valid && best[lane] == VMAS_SPAWN_MAX_TRIES) {
                 const unsigned long long o = off + (unsigned long long)k * per_try;
-                const float x = uniform_at(io.seed, o, g, b, io.x_lo, io.x_hi, io.mode);
-                const float y = uniform_at(io.seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
+                const float x = uniform_at(seed, o, g, b, io.x_lo, io.x_hi, io.mode);
+                const float y = uniform_at(seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
                 bool hit = false;
                 for (int m = 0; m < n_occ; ++m) {
                     const float2 o2 = occ[m][lane];
@@ -323,11 +382,11 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
                 if (!hit) {
                     won[wave][lane] = make_float2(x, y);
                     atomicMin(&best[lane], k);
-                    break;
                 }
             }
+            if (!__syncthreads_or(valid && best[lane] == VMAS_SPAWN_MAX_TRIES)) break;
         }
-        __syncthreads();
+        if (prof && threadIdx.x == 0) prof[(long)it * 6 + 3] = __builtin_amdgcn_s_memrealtime();
         if (wave == 0) {
             const int k = valid ? best[lane] : 0;
             const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
@@ -344,9 +403,148 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
             // the positions and the maxima have landed before the completion (the sc1 hand-off of
             // vmas_jit_ops.hpp: no agent fence, 1.7-6.5 us each)
             __builtin_amdgcn_s_waitcnt(0);
-            if (lane == 0) atomicAdd(&done[32 * i], 1);
+            int last = 0;
+            if (lane == 0) {
+                last = atomicAdd(&done[32 * i], 1) == n_groups - 1;
+                if (prof) prof[(long)it * 6 + 4] = __builtin_amdgcn_s_memrealtime();
+            }
+            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2]);
         }
         // (item_s is rewritten only after every wave has passed the barrier above)
+    }
+}
+
+// The same loop with a workgroup per 64-env group for every target (grid = the groups, used when
+// they fit the device at once: the launch then needs every workgroup resident, which holds on an
+// otherwise idle device -- stream order keeps the step's other kernels out -- and the bounded
+// wait turns anything else into the error word rather than a hang).  The group's occupied
+// positions stay in LDS from target to target (its own new positions included: no other
+// workgroup reads them), so the only hand-off between workgroups per target is the maxima: the
+// completion count, then one load of the maxima.  Per target ~6 us instead of the claimed
+// items' ~11 (a claim round trip and the sc1 position loads on the critical path).
+__global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(VmasSpawnTargetsIO io, DrawGrid g,
+                                                                           float d2_min, unsigned long long* prof,
+                                                                           ChanArgs ch) {
+    __shared__ int best[64];
+    __shared__ int abort_s;
+    __shared__ unsigned long long off_s, rng_s[3];
+    __shared__ float2 occ[32 + VMAS_SPAWN_MAX_TARGETS][64];  // agents, then every target
+    __shared__ float2 won[kSpawnWaves][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int T = io.n_targets, A = io.n_agents, n_groups = (int)gridDim.x;
+    int32_t* const W = io.max_accepted;
+    int32_t* const err = W + 64;
+    int32_t* const done = W + 96;
+    unsigned long long* const rep = reinterpret_cast<unsigned long long*>(W + 96 + 32 * T);  // 128-byte lines
+    const unsigned long long per_try = 2ull * g.inc;
+    const int b = (int)blockIdx.x * 64 + lane;
+    const bool valid = b < io.batch;
+    const int bb = valid ? b : io.batch - 1;
+    for (int m = wave; m < A + T; m += kSpawnWaves) {
+        const float* p;
+        int s1;
+        if (m < A) {
+            p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
+            s1 = io.ag_s2;
+        } else {
+            p = io.pos[m - A] + (long)bb * io.pos_s0[m - A];
+            s1 = io.pos_s1[m - A];
+        }
+        occ[m][lane] = make_float2(p[0], p[s1]);
+    }
+    if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);  // (read before the first barrier)
+    uint32_t covm = 0u;  // (wave 0) the lane's covered targets
+    if (wave == 0 && valid)
+        for (int i = 0; i < T; ++i) covm |= io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1] ? (1u << i) : 0u;
+    for (int i = 0; i < T; ++i) {
+        const long it = (long)i * n_groups + blockIdx.x;
+        if (threadIdx.x == 0) {
+            const unsigned long long t_claim = __builtin_amdgcn_s_memrealtime();
+            bool ok = true;
+            unsigned long long tries = 0;  // tries the earlier targets consumed
+            if (i > 0) {  // the last group done with target i - 1 publishes (i, tries) in our replica
+                const unsigned long long* rp = rep + 16 * (blockIdx.x % kSpawnReplicas);
+                unsigned long long v;
+                while (((v = ld_agent(rp)) >> 32) != (unsigned long long)i) {
+                    if (ld_agent(err) || __builtin_amdgcn_s_memrealtime() - t_claim > kSpawnWaitTicks) {
+                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+                tries = v & 0xFFFFFFFFull;
+            }
+            abort_s = ok ? 0 : 1;
+            if (prof) {
+                prof[it * 6 + 0] = t_claim;
+                prof[it * 6 + 1] = __builtin_amdgcn_s_memrealtime();
+                prof[it * 6 + 5] = blockIdx.x;
+            }
+            off_s = rng_s[1] + tries * per_try;
+        }
+        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+        __syncthreads();
+        if (abort_s) return;
+        if (prof && threadIdx.x == 0) prof[it * 6 + 2] = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long off = off_s, seed = rng_s[0];
+        for (int base = 0; base < VMAS_SPAWN_MAX_TRIES; base += kSpawnWaves) {  // (as k_spawn_targets)
+            const int k = base + wave;
+            if (valid && best[lane] == VMAS_SPAWN_MAX_TRIES) {
+                const unsigned long long o = off + (unsigned long long)k * per_try;
+                const float x = uniform_at(seed, o, g, b, io.x_lo, io.x_hi, io.mode);
+                const float y = uniform_at(seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
+                bool hit = false;
+                for (int m = 0; m < A + T; ++m) {
+                    if (m == A + i) continue;  // (the target itself)
+                    const float2 o2 = occ[m][lane];
+                    hit = hit || near(o2.x, o2.y, x, y, d2_min);
+                }
+                if (!hit) {
+                    won[wave][lane] = make_float2(x, y);
+                    atomicMin(&best[lane], k);
+                }
+            }
+            if (!__syncthreads_or(valid && best[lane] == VMAS_SPAWN_MAX_TRIES)) break;
+        }
+        if (prof && threadIdx.x == 0) prof[it * 6 + 3] = __builtin_amdgcn_s_memrealtime();
+        if (wave == 0) {
+            const int k = valid ? best[lane] : 0;
+            const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
+            if (unresolved) atomicAdd(&W[T], 1);
+            int km = unresolved ? 0 : k;
+            for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
+            if (lane == 0 && km > 0) atomicMax(&W[i], km);
+            if (((covm >> i) & 1u) && !unresolved) {
+                const float2 xy = won[k % kSpawnWaves][lane];
+                float* p = io.pos[i] + (long)b * io.pos_s0[i];
+                p[0] = xy.x;
+                p[io.pos_s1[i]] = xy.y;
+                occ[A + i][lane] = xy;  // (read by the next target's tries, after its barrier)
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // the maxima have landed before the completion
+            int last = 0;
+            if (lane == 0) {
+                last = atomicAdd(&done[32 * i], 1) == n_groups - 1;
+                if (prof) prof[it * 6 + 4] = __builtin_amdgcn_s_memrealtime();
+            }
+            // the last group done: every maximum has landed (each group's before its completion);
+            // it publishes the tries consumed so far to the replicas the others poll (kSpawnReplicas
+            // lines: one line polled by every workgroup took ~6 us to see the count complete)
+            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2]);
+            if (__shfl(last, 0) && i + 1 < T) {
+                int mv[VMAS_SPAWN_MAX_TARGETS];
+#pragma unroll
+                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j) mv[j] = j <= i ? ld_agent(W + j) : 0;
+                unsigned long long tries = 0;
+#pragma unroll
+                for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j)
+                    if (j <= i) tries += (unsigned long long)(mv[j] == 0 ? 1 : mv[j] + 2);
+                if (lane < kSpawnReplicas)
+                    __hip_atomic_store(rep + 16 * lane, ((unsigned long long)(i + 1) << 32) | tries, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -366,6 +564,21 @@ float spawn_d2_min(float min_dist) {
     memcpy(&r, &lo, 4);
     return r;
 }
+
+}  // namespace
+
+struct VmasSpawnChannel {
+    int device = 0;
+    uint64_t* h_in = nullptr;  // mapped pinned: seed, offset, seq
+    uint64_t* d_in = nullptr;
+    uint64_t* h_out = nullptr;  // mapped pinned: 16 maxima + unresolved + error (int32), seq word (u64 12)
+    uint64_t* d_out = nullptr;
+};
+
+namespace {
+
+unsigned long long* g_spawn_prof = nullptr;  // (VMAS_SPAWN_PROFILE) the last launch's item stamps
+size_t g_spawn_prof_n = 0;
 
 struct DevScratch {
     int32_t* d_out = nullptr;
@@ -424,6 +637,68 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
     return VMAS_OK;
 }
 
+int32_t vmas_spawn_channel_create(int32_t device, VmasSpawnChannel** out) {
+    if (!out || device < 0 || device >= 64) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_channel_create: bad arguments");
+    *out = nullptr;
+    int cur = -1;
+    VMAS_AUX_HIP(hipGetDevice(&cur));
+    if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
+    VmasSpawnChannel* ch = new VmasSpawnChannel();
+    ch->device = device;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipHostMalloc((void**)&ch->h_in, 4 * sizeof(uint64_t), fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ch->d_in, ch->h_in, 0);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ch->h_out, 16 * sizeof(uint64_t), fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&ch->d_out, ch->h_out, 0);
+    if (cur != device) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        vmas_spawn_channel_destroy(ch);
+        return vmas_aux::fail(VMAS_E_HIP, "vmas_spawn_channel_create: %s", hipGetErrorString(e));
+    }
+    for (int i = 0; i < 4; ++i) ch->h_in[i] = 0;
+    for (int i = 0; i < 16; ++i) ch->h_out[i] = 0;
+    *out = ch;
+    return VMAS_OK;
+}
+
+int32_t vmas_spawn_channel_destroy(VmasSpawnChannel* ch) {
+    if (!ch) return VMAS_OK;
+    if (ch->h_in) (void)hipHostFree(ch->h_in);
+    if (ch->h_out) (void)hipHostFree(ch->h_out);
+    delete ch;
+    return VMAS_OK;
+}
+
+int32_t vmas_spawn_channel_arm(VmasSpawnChannel* ch, uint64_t seed, uint64_t offset, uint32_t seq) {
+    if (!ch || seq == 0u) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_channel_arm: bad arguments");
+    __atomic_store_n(&ch->h_in[0], seed, __ATOMIC_RELAXED);
+    __atomic_store_n(&ch->h_in[1], offset, __ATOMIC_RELAXED);
+    __atomic_store_n(&ch->h_in[2], (uint64_t)seq, __ATOMIC_RELEASE);
+    return VMAS_OK;
+}
+
+int32_t vmas_spawn_channel_wait(VmasSpawnChannel* ch, uint32_t seq, int32_t* words, int32_t n_targets, void* stream) {
+    if (!ch || !words || seq == 0u || n_targets < 1 || n_targets > VMAS_SPAWN_MAX_TARGETS)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_channel_wait: bad arguments");
+    uint64_t v = 0;
+    if (int32_t rc = vmas_aux::wait_host_word64(ch->h_out + kChanOutSeqWord, seq, &v, (hipStream_t)stream)) return rc;
+    const int32_t* o = reinterpret_cast<const int32_t*>(ch->h_out);
+    for (int i = 0; i < n_targets; ++i) words[i] = __atomic_load_n(o + i, __ATOMIC_RELAXED);
+    words[n_targets] = __atomic_load_n(o + 16, __ATOMIC_RELAXED);
+    words[n_targets + 1] = __atomic_load_n(o + 17, __ATOMIC_RELAXED);
+    return VMAS_OK;
+}
+
+// (probe) copy the last profiled vmas_spawn_targets launch's item stamps (n words at most)
+int32_t vmas_spawn_profile(uint64_t* out, int64_t n) {
+    if (!g_spawn_prof || !out || n <= 0) return 0;
+    const size_t k = std::min<size_t>((size_t)n, g_spawn_prof_n);
+    VMAS_AUX_HIP(hipDeviceSynchronize());
+    VMAS_AUX_HIP(hipMemcpy(out, g_spawn_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return (int32_t)k;
+}
+
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream) {
     if (!io || !increment || device < 0 || device >= 64 || io->batch <= 0 || io->n_agents < 0 || io->n_agents > 32 ||
         io->n_targets < 1 || io->n_targets > VMAS_SPAWN_MAX_TARGETS || !io->covered || !io->max_accepted ||
@@ -434,7 +709,7 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     int cur = -1;
     VMAS_AUX_HIP(hipGetDevice(&cur));
     if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
-    static int max_blocks[64] = {0}, resident[64] = {0};
+    static int max_blocks[64] = {0}, resident[64] = {0}, resident_static[64] = {0};
     if (!max_blocks[device]) {
         hipDeviceProp_t prop;
         VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
@@ -443,6 +718,10 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
         int per_cu = 0;
         VMAS_AUX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spawn_targets, 64 * kSpawnWaves, 0));
         resident[device] = prop.multiProcessorCount * std::max(per_cu, 1);
+        per_cu = 0;
+        VMAS_AUX_HIP(
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spawn_targets_resident, 64 * kSpawnWaves, 0));
+        resident_static[device] = prop.multiProcessorCount * per_cu;
     }
     // torch's distribution-kernel grid and per-call philox increment on B elements (as
     // vmas_uniform_columns)
@@ -453,8 +732,33 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     hipStream_t st = (hipStream_t)stream;
     const int T = io->n_targets, n_groups = (int)((B + 63) / 64);
     VMAS_AUX_HIP(hipMemsetAsync(io->max_accepted, 0, sizeof(int32_t) * VMAS_SPAWN_WORDS(T), st));
+    const bool group_resident = n_groups <= resident_static[device] && !getenv("VMAS_SPAWN_CLAIMED");
     const long long grid = std::min<long long>(n_groups, resident[device]);
-    hipLaunchKernelGGL(k_spawn_targets, dim3((unsigned)grid), dim3(64 * kSpawnWaves), 0, st, *io, g, d2_min, n_groups);
+    // VMAS_SPAWN_PROFILE=1 (a probe's knob): per item s_memrealtime stamps [claimed, wait over,
+    // occupied loaded, tries done, completion added, workgroup] into g_spawn_prof (vmas_spawn_profile)
+    unsigned long long* prof = nullptr;
+    static const bool want_prof = getenv("VMAS_SPAWN_PROFILE") && getenv("VMAS_SPAWN_PROFILE")[0] == '1';
+    if (want_prof) {
+        const size_t need = (size_t)T * n_groups * 6;
+        if (g_spawn_prof_n < need) {
+            if (g_spawn_prof) (void)hipFree(g_spawn_prof);
+            VMAS_AUX_HIP(hipMalloc((void**)&g_spawn_prof, need * sizeof(unsigned long long)));
+            g_spawn_prof_n = need;
+        }
+        prof = g_spawn_prof;
+    }
+    ChanArgs ch{nullptr, nullptr};
+    if (io->channel) {
+        if (io->channel->device != device) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_targets: channel of another device");
+        ch.in = io->channel->d_in;
+        ch.out = io->channel->d_out;
+    }
+    if (group_resident)
+        hipLaunchKernelGGL(k_spawn_targets_resident, dim3((unsigned)n_groups), dim3(64 * kSpawnWaves), 0, st, *io, g,
+                           d2_min, prof, ch);
+    else
+        hipLaunchKernelGGL(k_spawn_targets, dim3((unsigned)grid), dim3(64 * kSpawnWaves), 0, st, *io, g, d2_min,
+                           n_groups, prof, ch);
     VMAS_AUX_HIP(hipGetLastError());
     *increment = g.inc;
     return VMAS_OK;

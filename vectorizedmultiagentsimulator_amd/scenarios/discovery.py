@@ -7,6 +7,7 @@ Each agent carries a target LIDAR (``n_lidar_rays_entities`` rays) and, with
 ``use_agent_lidar=True``, a second LIDAR that sees agents (``n_lidar_rays_agents`` rays).
 """
 import ctypes
+import os
 from typing import Dict
 
 import torch
@@ -177,8 +178,11 @@ class Scenario(BaseScenario):
             return False
         args = (ap, self.covered_targets, float(self._min_dist_between_entities), float(w.x_semidim),
                 float(w.y_semidim), *[t.state.pos for t in self._targets])
+        dsink = getattr(w, "_deferred_sink", None) if DEFERRED_RESPAWN else None
         sink = getattr(w, "_hole_sink", None)
-        if sink is not None:  # a graph-mode capture: the host read stays a hole of the step
+        if dsink is not None:  # a graph-mode capture: the launch stays inside the step's graph
+            dsink(DeferredRespawn(args))
+        elif sink is not None:  # (the segmented form: the host read is a hole of the step)
             sink(respawn_targets_native, args)
         else:
             respawn_targets_native(*args)
@@ -440,14 +444,9 @@ class HeuristicPolicy(BaseHeuristicPolicy):
         return torch.clamp((des_pos - current_pos) * 10, min=-u_range, max=u_range)
 
 
-def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
-                           *target_pos: Tensor, out: Tensor = None) -> Tensor:
-    """Discovery's target respawn loop (_respawn) through vmas_spawn_targets: target i moves to
-    find_random_pos_for_entity(occupied = agents + the other targets) where covered[:, i].
-    Returns the device int32 words of the call (N.spawn_words: per-target max accepted tries, the
-    count of envs that found no position, the launch's counters) after reading them once and
-    advancing the device generator by the tries the reference loop consumes.  ``out``: the
-    tensor of a graph-mode hole's replay."""
+def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
+                  target_pos, mx: Tensor, channel=None):
+    """One vmas_spawn_targets launch on the current stream; returns (io, philox increment)."""
     import numpy as np
 
     from vectorizedmultiagentsimulator_amd.simulator.environment import _uniform
@@ -457,7 +456,6 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     B, A = agents_pos.shape[0], agents_pos.shape[1]
     T = len(target_pos)
     gen = torch.cuda.default_generators[idx]
-    mx = out if out is not None else torch.empty(N.spawn_words(T), dtype=torch.int32, device=dev)
     f32 = lambda v: float(np.float32(v))  # noqa: E731 -- torch casts the bounds to float
     io = N.VmasSpawnTargetsIO()
     io.batch, io.n_agents, io.n_targets, io.mode = B, A, T, _uniform.mode(dev, B)
@@ -471,22 +469,117 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     io.cov_s0, io.cov_s1 = cov.stride()
     io.min_dist = float(torch.tensor(min_dist, dtype=torch.float32))
     io.x_lo, io.x_hi, io.y_lo, io.y_hi = f32(-x_semidim), f32(x_semidim), f32(-y_semidim), f32(y_semidim)
-    io.seed, io.offset = gen.initial_seed(), gen.get_offset()
+    if channel is None:  # (through a channel the launch reads them at run time)
+        io.seed, io.offset = gen.initial_seed(), gen.get_offset()
     io.max_accepted = mx.data_ptr()
+    io.channel = channel
     inc = ctypes.c_uint64(0)
     N.check_aux(N.load_library().vmas_spawn_targets(idx, ctypes.byref(io), ctypes.byref(inc),
                                                       ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
                 "vmas_spawn_targets")
-    h = mx.tolist()  # the step's one host wait
-    if h[N.VMAS_SPAWN_ERR_WORD]:
-        raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
+    return io, inc.value
+
+
+def _spawn_consumed(h, T: int, offset: int, inc: int, gen) -> None:
+    """Advance the generator by the tries the reference loop consumes (h: the launch's maxima,
+    unresolved count); raise where an env found no position."""
     # the generator is left where the tries it consumed put it, also when an env found no free
     # position (the reference warns and keeps trying forever, utils.py:285-317; here the kernels
     # stop after VMAS_SPAWN_MAX_TRIES tries and the call raises, with the targets of the resolved
     # envs moved and the generator consistent with the tries drawn)
-    gen.set_offset(io.offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc.value)
+    gen.set_offset(offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc)
     if h[T]:
         raise RuntimeError(
             f"find_random_pos_for_entity: {h[T]} env(s) found no free position within {N.VMAS_SPAWN_MAX_TRIES} "
             "tries; make sure the bounds or the min_dist_between_entities are not too tight to fit all entities")
+
+
+# Graph mode: the respawn captured inside the step's graph through a spawn channel (DeferredRespawn)
+# instead of a host hole splitting the step in two graphs (VMAS_GRAPH_DEFERRED_SPAWN=0: the hole)
+DEFERRED_RESPAWN = os.environ.get("VMAS_GRAPH_DEFERRED_SPAWN", "1") != "0"
+
+
+class DeferredRespawn:
+    """The respawn of a graph-mode step, kept inside the step's one graph.  At capture, one
+    vmas_spawn_targets launch through a spawn channel (mapped host words): the launch reads the
+    generator's seed and offset at run time and publishes its per-target maxima there.  Each replay:
+    ``arm`` (before the launch) writes the generator state into the channel; ``finish`` (after the
+    step's other host work is queued) waits for the maxima and advances the generator exactly as
+    the eager call does -- the step's one host wait, with the rest of the step still running on the
+    device, instead of a mid-step graph break and a second graph launch (StepGraph._deferred)."""
+
+    def __init__(self, args):
+        self.args = args
+        dev = args[0].device
+        self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.T = len(args) - 5
+        lib = N.load_library()
+        ch = ctypes.c_void_p()
+        N.check_aux(lib.vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
+        self.ch = ch
+        self.seq = 0
+        self.pending = None
+        self.inc = 0
+        self.offset = 0
+        self.mx = None
+
+    def capture(self):
+        a = self.args
+        self.mx = torch.empty(N.spawn_words(self.T), dtype=torch.int32, device=a[0].device)
+        _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch)
+
+    def arm(self):
+        if self.pending is not None:  # (an earlier replay never finished: drain it first)
+            self.finish(apply=False)
+        gen = torch.cuda.default_generators[self.idx]
+        self.seq = self.seq % 0xFFFFFFFF + 1
+        self.offset = gen.get_offset()
+        N.check_aux(N.load_library().vmas_spawn_channel_arm(self.ch, gen.initial_seed(), self.offset, self.seq),
+                    "vmas_spawn_channel_arm")
+        self.pending = self.seq
+
+    def finish(self, apply: bool = True):
+        if self.pending is None:
+            return
+        seq, self.pending = self.pending, None
+        words = (ctypes.c_int32 * (self.T + 2))()
+        rc = N.load_library().vmas_spawn_channel_wait(self.ch, seq, words, self.T,
+                                                      ctypes.c_void_p(torch.cuda.current_stream(self.idx).cuda_stream))
+        if rc < 0:
+            torch.cuda.synchronize(self.idx)
+            if self.mx is not None and int(self.mx[N.VMAS_SPAWN_ERR_WORD].item()):
+                raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
+            N.check_aux(rc, "vmas_spawn_channel_wait")
+        h = list(words)
+        if h[self.T + 1]:
+            raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
+        if apply:
+            _spawn_consumed(h, self.T, self.offset, self.inc, torch.cuda.default_generators[self.idx])
+
+    def __del__(self):
+        try:
+            if self.pending is not None:
+                torch.cuda.synchronize(self.idx)
+            N.load_library().vmas_spawn_channel_destroy(self.ch)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
+                           *target_pos: Tensor, out: Tensor = None) -> Tensor:
+    """Discovery's target respawn loop (_respawn) through vmas_spawn_targets: target i moves to
+    find_random_pos_for_entity(occupied = agents + the other targets) where covered[:, i].
+    Returns the device int32 words of the call (N.spawn_words: per-target max accepted tries, the
+    count of envs that found no position, the launch's counters) after reading them once and
+    advancing the device generator by the tries the reference loop consumes.  ``out``: the
+    tensor of a graph-mode hole's replay."""
+    dev = agents_pos.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    T = len(target_pos)
+    mx = out if out is not None else torch.empty(N.spawn_words(T), dtype=torch.int32, device=dev)
+    io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx)
+    h = mx[:N.VMAS_SPAWN_ERR_WORD + 1].tolist()  # the step's one host wait (maxima, unresolved, error)
+    if h[N.VMAS_SPAWN_ERR_WORD]:
+        raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
+    _spawn_consumed(h, T, io.offset, inc, torch.cuda.default_generators[idx])
     return mx

@@ -915,6 +915,7 @@ class World(TorchVectorizedObject):
         # graph mode's sink for host code that waits on the device inside the step (the spawn
         # sampler; None: run it inline)
         self._hole_sink = None
+        self._deferred_sink = None  # (graph capture) launches whose host side runs after each replay
         self._collidable_pairs = [
             {Sphere, Sphere},
             {Sphere, Box},

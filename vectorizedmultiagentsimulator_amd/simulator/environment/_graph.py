@@ -373,6 +373,9 @@ class StepGraph:
         self._executed = None  # outputs of a capture step that already ran (segmented capture)
         self._carry_ys: List[Tensor] = []  # the Y tensors as bound (version counters)
         self._post: Optional[dict] = None  # what the last post-replay launch covered (_post_replay)
+        # launches captured with their host side deferred (world._deferred_sink: discovery's
+        # DeferredRespawn): armed before every replay, finished after its host work is queued
+        self._deferred: List[Any] = []
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -511,7 +514,19 @@ class StepGraph:
                         + ", ".join(f"{names.get(i, '?')}.{k}" for i, k in changed[:4]))[:300]
         return out
 
+    def _finish_deferred(self, apply: bool = True):
+        err = None
+        for d in self._deferred:
+            try:
+                d.finish(apply)
+            except Exception as ex:  # noqa: BLE001 -- drain every channel, then raise the first
+                err = err or ex
+        if err is not None:
+            raise err
+
     def drop(self, why: str):
+        self._finish_deferred(apply=False)
+        self._deferred = []
         self.graph = None
         self._raw_exec = None
         self._segments, self._holes = [], []
@@ -556,10 +571,17 @@ class StepGraph:
         # before the hole for real, so a failure after that has state to restore
         contents = [(t, t.clone()) for t, _ in versions.values()]
         segs = _Segments(side)
+        deferred: List[Any] = []
+
+        def deferred_sink(d):  # captured here; armed / finished around each replay
+            d.capture()
+            deferred.append(d)
+
         try:
             env.world._assert_sink = asserts.capture_sink
             env.world._assert_range_sink = asserts.capture_range
             env.world._hole_sink = segs.hole
+            env.world._deferred_sink = deferred_sink
             torch.cuda.synchronize(dev)
             with torch.cuda.stream(side), consts:
                 segs.begin()
@@ -607,7 +629,9 @@ class StepGraph:
             env.world._assert_sink = None
             env.world._assert_range_sink = None
             env.world._hole_sink = None
+            env.world._deferred_sink = None
         del contents
+        self._deferred = deferred
         self.graph = g
         self._segments, self._holes = segs.graphs, segs.holes
         self._raw_exec = None
@@ -692,6 +716,8 @@ class StepGraph:
         that captured random ops read); if it did not advance the device generator, the graph
         draws no random numbers and later replays launch the instantiated graph directly
         (vmas_graph_launch), without the prologue's two fill kernels."""
+        for d in self._deferred:  # the generator state the captured launches read
+            d.arm()
         if self._holes:  # segmented step: graph, host hole, graph, ... (torch replays)
             for i, seg in enumerate(self._segments):
                 seg.replay()
@@ -727,9 +753,12 @@ class StepGraph:
             try:
                 self._asserts.after_replay(self.env.device)
             except AssertionError:
+                self._finish_deferred(apply=False)
                 self._rollback(rng, restore_actions=False)
                 raise
-        return self._post_replay()
+        out = self._post_replay()
+        self._finish_deferred()
+        return out
 
     # ---- speculative replay ---------------------------------------------------------------------
     def backup(self, u_buf: Optional[Tensor]):
@@ -769,15 +798,19 @@ class StepGraph:
         prep = self._post_prepare()
         if not flags_ok():
             self._asserts.after_replay(dev, raise_=False)
+            self._finish_deferred(apply=False)
             self._rollback(rng, restore_actions=True)
             return None
         try:
             self._asserts.after_replay(dev)
         except AssertionError:
+            self._finish_deferred(apply=False)
             self._rollback(rng, restore_actions=False)
             raise
         # only now: the post-replay carry overwrites X, which a rollback restores Y from
-        return self._post_replay(prep)
+        out = self._post_replay(prep)
+        self._finish_deferred()
+        return out
 
     def _rollback(self, rng: Tensor, restore_actions: bool):
         self._post = None
