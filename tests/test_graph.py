@@ -66,9 +66,7 @@ CASES = [
 @pytest.mark.parametrize("name,kw,substeps,expect", CASES, ids=[c[0] for c in CASES])
 def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, substeps, expect):
     if name == "discovery-hole":
-        from vectorizedmultiagentsimulator_amd.scenarios import discovery
-
-        monkeypatch.setattr(discovery, "DEFERRED_RESPAWN", False)
+        monkeypatch.setenv("VMAS_GRAPH_DEFERRED_SPAWN", "0")
         name = "discovery"
         hole = True
     else:
@@ -176,9 +174,7 @@ def test_failed_segmented_capture_restores_state_gpu(gpu_device, monkeypatch, de
     """A capture that fails after host holes already ran the graphs before them (discovery's
     spawn sampler) restores the world and the generator, and the env continues eagerly with the
     eager twin's results."""
-    from vectorizedmultiagentsimulator_amd.scenarios import discovery
-
-    monkeypatch.setattr(discovery, "DEFERRED_RESPAWN", deferred)
+    monkeypatch.setenv("VMAS_GRAPH_DEFERRED_SPAWN", "1" if deferred else "0")
     eager, graph = _twin_envs(gpu_device, "discovery", n_agents=4)
     orig = graph.scenario.info
 

@@ -13,3 +13,4 @@ run pytest 900 python -u -m pytest tests/test_graph.py tests/test_spawn.py tests
 run stepk_disc 300 python tools/step_kernels.py discovery 16384 8
 run host_disc 300 python tools/host_profile.py discovery 16384
 run bench_c4 300 python bench.py --scenario discovery --steps 100 --warmup 10 --cpu-steps 0
+run stepk_bal 300 python tools/step_kernels.py balance 32768 4

@@ -178,10 +178,15 @@ class Scenario(BaseScenario):
             return False
         args = (ap, self.covered_targets, float(self._min_dist_between_entities), float(w.x_semidim),
                 float(w.y_semidim), *[t.state.pos for t in self._targets])
-        dsink = getattr(w, "_deferred_sink", None) if DEFERRED_RESPAWN else None
+        deferred = deferred_respawn()
+        dsink = getattr(w, "_deferred_sink", None) if deferred else None
         sink = getattr(w, "_hole_sink", None)
-        if dsink is not None:  # a graph-mode capture: the launch stays inside the step's graph
-            dsink(DeferredRespawn(args))
+        if deferred and not torch.cuda.is_current_stream_capturing() and \
+                getattr(self, "_spawn_channel", None) is None:
+            self._spawn_channel = SpawnChannel(dev, len(self._targets))  # (pinned memory: not in a capture)
+        if dsink is not None and getattr(self, "_spawn_channel", None) is not None:
+            # a graph-mode capture: the launch stays inside the step's graph
+            dsink(DeferredRespawn(args, self._spawn_channel))
         elif sink is not None:  # (the segmented form: the host read is a hole of the step)
             sink(respawn_targets_native, args)
         else:
@@ -494,9 +499,34 @@ def _spawn_consumed(h, T: int, offset: int, inc: int, gen) -> None:
             "tries; make sure the bounds or the min_dist_between_entities are not too tight to fit all entities")
 
 
-# Graph mode: the respawn captured inside the step's graph through a spawn channel (DeferredRespawn)
-# instead of a host hole splitting the step in two graphs (VMAS_GRAPH_DEFERRED_SPAWN=0: the hole)
-DEFERRED_RESPAWN = os.environ.get("VMAS_GRAPH_DEFERRED_SPAWN", "1") != "0"
+def deferred_respawn() -> bool:
+    """Graph mode: the respawn captured inside the step's graph through a spawn channel
+    (DeferredRespawn) instead of a host hole splitting the step in two graphs
+    (VMAS_GRAPH_DEFERRED_SPAWN=0: the hole; read per call -- make_env loads scenario modules afresh)."""
+    return os.environ.get("VMAS_GRAPH_DEFERRED_SPAWN", "1") != "0"
+
+
+class SpawnChannel:
+    """Owner of a vmas_spawn_channel (mapped pinned host words), created outside any capture."""
+
+    def __init__(self, dev: torch.device, n_targets: int):
+        self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        # the launch's device words, owned here (allocated outside any capture: a buffer from a
+        # capture's private pool was found overwritten after a later replay)
+        self.mx = torch.zeros(N.spawn_words(n_targets), dtype=torch.int32, device=dev)
+        ch = ctypes.c_void_p()
+        N.check_aux(N.load_library().vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
+        self.ptr = ch
+        self.seq = 0
+        self.busy = None  # the DeferredRespawn with a launch in flight
+
+    def __del__(self):
+        try:
+            if self.busy is not None:
+                torch.cuda.synchronize(self.idx)
+            N.load_library().vmas_spawn_channel_destroy(self.ptr)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
 
 class DeferredRespawn:
@@ -508,16 +538,12 @@ class DeferredRespawn:
     the eager call does -- the step's one host wait, with the rest of the step still running on the
     device, instead of a mid-step graph break and a second graph launch (StepGraph._deferred)."""
 
-    def __init__(self, args):
+    def __init__(self, args, channel: SpawnChannel):
         self.args = args
-        dev = args[0].device
-        self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.chan = channel
+        self.ch = channel.ptr
+        self.idx = channel.idx
         self.T = len(args) - 5
-        lib = N.load_library()
-        ch = ctypes.c_void_p()
-        N.check_aux(lib.vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
-        self.ch = ch
-        self.seq = 0
         self.pending = None
         self.inc = 0
         self.offset = 0
@@ -525,23 +551,26 @@ class DeferredRespawn:
 
     def capture(self):
         a = self.args
-        self.mx = torch.empty(N.spawn_words(self.T), dtype=torch.int32, device=a[0].device)
+        self.mx = self.chan.mx
         _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch)
 
     def arm(self):
-        if self.pending is not None:  # (an earlier replay never finished: drain it first)
-            self.finish(apply=False)
+        if self.chan.busy is not None:  # (an earlier replay never finished: drain it first)
+            self.chan.busy.finish(apply=False)
         gen = torch.cuda.default_generators[self.idx]
-        self.seq = self.seq % 0xFFFFFFFF + 1
+        self.chan.seq = self.chan.seq % 0xFFFFFFFF + 1
         self.offset = gen.get_offset()
-        N.check_aux(N.load_library().vmas_spawn_channel_arm(self.ch, gen.initial_seed(), self.offset, self.seq),
+        N.check_aux(N.load_library().vmas_spawn_channel_arm(self.ch, gen.initial_seed(), self.offset, self.chan.seq),
                     "vmas_spawn_channel_arm")
-        self.pending = self.seq
+        self.pending = self.chan.seq
+        self.chan.busy = self
 
     def finish(self, apply: bool = True):
         if self.pending is None:
             return
         seq, self.pending = self.pending, None
+        if self.chan.busy is self:
+            self.chan.busy = None
         words = (ctypes.c_int32 * (self.T + 2))()
         rc = N.load_library().vmas_spawn_channel_wait(self.ch, seq, words, self.T,
                                                       ctypes.c_void_p(torch.cuda.current_stream(self.idx).cuda_stream))
@@ -556,13 +585,6 @@ class DeferredRespawn:
         if apply:
             _spawn_consumed(h, self.T, self.offset, self.inc, torch.cuda.default_generators[self.idx])
 
-    def __del__(self):
-        try:
-            if self.pending is not None:
-                torch.cuda.synchronize(self.idx)
-            N.load_library().vmas_spawn_channel_destroy(self.ch)
-        except Exception:  # noqa: BLE001 -- interpreter shutdown
-            pass
 
 
 def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
