@@ -599,7 +599,10 @@ int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* 
 /* Device-to-device byte copies, all spans in one launch (csrc/vmas_copy.hip): graph mode's carried
  * state, output clones and per-step backups (simulator/environment/_graph.py; no reference
  * counterpart -- the reference returns fresh tensors from its eager ops).  Spans must not
- * overlap one another's destinations; more than VMAS_COPY_MAX_SPANS spans take several launches. */
+ * overlap one another's destinations; more than VMAS_COPY_MAX_SPANS spans take several launches.
+ * A span with src == NULL is an increment, not a copy: 1.0f is added to each of the nbytes / 4
+ * floats at dst (4-byte aligned) -- graph mode's `Environment.steps += 1` (ref environment.py:397),
+ * folded into the post-replay launch instead of a kernel node of its own. */
 #define VMAS_COPY_MAX_SPANS 48
 typedef struct VmasCopySpan {
     const void* src;

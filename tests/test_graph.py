@@ -101,6 +101,7 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
         out_g = graph.step([a.clone() for a in actions])
         _assert_same(out_e, out_g, f"{name} outputs step {t}")
         _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
+        assert torch.equal(eager.steps, graph.steps), (name, t)  # (folded into the post-replay launch)
         if t == 4:
             held = _flat(out_g, [])[0].clone(), _flat(out_g, [])[0]
     # returned tensors are fresh copies: a later replay does not overwrite them
@@ -108,6 +109,7 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
     assert graph.graph_status == expect, graph.graph_reason
     if expect == "graph":
         assert graph._graph.replays >= 5
+        assert graph._graph._steps_folded  # no max_steps: steps += 1 left the graph
     if name == "discovery":  # the targets' respawn is one native call: inside the one graph with
         # its host side after the replay (a spawn channel), or one host hole between two graphs
         n_holes, n_segments = len(graph._graph._holes), len(graph._graph._segments)
@@ -347,8 +349,9 @@ def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,kw,substeps", [("balance", dict(n_agents=4), 10), ("flocking", dict(n_agents=4), None)],
-                         ids=["balance", "flocking"])
+@pytest.mark.parametrize("name,kw,substeps", [("balance", dict(n_agents=4), 10), ("flocking", dict(n_agents=4), None),
+                                               ("discovery", dict(n_agents=4), None)],
+                         ids=["balance", "flocking", "discovery"])
 def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substeps):
     """env.step(env.get_random_actions()) in graph mode: the draw kernel also writes the applied
     actions into the graph's action buffer, and the step launches no action kernel.  Bit-identical
@@ -377,5 +380,43 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substep
         _assert_same(out_e, out_g, f"{name} outputs step {t}")
         _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
         _assert_same([a.action.u for a in eager.agents], [a.action.u for a in graph.agents], f"u step {t}")
+        assert torch.equal(eager.steps, graph.steps), (name, t)
     assert graph.graph_status == "graph", graph.graph_reason
     assert graph.preapplied_steps >= 5
+
+
+@pytest.mark.gpu
+def test_max_steps_keeps_the_counter_in_the_graph_gpu(gpu_device):
+    """With max_steps the done program reads the step counter (ref environment.py:415-418), so the
+    capture keeps `steps += 1` inside the graph; dones (terminated + truncated) match the eager
+    step across the truncation and a reset_at, and setting max_steps on a folded graph drops it."""
+    envs = []
+    for graph in (False, True):
+        saved = _rng_save()
+        envs.append(make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=graph, n_agents=3,
+                             max_steps=6))
+        if not graph:
+            _rng_load(saved)
+    eager, graph = envs
+    for t in range(10):
+        actions = eager.get_random_actions()
+        if t == 7:
+            for env in (eager, graph):
+                s = _rng_save()
+                env.reset_at(5)
+                if env is eager:
+                    _rng_load(s)
+        out_e, out_g = _step_both(eager, graph, actions)
+        _assert_same(out_e, out_g, f"max_steps outputs step {t}")
+        assert torch.equal(eager.steps, graph.steps), t
+    assert graph.graph_status == "graph", graph.graph_reason
+    assert not graph._graph._steps_folded
+    # a folded capture, then max_steps set: the graph is dropped and the next steps stay exact
+    eager, graph = _twin_envs(gpu_device, "balance", n_agents=3)
+    for t in range(8):
+        if t == 5:
+            eager.max_steps = graph.max_steps = 6
+        actions = eager.get_random_actions()
+        out_e, out_g = _step_both(eager, graph, actions)
+        _assert_same(out_e, out_g, f"max_steps set later, step {t}")
+        assert torch.equal(eager.steps, graph.steps), t

@@ -17,7 +17,10 @@ for t in range(14):
     if t == 9:
         env.reset()
     try:
-        env.step(env.get_random_actions())
+        acts = env.get_random_actions()
+        if os.environ.get("PROBE_CLONE", "1") == "1":  # test_fused's form: cloned actions (the speculative path)
+            acts = [a.clone() for a in acts]
+        env.step(acts)
     except Exception as ex:  # noqa: BLE001
         g = env._graph
         print(f"step {t}: {type(ex).__name__}: {ex}", flush=True)

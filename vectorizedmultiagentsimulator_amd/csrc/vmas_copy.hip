@@ -39,6 +39,13 @@ __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restr
 
 __global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) {
     const VmasCopySpan& s = a.s[blockIdx.y];
+    if (!s.src) {  // an increment span: dst[i] += 1.0f
+        float* d = reinterpret_cast<float*>(s.dst);
+        const int64_t n = s.nbytes / 4;
+        for (int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kCopyThreads)
+            d[i] = d[i] + 1.0f;
+        return;
+    }
     const uintptr_t al = (uintptr_t)s.src | (uintptr_t)s.dst | (uintptr_t)s.nbytes;
     if ((al & 15) == 0)
         copy_units(reinterpret_cast<const uint4*>(s.src), reinterpret_cast<uint4*>(s.dst), s.nbytes / 16);
@@ -59,7 +66,8 @@ extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, in
         int64_t most = 0;  // units of the largest span (16-byte units: sets the grid)
         for (int i = first; i < std::min(n, first + VMAS_COPY_MAX_SPANS); ++i) {
             const VmasCopySpan& s = spans[i];
-            if (s.nbytes < 0 || (s.nbytes > 0 && (!s.src || !s.dst)))
+            if (s.nbytes < 0 || (s.nbytes > 0 && !s.dst) ||
+                (!s.src && (s.nbytes % 4 != 0 || ((uintptr_t)s.dst & 3) != 0)))
                 return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad span %d", i);
             if (s.nbytes == 0 || s.src == s.dst) continue;
             a.s[a.n++] = s;

@@ -4,8 +4,8 @@ The reference's step is an eager tensor program: per step ~70 small kernels for 
 (scenario rewards / observations / dones around the physics launch), each launched from Python.
 On the MI355X that host work, not the GPU, sets the step time.  Once a world is warm this module
 captures everything after the action check -- ``env_process_action``, ``pre_step``,
-``World.step`` (the k_world launch and its fixed-point control words), ``post_step``, the step
-counter and the scenario's rewards / observations / infos / dones -- into ONE HIP graph
+``World.step`` (the k_world launch and its fixed-point control words), ``post_step`` and the
+scenario's rewards / observations / infos / dones -- into ONE HIP graph
 (``torch.cuda.CUDAGraph``: stream capture, hipGraphInstantiate, hipGraphLaunch) and replays it.
 
 What a replay must honour, and how:
@@ -26,7 +26,9 @@ What a replay must honour, and how:
     Entity / world parameter changes (mass, shape, substeps, ...) drop the graph; the next step
     runs eagerly and captures again.
   * Outputs.  The returned observations / rewards / dones / infos are fresh copies (the
-    reference clones them too), made by one multi-tensor copy per dtype after the replay.
+    reference clones them too), made by one multi-tensor copy after the replay.  The same launch
+    adds one to the step counter (``steps += 1``) when nothing in the step reads it (no
+    ``max_steps``): one kernel node fewer per step.
   * Asserts on device tensors inside the step (a scripted agent's action range check,
     core.py:977-980) are captured as device checks (``_DeviceAsserts``); a failed one rolls the
     replayed step back -- the tensors the step modifies in place (found by version counters at
@@ -376,6 +378,11 @@ class StepGraph:
         # launches captured with their host side deferred (world._deferred_sink: discovery's
         # DeferredRespawn): armed before every replay, finished after its host work is queued
         self._deferred: List[Any] = []
+        # Environment.steps += 1 (ref environment.py:397) folded into the post-replay launch (an
+        # increment span of vmas_copy_spans) instead of a kernel node of the graph: set while the
+        # capture records body(), kept for the captured graph (_steps_folded)
+        self._folding = False
+        self._steps_folded = False
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -386,7 +393,8 @@ class StepGraph:
         env.scenario.pre_step()
         env.world.step()
         env.scenario.post_step()
-        env.steps += 1
+        if not self._folding:
+            env.steps += 1
         return env._get_from_scenario(get_observations=True, get_infos=True, get_rewards=True, get_dones=True)
 
     def before_actions(self):
@@ -402,6 +410,9 @@ class StepGraph:
         self.env.world.engine.check_device_errors()
         if not self._still_valid():
             self.drop("world or entity parameters changed")
+            return
+        if self._steps_folded and not self._fold_steps_ok():  # (max_steps set: the done program reads steps)
+            self.drop("max_steps set or Environment.steps re-bound after the capture")
             return
         for d, k, t in self._watch:
             cur = d.get(k, None)
@@ -537,8 +548,19 @@ class StepGraph:
         self._out_tensors = []
         self._carry_dst, self._carry_src, self._watch = [], [], []
         self._carry_ys, self._post = [], None
+        self._steps_folded = False
 
     # ---- capture --------------------------------------------------------------------------------
+    _FOLD_STEPS = os.environ.get("VMAS_GRAPH_FOLD_STEPS", "1") != "0"  # (A/B knob)
+
+    def _fold_steps_ok(self) -> bool:
+        """Whether the capture leaves `steps += 1` to the post-replay launch: nothing in the
+        captured step reads steps (no max_steps: the done program reads it, ref
+        environment.py:415-418) and it is a contiguous fp32 tensor on the step's device."""
+        st = getattr(self.env, "steps", None)
+        return (self._FOLD_STEPS and self.env.max_steps is None and isinstance(st, Tensor)
+                and st.dtype is torch.float32 and st.is_contiguous() and st.device.type == "cuda")
+
     def _capture(self) -> bool:
         env = self.env
         eng = env.world.engine
@@ -583,6 +605,7 @@ class StepGraph:
             env.world._hole_sink = segs.hole
             env.world._deferred_sink = deferred_sink
             torch.cuda.synchronize(dev)
+            self._folding = self._fold_steps_ok()
             with torch.cuda.stream(side), consts:
                 segs.begin()
                 out = self.body()
@@ -621,6 +644,7 @@ class StepGraph:
             self.status = "eager"
             self.why = f"{type(ex).__name__}: {str(ex).splitlines()[0] if str(ex) else ''}"[:300]
             self.graph = None
+            self._folding = False
             return False
         finally:
             if gc_was_on:
@@ -631,6 +655,7 @@ class StepGraph:
             env.world._hole_sink = None
             env.world._deferred_sink = None
         del contents
+        self._steps_folded, self._folding = self._folding, False
         self._deferred = deferred
         self.graph = g
         self._segments, self._holes = segs.graphs, segs.holes
@@ -779,6 +804,22 @@ class StepGraph:
                 else:
                     torch._foreach_copy_(self._bk_dst[:n], self._bk_src[:n])
 
+    def rollback_free(self) -> bool:
+        """No device assert in the captured step: a step whose actions pass by construction (drawn
+        and applied by get_random_actions) can then never be rolled back."""
+        return self._asserts is None or not self._asserts.msgs
+
+    def replay_preapplied(self):
+        """One replay of a step whose actions were drawn and applied by the draw's own launch and
+        that has no device asserts (rollback_free): the speculative replay without its backups and
+        generator snapshot, which only a rollback reads."""
+        self._first_replay = False
+        self._launch()
+        self.replays += 1
+        out = self._post_replay()
+        self._finish_deferred()
+        return out
+
     def replay_speculative(self, flags_ok):
         """Replays the step while the action kernel's flags are still in flight, then waits for
         them (flags_ok(): the host wait of the eager path, now overlapping the replay).  Passing
@@ -869,6 +910,8 @@ class StepGraph:
     def _post_prepare(self):
         """The host half of _post_replay: (span table, fresh output views, non-contiguous rest)."""
         t = self._post_table()
+        if t["steps_row"] is not None:
+            self._steps_current(t)
         views, rest = self._clone_alloc(t)
         return t, views, rest
 
@@ -911,6 +954,11 @@ class StepGraph:
             return c[4]
         out_rows = [(x.data_ptr(), 0, x.numel() * x.element_size()) for _, _, srcs in self._clone_group_srcs
                     for x in srcs if x.is_contiguous()]
+        steps_row = None
+        if self._steps_folded:  # (last output row: the launch of the outputs always covers it)
+            st = self.env.steps
+            steps_row = len(out_rows)
+            out_rows.append((0, st.data_ptr(), st.numel() * 4))
         carry, bk, n_bk = self._post_spans()
         plain = bool(self._carry_other) or bk is None
         extra = [] if plain else carry + bk
@@ -920,30 +968,44 @@ class StepGraph:
         clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows for _, x, cn in carry)
         t = {"tbl": tbl, "addr": tbl.ctypes.data, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra),
              "plain": plain,
-             "clash": clash, "n_bk": n_bk,
+             "clash": clash, "n_bk": n_bk, "steps_row": steps_row, "steps": self.env.steps if self._steps_folded else None,
              "contig": [[x.is_contiguous() for x in srcs] for _, _, srcs in self._clone_group_srcs]}
         self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
         return t
 
+    def _steps_current(self, t) -> None:
+        """Point the table's increment row at env.steps as bound now (reset() re-binds it)."""
+        st = self.env.steps  # (checked by before_actions: fp32, contiguous, on the device)
+        if t["steps"] is not st:
+            t["tbl"][t["steps_row"]]["dst"] = st.data_ptr()
+            t["tbl"][t["steps_row"]]["nbytes"] = st.numel() * 4
+            t["steps"] = st
+
     def _clone_alloc(self, t):
         """Fresh output tensors for one step, their addresses written into the table's output
         rows: (views in the plan's order, the non-contiguous (dst, src) rest)."""
-        dev = self._out_tensors[0].device
+        plan = t.get("alloc")
+        if plan is None:  # per table: each group's rows and the byte offsets of its contiguous members
+            plan, row = [], 0
+            dev = self._out_tensors[0].device
+            for (dt, shape, n), (_, _, srcs), contig in zip(self._clone_groups, self._clone_group_srcs, t["contig"]):
+                step = int(np.prod(shape, dtype=np.int64)) * torch.empty((), dtype=dt).element_size()
+                ks = [k for k, c in enumerate(contig) if c]
+                plan.append(((n,) + shape, dt, dev, row, row + len(ks), np.array(ks, dtype=np.uint64) * np.uint64(step),
+                             [(k, srcs[k]) for k, c in enumerate(contig) if not c]))
+                row += len(ks)
+            t["alloc"] = plan
         views = ()
         dst = t["tbl"]["dst"]
-        row = 0
         rest = []
-        for (dt, shape, n), (_, _, srcs), contig in zip(self._clone_groups, self._clone_group_srcs, t["contig"]):
-            buf = torch.empty((n,) + shape, dtype=dt, device=dev)
+        for shape, dt, dev, r0, r1, offs, loose in plan:
+            buf = torch.empty(shape, dtype=dt, device=dev)
             vs = buf.unbind(0)
             views += vs
-            base, step = buf.data_ptr(), buf.stride(0) * buf.element_size()
-            for k, c in enumerate(contig):
-                if c:
-                    dst[row] = base + k * step
-                    row += 1
-                else:
-                    rest.append((vs[k], srcs[k]))
+            if r1 > r0:
+                np.add(offs, buf.data_ptr(), out=dst[r0:r1], casting="unsafe")
+            for k, src in loose:
+                rest.append((vs[k], src))
         return views, rest
 
     def _clone_plan(self):
@@ -996,6 +1058,8 @@ class StepGraph:
     def _clone_outputs(self):
         """Fresh copies of the replay's outputs (the reference returns fresh tensors too)."""
         t = self._post_table()
+        if t["steps_row"] is not None:
+            self._steps_current(t)
         views, rest = self._clone_alloc(t)
         N.copy_table_at(self._dev_index(), t["addr"], 0, t["n_out"], self._stream())
         self._clone_finish(rest)

@@ -272,9 +272,18 @@ class Environment(TorchVectorizedObject):
         g = self._graph
         if g is not None and g.graph is not None and self.continuous_actions:
             try:
-                actions = self._check_action_list(actions)
+                # the last draw's own tensors, unmodified, pass every check of _check_action_list by
+                # construction (a list of [B, action_size] fp32 device tensors, one per agent)
+                drawn = self._drawn
+                if not (drawn is not None and type(actions) is list and len(actions) == len(drawn[0])
+                        and all(a is t and a._version == v for a, t, v in zip(actions, drawn[0], drawn[2]))):
+                    actions = self._check_action_list(actions)
                 g.before_actions()
                 if g.graph is not None:
+                    if self._can_speculate() and g.rollback_free() and self._take_preapplied(actions):
+                        # drawn + applied by get_random_actions, and nothing in the step can roll it
+                        # back: no backup, no generator snapshot
+                        return g.replay_preapplied()
                     if self._can_speculate():
                         # the replay is launched before the action flags are known; a failed flag
                         # rolls the step back (StepGraph.replay_speculative) and the eager check
