@@ -264,8 +264,14 @@ typedef const VmasFlockingIO __attribute__((address_space(4))) KFlockingIO;  // 
 #else
 typedef const VmasFlockingIO KFlockingIO;  // (the host pass only parses the kernel)
 #endif
+// NR / NT > 0: the ray and target counts fixed at compile time (flocking's 12 rays; instantiated
+// for 1..8 targets): every ray unrolled with its angle in a register, so the rays' chains
+// interleave (the rolled loop left each wave one ray's dependent chain at a time, at 4 waves per
+// SIMD), no per-target branch, and the LIDAR row split by a constant.  Same operations per ray
+// in the same order as the runtime form (bit-identical).
+template <int NR, int NT>
 __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
-    constexpr int RM = kFlockFastRays, TM = kFlockFastTargets;
+    constexpr int RM = NR > 0 ? NR : kFlockFastRays, TM = NT > 0 ? NT : kFlockFastTargets;
     // The argument block read in place (s_load from the kernel argument segment): indexed by the
     // wave's agent, the by-value parameter was copied to scratch (3.5 KiB per lane)
 #ifdef __HIP_DEVICE_COMPILE__
@@ -282,7 +288,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
     const int p = __builtin_amdgcn_readfirstlane((int)blockIdx.y * 4 + w);
     if (p >= io.n_policy) return;  // (wave-uniform; no workgroup barrier below)
     const bool valid = b < io.batch;
-    const int nr = io.n_rays, nt = io.n_ray_targets, W = 6 + nr;
+    const int nr = NR > 0 ? NR : io.n_rays, nt = NT > 0 ? NT : io.n_ray_targets, W = 6 + nr;
     const int bb = valid ? b : io.batch - 1;
     const int row = lane * W;
     if (io.what & VMAS_SCN_OBS) {
@@ -316,32 +322,50 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
         float C[TM];
 #pragma unroll
         for (int t = 0; t < TM; ++t) C[t] = R2[t] - (T[t].x * T[t].x + T[t].y * T[t].y);
-        // rays in a rolled loop, targets unrolled inside (see k_discovery_obs_fast)
-        // (the angles wait in the rays' own LDS slots: a register array indexed at run time goes to
-        // scratch)
+        if constexpr (NR > 0 && NT > 0) {
 #pragma unroll
-        for (int r = 0; r < RM; ++r)
-            if (r < nr) S[w][row + 6 + r] = A[r] + rot;
+            for (int r = 0; r < NR; ++r) {
+                const float a = A[r] + rot;
+                // hardware sin / cos (v_sin / v_cos_f32: a few 1e-7 rad at these angles, within
+                // the LIDAR certification's 1e-6 rad) instead of ocml's range-reduced sincosf;
+                // large angles keep sincosf
+                float ds, dc;
+                if (fabsf(a) < 256.f) {
+                    ds = __sinf(a);
+                    dc = __cosf(a);
+                } else {
+                    sincosf(a, &ds, &dc);
+                }
+                float best = io.max_range;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) best = min_drop_nan(best, ray_sphere_fast_nan(T[t].x, T[t].y, C[t], dc, ds));
+                S[w][row + 6 + r] = best;
+            }
+        } else {
+            // rays in a rolled loop, targets unrolled inside (see k_discovery_obs_fast)
+            // (the angles wait in the rays' own LDS slots: a register array indexed at run time
+            // goes to scratch)
+#pragma unroll
+            for (int r = 0; r < RM; ++r)
+                if (r < nr) S[w][row + 6 + r] = A[r] + rot;
 #pragma unroll 1
-        for (int r = 0; r < nr; ++r) {
-            const float a = S[w][row + 6 + r];
-            // hardware sin / cos (v_sin / v_cos_f32: a few 1e-7 rad at these angles, within the
-            // LIDAR certification's 1e-6 rad) instead of ocml's range-reduced sincosf; large
-            // angles keep sincosf
-            float ds, dc;
-            if (fabsf(a) < 256.f) {
-                ds = __sinf(a);
-                dc = __cosf(a);
-            } else {
-                sincosf(a, &ds, &dc);
-            }
-            float best = io.max_range;
+            for (int r = 0; r < nr; ++r) {
+                const float a = S[w][row + 6 + r];
+                float ds, dc;
+                if (fabsf(a) < 256.f) {
+                    ds = __sinf(a);
+                    dc = __cosf(a);
+                } else {
+                    sincosf(a, &ds, &dc);
+                }
+                float best = io.max_range;
 #pragma unroll
-            for (int t = 0; t < TM; ++t) {
-                if (t >= nt) continue;
-                best = min_drop_nan(best, ray_sphere_fast_nan(T[t].x, T[t].y, C[t], dc, ds));
+                for (int t = 0; t < TM; ++t) {
+                    if (t >= nt) continue;
+                    best = min_drop_nan(best, ray_sphere_fast_nan(T[t].x, T[t].y, C[t], dc, ds));
+                }
+                S[w][row + 6 + r] = best;
             }
-            S[w][row + 6 + r] = best;
         }
         // the wave's rows out as contiguous blocks: obs [64 x W], the LIDAR [64 x nr]
         const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
@@ -766,10 +790,21 @@ int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* st
     VMAS_AUX_HIP(hipSetDevice(device));
     static_assert(sizeof(VmasFlockingIO) <= 4096, "kernel argument block");
     const int parts = (io->what & VMAS_SCN_OBS) ? 1 + io->n_rays : 1;
-    if (io->fast_lidar && io->n_rays <= kFlockFastRays && io->n_ray_targets <= kFlockFastTargets)
-        hipLaunchKernelGGL(k_flocking_fast, dim3((io->batch + 63) / 64, (io->n_policy + 3) / 4), dim3(256), 0,
-                           (hipStream_t)stream, *io);
-    else
+    if (io->fast_lidar && io->n_rays <= kFlockFastRays && io->n_ray_targets <= kFlockFastTargets) {
+        const dim3 grid((io->batch + 63) / 64, (io->n_policy + 3) / 4);
+        const hipStream_t st = (hipStream_t)stream;
+        // flocking's 12 rays with 1..8 targets: the unrolled instantiation (VMAS_FLOCK_UNROLL=0: runtime form)
+        static const bool unroll = !getenv("VMAS_FLOCK_UNROLL") || getenv("VMAS_FLOCK_UNROLL")[0] != '0';
+        const int nt = unroll && io->n_rays == 12 ? io->n_ray_targets : 0;
+        switch (nt) {
+#define VMAS_FLOCK_CASE(k) \
+    case k: hipLaunchKernelGGL((k_flocking_fast<12, k>), grid, dim3(256), 0, st, *io); break;
+            VMAS_FLOCK_CASE(1) VMAS_FLOCK_CASE(2) VMAS_FLOCK_CASE(3) VMAS_FLOCK_CASE(4)
+            VMAS_FLOCK_CASE(5) VMAS_FLOCK_CASE(6) VMAS_FLOCK_CASE(7) VMAS_FLOCK_CASE(8)
+#undef VMAS_FLOCK_CASE
+            default: hipLaunchKernelGGL((k_flocking_fast<0, 0>), grid, dim3(256), 0, st, *io); break;
+        }
+    } else
         hipLaunchKernelGGL(k_flocking, dim3((io->batch + 63) / 64, io->n_policy * parts), dim3(64), 0, (hipStream_t)stream,
                            *io);
     VMAS_AUX_HIP(hipGetLastError());

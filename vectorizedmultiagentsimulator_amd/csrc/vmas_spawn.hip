@@ -548,6 +548,16 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
     }
 }
 
+// Zeroes a launch's words (vmas_spawn_targets) ahead of the spawn kernel.  A kernel rather than
+// hipMemsetAsync: inside a captured HIP graph a memset node in front of the spawn kernel was seen
+// to leave the words holding a repeated 16-byte pattern of pointer-like values on some replays
+// (ROCm 7.2 / MI355X; discovery's graph step then timed out in the kernel's bounded wait), and
+// round 1 saw memset nodes in front of k_world's persistent launch that had not completed when the
+// kernel ran.  A kernel node is ordered like every other node of the graph.
+__global__ void __launch_bounds__(256) k_spawn_clear(int32_t* w, int n) {
+    for (int i = (int)threadIdx.x; i < n; i += 256) w[i] = 0;
+}
+
 // The smallest float x >= 0 with sqrtf(x) >= min_dist (binary search over the ordered bit patterns
 // of non-negative floats; sqrtf is correctly rounded on the host as on the device).
 float spawn_d2_min(float min_dist) {
@@ -731,7 +741,7 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     const float d2_min = spawn_d2_min(io->min_dist);
     hipStream_t st = (hipStream_t)stream;
     const int T = io->n_targets, n_groups = (int)((B + 63) / 64);
-    VMAS_AUX_HIP(hipMemsetAsync(io->max_accepted, 0, sizeof(int32_t) * VMAS_SPAWN_WORDS(T), st));
+    hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T));
     const bool group_resident = n_groups <= resident_static[device] && !getenv("VMAS_SPAWN_CLAIMED");
     const long long grid = std::min<long long>(n_groups, resident[device]);
     // VMAS_SPAWN_PROFILE=1 (a probe's knob): per item s_memrealtime stamps [claimed, wait over,

@@ -730,7 +730,11 @@ class StepGraph:
                 if isinstance(v, Tensor):
                     self._watch.append((d, k, v))
         self._out_tree = out
-        self._out_tensors = _tensors(out, [])
+        # an output marked constant (BaseScenario.done's all-False view of one element made outside
+        # the capture, which no replay writes) is copied from a contiguous copy made once here:
+        # part of the post-replay launch instead of a strided torch copy per step
+        self._out_tensors = [t.contiguous() if getattr(t, "_vmas_constant", False) and not t.is_contiguous() else t
+                             for t in _tensors(out, [])]
 
     def _still_valid(self) -> bool:
         return self.env.world.engine.graph_token() == self._sig

@@ -73,7 +73,18 @@ class BaseScenario(ABC):
         raise NotImplementedError()
 
     def done(self) -> Tensor:
-        return torch.tensor([False], device=self.world.device).expand(self.world.batch_dim)
+        # ref scenario.py:300-328: a [batch_dim] all-False view expanded from one element.  The
+        # element is made once per device and reused (the view is read-only, as the reference's
+        # expanded tensor; a write through an earlier view bumps the version counter and a fresh
+        # element is made): a captured step then holds no host-to-device copy of it per replay.
+        w = self.world
+        c = getattr(self, "_done_false", None)
+        if c is None or c[0]._version != c[1] or c[0].device != torch.device(w.device):
+            t = torch.tensor([False], device=w.device)
+            c = self._done_false = (t, t._version)
+        v = c[0].expand(w.batch_dim)
+        v._vmas_constant = True  # (graph mode copies it from a contiguous copy made at capture)
+        return v
 
     def info(self, agent: Agent) -> AGENT_INFO_TYPE:
         return {}
