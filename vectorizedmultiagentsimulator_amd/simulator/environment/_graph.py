@@ -363,6 +363,7 @@ class StepGraph:
         self._carry_dst: List[Tensor] = []  # X (read by the graph)
         self._carry_src: List[Tensor] = []  # Y (written by the graph)
         self._watch: List[Tuple[dict, str, Tensor]] = []  # (obj.__dict__, key, bound tensor)
+        self._watch_cols = None  # the same as three parallel tuples (dicts, keys, tensors)
         self._first_replay = True
         self._asserts: Optional[_DeviceAsserts] = None
         self._inplace: List[Tensor] = []
@@ -383,6 +384,7 @@ class StepGraph:
         # capture records body(), kept for the captured graph (_steps_folded)
         self._folding = False
         self._steps_folded = False
+        self._steps_t = None
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -411,10 +413,16 @@ class StepGraph:
         if not self._still_valid():
             self.drop("world or entity parameters changed")
             return
-        if self._steps_folded and not self._fold_steps_ok():  # (max_steps set: the done program reads steps)
+        env = self.env
+        if self._steps_folded and (env.max_steps is not None or (env.steps is not self._steps_t and not self._fold_steps_ok())):
+            # (max_steps set: the done program reads steps)
             self.drop("max_steps set or Environment.steps re-bound after the capture")
             return
-        for d, k, t in self._watch:
+        w = self._watch_cols
+        # (every watched attribute still bound to its tensor: two C-level passes, no Python loop)
+        if w is not None and all(map(operator.is_, map(dict.get, w[0], w[1]), w[2])):
+            w = None
+        for d, k, t in (self._watch if w is not None else ()):
             cur = d.get(k, None)
             if cur is not t:
                 if not isinstance(cur, Tensor) or cur.shape != t.shape or cur.dtype != t.dtype:
@@ -547,6 +555,7 @@ class StepGraph:
         self._out_tree = None
         self._out_tensors = []
         self._carry_dst, self._carry_src, self._watch = [], [], []
+        self._watch_cols = None
         self._carry_ys, self._post = [], None
         self._steps_folded = False
 
@@ -656,6 +665,7 @@ class StepGraph:
             env.world._deferred_sink = None
         del contents
         self._steps_folded, self._folding = self._folding, False
+        self._steps_t = env.steps
         self._deferred = deferred
         self.graph = g
         self._segments, self._holes = segs.graphs, segs.holes
@@ -729,6 +739,8 @@ class StepGraph:
             for k, v in d.items():
                 if isinstance(v, Tensor):
                     self._watch.append((d, k, v))
+        self._watch_cols = (tuple(d for d, _, _ in self._watch), tuple(k for _, k, _ in self._watch),
+                            tuple(t for _, _, t in self._watch))
         self._out_tree = out
         # an output marked constant (BaseScenario.done's all-False view of one element made outside
         # the capture, which no replay writes) is copied from a contiguous copy made once here:
