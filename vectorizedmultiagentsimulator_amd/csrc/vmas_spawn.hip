@@ -232,7 +232,8 @@ __device__ __forceinline__ bool near(float ox, float oy, float x, float y, float
 // word sat on one line and 1024 workgroups polled it).
 //
 // max_accepted words: [0, T) per-target max accepted try, [T] unresolved envs, [32] the claim
-// counter, [64] error (1: a wait timed out), [96 + 32 i] target i's done items, then
+// counter, [40, 46) a channel's (seed, offset, seq) staged by k_spawn_clear, [64] error (1: a wait
+// timed out), [96 + 32 i] target i's done items, then
 // (k_spawn_targets_resident) kSpawnReplicas 64-bit words 128 bytes apart.
 constexpr int kSpawnWaves = 16;
 constexpr int kSpawnMaxOcc = 32 + VMAS_SPAWN_MAX_TARGETS - 1;  // agents + the other targets
@@ -253,13 +254,20 @@ struct ChanArgs {
     uint64_t* out;
 };
 
-// Generator state of a launch: the channel's (read at run time) or the arguments'.
+// With a channel, k_spawn_clear copies its (seed, offset, seq) into the launch's words at this
+// int32 index (free words of the claim counter's line) and the spawn kernel's workgroups read them
+// there: 256 workgroups each reading the mapped host words over PCIe took up to 54 us to all start
+// (the reads serialise), one copy by one thread takes one round trip.
+constexpr int kRngWord = 40;
+
+// Generator state of a launch: the channel's (staged by k_spawn_clear) or the arguments'.
 __device__ __forceinline__ void launch_rng(const VmasSpawnTargetsIO& io, const ChanArgs& ch, unsigned long long* seed,
                                            unsigned long long* off, unsigned long long* seq) {
     if (ch.in) {
-        *seed = __hip_atomic_load(ch.in + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        *off = __hip_atomic_load(ch.in + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        *seq = __hip_atomic_load(ch.in + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long* r = reinterpret_cast<const unsigned long long*>(io.max_accepted + kRngWord);
+        *seed = r[0];
+        *off = r[1];
+        *seq = r[2];
     } else {
         *seed = io.seed;
         *off = io.offset;
@@ -554,8 +562,13 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
 // (ROCm 7.2 / MI355X; discovery's graph step then timed out in the kernel's bounded wait), and
 // round 1 saw memset nodes in front of k_world's persistent launch that had not completed when the
 // kernel ran.  A kernel node is ordered like every other node of the graph.
-__global__ void __launch_bounds__(256) k_spawn_clear(int32_t* w, int n) {
+// (With a channel it also stages the channel's generator state at kRngWord, see launch_rng.)
+__global__ void __launch_bounds__(256) k_spawn_clear(int32_t* w, int n, const uint64_t* chan_in) {
     for (int i = (int)threadIdx.x; i < n; i += 256) w[i] = 0;
+    __syncthreads();
+    if (chan_in && threadIdx.x < 3)
+        reinterpret_cast<unsigned long long*>(w + kRngWord)[threadIdx.x] =
+            __hip_atomic_load(chan_in + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The smallest float x >= 0 with sqrtf(x) >= min_dist (binary search over the ordered bit patterns
@@ -741,7 +754,6 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     const float d2_min = spawn_d2_min(io->min_dist);
     hipStream_t st = (hipStream_t)stream;
     const int T = io->n_targets, n_groups = (int)((B + 63) / 64);
-    hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T));
     const bool group_resident = n_groups <= resident_static[device] && !getenv("VMAS_SPAWN_CLAIMED");
     const long long grid = std::min<long long>(n_groups, resident[device]);
     // VMAS_SPAWN_PROFILE=1 (a probe's knob): per item s_memrealtime stamps [claimed, wait over,
@@ -763,6 +775,7 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
         ch.in = io->channel->d_in;
         ch.out = io->channel->d_out;
     }
+    hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T), ch.in);
     if (group_resident)
         hipLaunchKernelGGL(k_spawn_targets_resident, dim3((unsigned)n_groups), dim3(64 * kSpawnWaves), 0, st, *io, g,
                            d2_min, prof, ch);
