@@ -464,6 +464,17 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
     uint32_t covm = 0u;  // (wave 0) the lane's covered targets
     if (wave == 0 && valid)
         for (int i = 0; i < T; ++i) covm |= io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1] ? (1u << i) : 0u;
+    // (wave 0) the targets whose new position waits in occ[A + i]: stored after the last target (no
+    // other workgroup reads them), so a target's completion waits only for its maximum
+    uint32_t movm = 0u;
+    auto store_moved = [&]() {
+        for (int i = 0; i < T; ++i)
+            if ((movm >> i) & 1u) {
+                float* p = io.pos[i] + (long)b * io.pos_s0[i];
+                p[0] = occ[A + i][lane].x;
+                p[io.pos_s1[i]] = occ[A + i][lane].y;
+            }
+    };
     for (int i = 0; i < T; ++i) {
         const long it = (long)i * n_groups + blockIdx.x;
         if (threadIdx.x == 0) {
@@ -493,7 +504,10 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
         }
         if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
         __syncthreads();
-        if (abort_s) return;
+        if (abort_s) {
+            if (wave == 0) store_moved();  // (the targets done before the timeout, as they were)
+            return;
+        }
         if (prof && threadIdx.x == 0) prof[it * 6 + 2] = __builtin_amdgcn_s_memrealtime();
         const unsigned long long off = off_s, seed = rng_s[0];
         for (int base = 0; base < VMAS_SPAWN_MAX_TRIES; base += kSpawnWaves) {  // (as k_spawn_targets)
@@ -524,11 +538,8 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
             for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
             if (lane == 0 && km > 0) atomicMax(&W[i], km);
             if (((covm >> i) & 1u) && !unresolved) {
-                const float2 xy = won[k % kSpawnWaves][lane];
-                float* p = io.pos[i] + (long)b * io.pos_s0[i];
-                p[0] = xy.x;
-                p[io.pos_s1[i]] = xy.y;
-                occ[A + i][lane] = xy;  // (read by the next target's tries, after its barrier)
+                occ[A + i][lane] = won[k % kSpawnWaves][lane];  // (read by the next target's tries, after its barrier)
+                movm |= 1u << i;
             }
             __builtin_amdgcn_s_waitcnt(0);  // the maxima have landed before the completion
             int last = 0;
@@ -554,6 +565,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
             }
         }
     }
+    if (wave == 0) store_moved();
 }
 
 // Zeroes a launch's words (vmas_spawn_targets) ahead of the spawn kernel.  A kernel rather than
