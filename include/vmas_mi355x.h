@@ -593,6 +593,12 @@ typedef struct VmasDiscoveryIO {
     float* covering[VMAS_DISC_MAX_AGENTS];        /* [B] in place */
     float* collision[VMAS_DISC_MAX_AGENTS];       /* [B] in place (zeroed) */
     float* rewards[VMAS_DISC_MAX_AGENTS];         /* [B] fresh */
+    /* (REWARD, optional: NULL skips) the step's other reductions over the targets, computed where
+     * covered_targets is: info's targets_covered = covered_targets.sum(-1) (discovery.py:247-255)
+     * and done() = all_time_covered_targets.all(-1) (discovery.py:264-265) */
+    int64_t* covered_count;                       /* [B] fresh */
+    const uint8_t* all_time;                      /* [B, T] torch.bool, contiguous */
+    uint8_t* done;                                /* [B] torch.bool fresh */
 } VmasDiscoveryIO;
 int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream);
 
@@ -603,7 +609,7 @@ int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* 
  * A span with src == NULL is an increment, not a copy: 1.0f is added to each of the nbytes / 4
  * floats at dst (4-byte aligned) -- graph mode's `Environment.steps += 1` (ref environment.py:397),
  * folded into the post-replay launch instead of a kernel node of its own. */
-#define VMAS_COPY_MAX_SPANS 48
+#define VMAS_COPY_MAX_SPANS 160 /* (spans travel as kernel arguments: 160 x 24 B < 4 KiB) */
 typedef struct VmasCopySpan {
     const void* src;
     void* dst;

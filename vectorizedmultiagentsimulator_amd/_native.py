@@ -228,7 +228,7 @@ class VmasShapeRef(ctypes.Structure):
     ]
 
 
-VMAS_COPY_MAX_SPANS = 48
+VMAS_COPY_MAX_SPANS = 160
 
 
 class VmasCopySpan(ctypes.Structure):
@@ -403,6 +403,7 @@ class VmasDiscoveryIO(ctypes.Structure):
         ("agents_pos", _vp), ("targets_pos", _vp), ("dists", _vp), ("per_target", _vp), ("covered", _vp),
         ("time_rew", _vp), ("shared", _vp), ("covering", _vp * _DA), ("collision", _vp * _DA),
         ("rewards", _vp * _DA),
+        ("covered_count", _vp), ("all_time", _vp), ("done", _vp),
     ]
 
 

@@ -22,6 +22,7 @@ struct CopyArgs {
     VmasCopySpan s[VMAS_COPY_MAX_SPANS];
     int n;
 };
+static_assert(sizeof(CopyArgs) <= 4096, "kernel argument block");
 
 template <typename T>
 __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restrict__ dst, int64_t n) {

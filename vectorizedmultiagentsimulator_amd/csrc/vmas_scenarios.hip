@@ -452,6 +452,18 @@ __global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
     }
 }
 
+// The optional reductions over the targets (VmasDiscoveryIO.covered_count / done): the count of
+// covered targets (an integer sum: exact) and all() of the all-time covered flags.
+template <class IO>
+__device__ __forceinline__ void disc_reductions(IO& io, int b, int T, int n_cov) {
+    if (io.covered_count) io.covered_count[b] = (int64_t)n_cov;
+    if (io.done) {
+        bool all = true;
+        for (int j = 0; j < T; ++j) all = all && io.all_time[(long)b * T + j] != 0;
+        io.done[b] = all ? 1 : 0;
+    }
+}
+
 // discovery.py:146-246 (restated in scenarios/discovery.py), REWARD part: one thread per env.
 __global__ void __launch_bounds__(64) k_discovery_reward(VmasDiscoveryIO io) {
     constexpr int MA = VMAS_DISC_MAX_AGENTS, MT = VMAS_DISC_MAX_TARGETS;
@@ -489,14 +501,17 @@ __global__ void __launch_bounds__(64) k_discovery_reward(VmasDiscoveryIO io) {
         }
     }
     bool cov[MT];
+    int n_cov = 0;
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
         cov[j] = cnt[j] >= io.agents_per_target;
         if (j < T) {
             io.per_target[(long)b * T + j] = (int64_t)cnt[j];
             io.covered[(long)b * T + j] = cov[j] ? 1 : 0;
+            n_cov += cov[j] ? 1 : 0;
         }
     }
+    disc_reductions(io, b, T, n_cov);
     // agent_reward: covering_reward[:] = 0; += (count of covered targets in range) * coeff;
     // shared[:] = 0; += each agent's covering reward in agent order; halved where nonzero
     float shared = 0.f;
@@ -623,6 +638,7 @@ __global__ void __launch_bounds__(1024) k_discovery_reward_fast(VmasDiscoveryIO 
             io.covered[(long)b * T + j] = cnt >= io.agents_per_target ? 1 : 0;
         }
     }
+    if (i == 1 % A && valid) disc_reductions(io, b, T, __builtin_popcount(covm));
     // agent i's covering reward: (count of covered targets in range) * coeff
     const float covr = 0.f + (float)__builtin_popcount(in & covm) * io.covering_rew_coeff;
     CR[i][lane] = covr;
@@ -829,7 +845,8 @@ int32_t vmas_transport_outputs(int32_t device, const VmasTransportIO* io, void* 
 int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream) {
     if (!io || device < 0 || io->batch <= 0 || io->n_agents < 1 || io->n_agents > VMAS_DISC_MAX_AGENTS ||
         io->n_targets < 0 || io->n_targets > VMAS_DISC_MAX_TARGETS || io->n_entities < 1 ||
-        io->n_entities > VMAS_DISC_MAX_ENTITIES || io->n_lidars < 0 || io->n_lidars > VMAS_DISC_MAX_LIDARS)
+        io->n_entities > VMAS_DISC_MAX_ENTITIES || io->n_lidars < 0 || io->n_lidars > VMAS_DISC_MAX_LIDARS ||
+        (io->done && !io->all_time))
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_discovery_outputs: bad arguments");
     for (int i = 0; i < io->n_agents; ++i)
         if (io->agent_entity[i] < 0 || io->agent_entity[i] >= io->n_entities)

@@ -290,6 +290,16 @@ class Scenario(BaseScenario):
             }
             for k in ("agents_pos", "targets_pos", "dists", "per_target", "covered", "time_rew"):
                 setattr(io, k, out[k].data_ptr())
+            # the step's other reductions over the targets, in the same launch: info's count of
+            # covered targets and done() (handed out by _targets_covered_count / done while their
+            # inputs are the same tensors at the same versions)
+            out["count"] = torch.empty(B, device=dev, dtype=torch.int64)
+            io.covered_count = out["count"].data_ptr()
+            at = self.all_time_covered_targets
+            fuse_done = (at.dtype is torch.bool and at.is_contiguous() and at.shape == (B, T) and at.device == dev)
+            if fuse_done:
+                out["done"] = torch.empty(B, device=dev, dtype=torch.bool)
+                io.all_time, io.done = at.data_ptr(), out["done"].data_ptr()
             inplace = [self.shared_covering_rew] + [a.covering_reward for a in w.agents] + [a.collision_rew for a in w.agents]
             if any(t.dtype is not torch.float32 or not t.is_contiguous() or t.shape != (B,) or t.device != dev
                    for t in inplace):
@@ -309,6 +319,8 @@ class Scenario(BaseScenario):
             self.agents_targets_dists = out["dists"]
             self.agents_per_target, self.covered_targets = out["per_target"], out["covered"]
             self._fc = {"rew": dict(enumerate(out["rewards"])), "rew_key": self._rew_key()}
+            self._cov_count = (out["covered"], out["covered"]._version, out["count"])
+            self._fdone = (at, at._version, out["done"]) if fuse_done else None
         c = getattr(self, "_fc", None)
         if c is not None and i in c.get("rew", {}) and c["rew_key"] == self._rew_key():
             r = c["rew"].pop(i)
@@ -411,7 +423,12 @@ class Scenario(BaseScenario):
         return c[2]
 
     def done(self):
-        return self.all_time_covered_targets.all(dim=-1)
+        c = getattr(self, "_fdone", None)  # (computed by the reward launch, see _fused_reward)
+        self._fdone = None
+        at = self.all_time_covered_targets
+        if c is not None and c[0] is at and at._version == c[1]:
+            return c[2]
+        return at.all(dim=-1)
 
 
 class HeuristicPolicy(BaseHeuristicPolicy):
