@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define VMAS_ABI_VERSION 2
+/* v3: VmasDiscoveryIO gained covered_count / all_time / done; increment spans (src NULL) in
+ * vmas_copy_spans; VMAS_COPY_MAX_SPANS 160 */
+#define VMAS_ABI_VERSION 3
 
 /* error codes */
 #define VMAS_OK 0

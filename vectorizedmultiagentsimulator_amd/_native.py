@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("VMAS_LIB_PATH") or Path(__file__).resolve().pare
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
-VMAS_ABI_VERSION = 2
+VMAS_ABI_VERSION = 3
 VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
 (
     VMAS_PAIR_JOINT,
