@@ -602,11 +602,18 @@ class Environment(TorchVectorizedObject):
                 self._preapply = pre if pre is not None else (key, None)
             ok = self._preapply[1] is not None
         if ok:
-            _, u_out, u_rng, u_mul, strides = self._preapply
-            cols["u_out"], cols["u_stride"], cols["u_range"], cols["u_mult"] = u_out, strides, u_rng, u_mul
-            cols["u_clamp"] = int(bool(self.clamp_action))
+            # (the five column fields are written once per (column table, plan, clamp), not per draw)
+            # (the table itself in the tag, compared by identity: kept alive, its id cannot be reused)
+            tag = getattr(self, "_preapply_tag", None)
+            if tag is None or tag[0] is not cols or tag[1] != self._preapply[0] or tag[2] != bool(self.clamp_action):
+                tag = (cols, self._preapply[0], bool(self.clamp_action))
+                _, u_out, u_rng, u_mul, strides = self._preapply
+                cols["u_out"], cols["u_stride"], cols["u_range"], cols["u_mult"] = u_out, strides, u_rng, u_mul
+                cols["u_clamp"] = int(bool(self.clamp_action))
+                self._preapply_tag = tag
         elif cols["u_out"].any():
             cols["u_out"] = 0
+            self._preapply_tag = None
         return ok
 
     def _take_preapplied(self, actions) -> bool:
