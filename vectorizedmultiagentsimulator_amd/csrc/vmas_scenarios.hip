@@ -731,19 +731,38 @@ __global__ void __launch_bounds__(256) k_discovery_obs_fast(VmasDiscoveryIO io_a
         // the fully unrolled rays x entities body was ~35 KiB of straight-line code, each wave
         // streaming it through the instruction cache once
         // (the angles, loaded together up front, wait in the rays' own LDS slots)
+        // (rays in pairs: two rays' independent chains interleave -- at 4 waves per SIMD one chain
+        // at a time left the SIMDs waiting; the same operations per ray, in the same order)
 #pragma unroll
         for (int r = 0; r < RM; ++r)
             if (r < nr) S[w][row + col + r] = ang[(long)r * as1] + rot;
-#pragma unroll 1
-        for (int r = 0; r < nr; ++r) {
-            const float th = S[w][row + col + r];
-            float dc, ds;
+        auto sc = [](float th, float& ds, float& dc) {
             if (fabsf(th) < 256.f) {
                 ds = __sinf(th);
                 dc = __cosf(th);
             } else {
                 sincosf(th, &ds, &dc);
             }
+        };
+        int r = 0;
+#pragma unroll 1
+        for (; r + 1 < nr; r += 2) {
+            float dc0, ds0, dc1, ds1;
+            sc(S[w][row + col + r], ds0, dc0);
+            sc(S[w][row + col + r + 1], ds1, dc1);
+            float b0 = mr, b1 = mr;
+#pragma unroll
+            for (int e = 0; e < ME; ++e) {
+                if (e >= ne || !((mask >> e) & 1u)) continue;
+                b0 = min_drop_nan(b0, ray_sphere_fast_nan(T[e].x, T[e].y, C[e], dc0, ds0));
+                b1 = min_drop_nan(b1, ray_sphere_fast_nan(T[e].x, T[e].y, C[e], dc1, ds1));
+            }
+            S[w][row + col + r] = b0;
+            S[w][row + col + r + 1] = b1;
+        }
+        if (r < nr) {
+            float dc, ds;
+            sc(S[w][row + col + r], ds, dc);
             float best = mr;
 #pragma unroll
             for (int e = 0; e < ME; ++e) {
