@@ -632,7 +632,9 @@ class Environment(TorchVectorizedObject):
         if us is None:
             return False
         for i, ag in enumerate(self.agents):
-            ag.action.u = us[i]
+            act = ag.action
+            if act._u is not us[i]:  # (bound by the previous step already: the setter's checks passed)
+                act.u = us[i]
         self.preapplied_steps += 1
         return True
 
@@ -913,9 +915,13 @@ class Environment(TorchVectorizedObject):
 
     def _can_speculate(self) -> bool:
         c = self._apply_cache
-        return (self._SPECULATE and c is not None and c[1] is not None and c[1][6] >= 0 and len(self.agents) <= 8
-                and self._u_persist is not None and self._u_persist[0] is c
-                and all(ag.action.u_noise <= 0 for ag in self.agents))
+        if not (self._SPECULATE and c is not None and c[1] is not None and c[1][6] >= 0 and len(self.agents) <= 8
+                and self._u_persist is not None and self._u_persist[0] is c):
+            return False
+        for ag in self.agents:  # (the Action's own field: u_noise is a property per call)
+            if ag._action._u_noise > 0:
+                return False
+        return True
 
     def _speculative_flags_ok(self, seq: int) -> bool:
         """Waits for the flags of a speculative launch; True when every agent's actions pass."""
