@@ -179,3 +179,17 @@ def test_state_replacement_semantics():
     line.set_vel(torch.zeros(4, 2), batch_index=None)
     env.step([torch.zeros(4, 2) for _ in env.agents])
     assert float(line.state.pos[0, 1]) < 0.5  # fell under gravity from the new position
+
+
+def test_default_done_is_a_fresh_all_false_view_after_writes():
+    """BaseScenario.done (ref scenario.py:300-328): an all-False [batch_dim] view of one element;
+    the element is reused between calls, but a write through an earlier view does not leak into
+    later dones (a fresh element is made when its version counter moved)."""
+    env = make_env("flocking", num_envs=8, device="cpu", seed=0, n_agents=3)
+    d = env.scenario.done()
+    assert d.shape == (8,) and d.dtype == torch.bool and not d.any()
+    d[0].fill_(True)  # writes the shared element through a 0-d view
+    d2 = env.scenario.done()
+    assert not d2.any() and d2.data_ptr() != d.data_ptr()
+    _, _, dones, _ = env.step(env.get_random_actions())
+    assert dones.shape == (8,) and not dones.any()
