@@ -385,7 +385,11 @@ def main():
     math_mode = ("relaxed" if "VMAS_PHYS_RELAXED" in (src or "") else "exact") if on_gpu else "exact (host backend)"
     roofline = None
     if on_gpu and launches:
-        per_launch_ms = kernel_ms / launches
+        inkernel_ms = kernel_ms / launches
+        # the headline is the event-timed launch (what rocprofv3's kernel trace measures: dispatch
+        # to completion signal); the in-kernel timer (graph replays) misses the dispatch ramp and
+        # the exit tail, so it is reported beside it, not as the frac
+        per_launch_ms = event_us * 1e-3 if event_us else inkernel_ms
         achieved = b_env * args.envs / (per_launch_ms * 1e-3) / 1e9
         src_hash = kernel_source_hash(world)
         pmc = load_pmc(workload, world.engine.kernel_name, src_hash)
@@ -399,11 +403,13 @@ def main():
             "traffic": traffic,
             "kernel": world.engine.kernel_name,
             "kernel_us_per_launch": round(per_launch_ms * 1e3, 3),
+            "timer": ("HIP events on the dispatch packets of eager launches after the timed region "
+                      "(rocprofv3-consistent)") if event_us else timer,
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,
-            "timer": timer,
-            "kernel_us_event": round(event_us, 3) if event_us else None,
-            "frac_event": round(b_env * args.envs / (event_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5) if event_us else None,
+            "kernel_us_timed_region": round(inkernel_ms * 1e3, 3),
+            "timer_timed_region": timer,
+            "frac_timed_region": round(b_env * args.envs / (inkernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "kernel_source_sha256": src_hash,
             "pmc_record": ("profiles/pmc_traffic.json" if traffic else pmc.get("stale", "none")),
         }

@@ -330,6 +330,13 @@ typedef struct VmasUniformColumn {
 int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformColumn* cols,
                              int32_t n_cols, uint64_t seed, uint64_t offset, int32_t mode,
                              uint64_t* increment, void* stream);
+/* The same draw; with u_snap_delta != 0 every pre-applied element's previous value (u_out[i *
+ * u_stride] before this launch) is first stored u_snap_delta bytes from it: graph mode keeps the
+ * values agents' action.u / state.force show until the step that consumes the draw (the reference's
+ * get_random_action has no side effect on the agents, environment.py:524-582). */
+int32_t vmas_uniform_columns_snap(int32_t device, int64_t numel, const VmasUniformColumn* cols,
+                                  int32_t n_cols, uint64_t seed, uint64_t offset, int32_t mode,
+                                  int64_t u_snap_delta, uint64_t* increment, void* stream);
 
 /* Deferred device assertions for graph mode (csrc/vmas_actions.hip).  Replaces the host sync of
  * a reference assert on a device tensor inside the step -- Agent.action_callback's range check of

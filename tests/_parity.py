@@ -63,6 +63,11 @@ def summarize(config, env, reps, lidar=None):
         "certified_max_margin": max((r.get("certified_max_margin", 0.0) for r in reps), default=0.0),
         "certified_max_bound_frac": max((r.get("certified_max_bound_frac", 0.0) for r in reps), default=0.0),
         "max_abs": {k: max(r["max_abs"].get(k, 0.0) for r in reps) for k in reps[0]["max_abs"]} if reps else {},
+        # aggregate guards (max over the steps): p99.9 and mean over envs of the per-env max |diff|
+        "p999_abs": {k: max(r.get("p999_abs", {}).get(k, 0.0) for r in reps) for k in reps[0].get("p999_abs", {})}
+        if reps else {},
+        "mean_abs": {k: max(r.get("mean_abs", {}).get(k, 0.0) for r in reps) for k in reps[0].get("mean_abs", {})}
+        if reps else {},
         "band_max": {k: max(r.get("band_max", {}).get(k, 0.0) for r in reps) for k in reps[0].get("band_max", {})}
         if reps else {},
         "passes": [r.get("iterations") for r in reps],

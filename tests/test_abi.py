@@ -69,3 +69,17 @@ def test_invalid_arguments_return_errors_not_crashes():
     assert lib.vmas_world_create(None, None, None, None, ctypes.byref(h)) == -1
     assert b"null" in lib.vmas_last_error()
     assert lib.vmas_world_step(None, None, None, None) == -1
+
+
+def test_host_extension_loads():
+    """The _vmas_host torch extension (csrc/vmas_host.cpp: the host half of a graph-mode step)
+    loads next to the library and carries the library's ABI version (no GPU call is made)."""
+    h = N.load_host()
+    assert h.ABI_VERSION == N.VMAS_ABI_VERSION
+    assert hasattr(h, "OutputAlloc") and hasattr(h, "UniformDraw")
+    assert N.fn_addr("vmas_copy_spans") and N.fn_addr("vmas_uniform_columns")
+    import torch
+
+    ts = [torch.zeros(3), torch.zeros(2)]
+    ts[1].add_(1)
+    assert h.versions(ts) == (0, 1)

@@ -61,10 +61,16 @@ def test_sub_dt_attribute_host():
 
 
 @pytest.mark.gpu
-def test_features_full_size_gpu(gpu_device):
+@pytest.mark.parametrize("math", ["relaxed", "exact"])
+def test_features_full_size_gpu(gpu_device, monkeypatch, math):
+    """The same 16 384-env world and seed in both math modes: the relaxed / exact pair of PARITY
+    lines separates what relaxed math costs from the world's own conditioning (band_max)."""
+    if math == "exact":
+        monkeypatch.setenv("VMAS_JIT_MATH", "exact")
     env = make("features", dict(n_agents=8), None, gpu_device, num_envs=16384, seed=0)
     reps = step_parity(env, n_steps=2)
-    summarize("features 16384 envs n_agents=8", env, reps)
+    rec = summarize(f"features 16384 envs n_agents=8 {math}-math", env, reps)
+    assert rec["math"] == math
     for rep in reps:
         assert rep["ok"], rep
     assert env.world.engine.kernel_name == "k_world", env.world.engine.jit_error

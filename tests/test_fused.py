@@ -5,6 +5,7 @@ scenarios/): the same env stepped with the program forced to torch must give bit
 outputs, scenario attributes and world state, eagerly and replayed from a HIP graph, across
 reset_at / reset."""
 
+import math
 import pytest
 import torch
 
@@ -180,3 +181,42 @@ def test_fast_lidar_program_gpu(gpu_device, name, kw, lidar_cols):
         assert rep["ok"], (t, rep)
         worst = max(worst, rep["bad_rows"] / max(rep["rows"], 1))
     assert worst < 1e-3  # boundary rays are rare
+
+
+@pytest.mark.gpu
+def test_fast_lidar_rotated_agents_gpu(gpu_device):
+    """Agents turned by up to +-300 rad: the fast LIDAR's hardware sin / cos take the
+    angle in revolutions and lose |angle| * 2^-24 rad, so angles beyond 16 rad go through the
+    range-reduced sincosf; the measured rays stay within the oracle's LIDAR tolerance."""
+    from tests._parity import lidar_parity
+
+    env = make_env("flocking", num_envs=4096, device=gpu_device, seed=7, n_agents=5)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for a in env.world.agents:
+        rot = (torch.rand(4096, 1, generator=g) * 600.0 - 300.0).to(gpu_device)
+        a.set_rot(rot, batch_index=None)
+    for _ in range(2):
+        env.step(env.get_random_actions())
+        rep = lidar_parity(env, measured=True)
+        assert rep["ok"], rep
+        assert rep["bad_rows"] <= 4, rep
+
+
+@pytest.mark.gpu
+def test_relaxed_trig_large_rotation_gpu(gpu_device):
+    """Relaxed math (the GPU default of jointless worlds) with rotatable boxes and lines turned by
+    hundreds of radians (the reference never wraps rot, core.py:2907): one teacher-forced step
+    against the oracle (entity trig beyond 16 rad goes through the library sin / cos)."""
+    from oracle import vmas_oracle as O
+    from tests._parity import make
+
+    env = make("features", dict(n_agents=4), None, gpu_device, num_envs=2048, seed=2)
+    env.step(env.get_random_actions())
+    g = torch.Generator(device="cpu").manual_seed(1)
+    for e in env.world.entities:
+        if e.rotatable:
+            turns = torch.randint(-60, 61, (2048, 1), generator=g).float() * (2 * math.pi)
+            e.set_rot(e.state.rot + turns.to(gpu_device), batch_index=None)
+    rep = O.compare_one_step(env.world)
+    assert "VMAS_PHYS_RELAXED" in env.world.engine.jit_source()
+    assert rep["ok"], rep

@@ -91,8 +91,9 @@ def test_split_box_pairs_gpu(gpu_device, monkeypatch, split, name, kw, substeps)
 @pytest.mark.parametrize("name,kw,envs", [
     ("transport", dict(n_agents=4), 32768),                         # C3
     ("discovery", dict(n_agents=8, use_agent_lidar=True), 16384),   # C4
-    ("flocking", dict(n_agents=8), 32768),                          # C5 (per GPU)
-], ids=["C3_transport", "C4_discovery", "C5_flocking"])
+    ("flocking", dict(n_agents=8), 32768),                          # C5 (per-GPU shard of 8)
+    ("flocking", dict(n_agents=8), 262144),                         # C5 (the whole workload, one GPU)
+], ids=["C3_transport", "C4_discovery", "C5_flocking_shard", "C5_flocking_full"])
 def test_baseline_configs_full_size_gpu(gpu_device, name, kw, envs):
     """BASELINE.json configs C3-C5 at their full per-GPU sizes: teacher-forced step parity and
     LIDAR parity against the oracle (only certified cut-off envs may differ)."""

@@ -84,6 +84,7 @@ EXPORTED_SYMBOLS = (
     "vmas_apply_actions_launch",
     "vmas_apply_actions_flags",
     "vmas_uniform_columns",
+    "vmas_uniform_columns_snap",
     "vmas_assert_create",
     "vmas_assert_destroy",
     "vmas_assert_publish",
@@ -575,6 +576,9 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_uniform_columns.restype = _i32
     lib.vmas_uniform_columns.argtypes = [_i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64, ctypes.c_uint64, _i32,
                                          ctypes.POINTER(ctypes.c_uint64), _vp]
+    lib.vmas_uniform_columns_snap.restype = _i32
+    lib.vmas_uniform_columns_snap.argtypes = [_i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64, ctypes.c_uint64, _i32,
+                                              ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64), _vp]
     lib.vmas_assert_create.restype = _i32
     lib.vmas_assert_create.argtypes = [_i32, _i32, ctypes.POINTER(_vp)]
     lib.vmas_assert_destroy.restype = _i32
@@ -659,3 +663,35 @@ def jit_stats():
     c, n = ctypes.c_int64(0), ctypes.c_int64(0)
     load_library().vmas_jit_stats(ctypes.byref(c), ctypes.byref(n))
     return c.value, n.value
+
+
+# ---- the host half of a graph-mode step (csrc/vmas_host.cpp, the _vmas_host torch extension) -----
+HOST_EXT_PATH = Path(__file__).resolve().parent / "_vmas_host.so"
+_host = None
+
+
+def load_host():
+    """Load (once) and return the _vmas_host extension: the per-step host work of a replayed step
+    (fresh outputs + the post-replay copy launch, the random-action draw) in C++.  Raises
+    NativeLibraryError if it is missing -- graph mode on a GPU has no Python stand-in for it."""
+    global _host
+    if _host is not None:
+        return _host
+    if not HOST_EXT_PATH.exists():
+        raise NativeLibraryError(
+            f"{HOST_EXT_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    import importlib.util
+
+    load_library()  # (first: the extension calls into this library through the pointers below)
+    spec = importlib.util.spec_from_file_location("_vmas_host", HOST_EXT_PATH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if mod.ABI_VERSION != VMAS_ABI_VERSION:
+        raise NativeLibraryError(f"_vmas_host ABI {mod.ABI_VERSION} != library ABI {VMAS_ABI_VERSION}")
+    _host = mod
+    return mod
+
+
+def fn_addr(name: str) -> int:
+    """Address of a C entry point of the loaded library (handed to _vmas_host)."""
+    return ctypes.cast(getattr(load_library(), name), ctypes.c_void_p).value

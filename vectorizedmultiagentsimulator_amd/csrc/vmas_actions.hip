@@ -232,6 +232,7 @@ struct UniformArgs {
     VmasUniformColumn c[kMaxUniformCols];
     unsigned long long seed;
     long long numel;
+    long long snap;  // bytes from a pre-applied element to its snapshot slot (0: no snapshot)
     int mode;  // bit 0: fused (0, 1] mapping; bit 1: fused affine transform
 };
 
@@ -262,7 +263,9 @@ __global__ void __launch_bounds__(kUniformThreads) k_uniform_columns(UniformArgs
                 col.out[li * col.stride] = x;
                 if (col.u_out) {  // apply_one's operations on the same value
                     const float v = col.u_clamp ? fminf(fmaxf(x, -col.u_range), col.u_range) : x;
-                    col.u_out[li * col.u_stride] = v * col.u_mult;
+                    float* uo = col.u_out + li * col.u_stride;
+                    if (a.snap) *reinterpret_cast<float*>(reinterpret_cast<char*>(uo) + a.snap) = *uo;
+                    *uo = v * col.u_mult;
                 }
             }
         }
@@ -362,6 +365,12 @@ int32_t vmas_apply_actions(int32_t device, int32_t batch, const VmasActionApplyR
 
 int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformColumn* cols, int32_t n_cols,
                              uint64_t seed, uint64_t offset, int32_t mode, uint64_t* increment, void* stream) {
+    return vmas_uniform_columns_snap(device, numel, cols, n_cols, seed, offset, mode, 0, increment, stream);
+}
+
+int32_t vmas_uniform_columns_snap(int32_t device, int64_t numel, const VmasUniformColumn* cols, int32_t n_cols,
+                                  uint64_t seed, uint64_t offset, int32_t mode, int64_t u_snap_delta,
+                                  uint64_t* increment, void* stream) {
     if (device < 0 || device >= 64 || numel <= 0 || n_cols <= 0 || n_cols > kMaxUniformCols || !cols ||
         !increment || mode < 0 || mode > 3)
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_uniform_columns: bad arguments");
@@ -383,6 +392,7 @@ int32_t vmas_uniform_columns(int32_t device, int64_t numel, const VmasUniformCol
     }
     a.seed = seed;
     a.numel = numel;
+    a.snap = u_snap_delta;
     a.mode = mode;
     int cur = -1;
     VMAS_AUX_HIP(hipGetDevice(&cur));

@@ -24,6 +24,13 @@ int32_t wait_host_word(const uint32_t* word, uint32_t seq, hipStream_t stream);
 // published by the same single store); the whole word goes to *value.
 int32_t wait_host_word64(const uint64_t* word, uint32_t seq, uint64_t* value, hipStream_t stream);
 
+// Sets n_words 32-bit words at dst to value, stream-ordered, as a KERNEL launch (vmas_copy.hip).
+// Used in place of hipMemsetAsync wherever the call can sit on a captured stream: a memset node
+// of a captured graph misbehaved twice on ROCm 7.2 / MI355X ("Graph mode": a node
+// found not complete before the next kernel, and words left holding pointer-like data), while a
+// kernel node is ordered and parameterised like every other node of the graph.
+hipError_t fill_u32_async(void* dst, uint32_t value, size_t n_words, hipStream_t stream);
+
 }  // namespace vmas_aux
 
 #define VMAS_AUX_HIP(x)                                                                               \

@@ -56,7 +56,22 @@ __global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) {
         copy_units(reinterpret_cast<const uint8_t*>(s.src), reinterpret_cast<uint8_t*>(s.dst), s.nbytes);
 }
 
+constexpr int kFillThreads = 256;
+
+__global__ void __launch_bounds__(kFillThreads) k_fill_u32(uint32_t* __restrict__ dst, uint32_t value, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kFillThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kFillThreads)
+        dst[i] = value;
+}
+
 }  // namespace
+
+hipError_t vmas_aux::fill_u32_async(void* dst, uint32_t value, size_t n_words, hipStream_t stream) {
+    if (n_words == 0) return hipSuccess;
+    const int64_t n = (int64_t)n_words;
+    const int gx = (int)std::min<int64_t>(1024, (n + kFillThreads - 1) / kFillThreads);
+    hipLaunchKernelGGL(k_fill_u32, dim3(gx), dim3(kFillThreads), 0, stream, (uint32_t*)dst, value, n);
+    return hipGetLastError();
+}
 
 extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, void* stream) {
     if (n < 0 || (n > 0 && !spans) || device < 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad arguments");

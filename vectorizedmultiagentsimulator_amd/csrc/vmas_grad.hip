@@ -688,7 +688,7 @@ extern "C" int32_t vmas_world_step_vjp(const VmasWorldConfig* cfg, const VmasEnt
     ga.n_blocks = n_blocks;
     int32_t rc = VMAS_OK;
     for (int it = 0; batch_bp && it < S + 2; ++it) {  // the forward's fixed point (R/Z rule)
-        VMAS_AUX_HIP(hipMemsetAsync(ga.R, 0, 8 * nwords, stream));
+        VMAS_AUX_HIP(vmas_aux::fill_u32_async(ga.R, 0u, 2 * (size_t)nwords, stream));
         ga.value_pass = true;
         hipLaunchKernelGGL(k_grad, dim3((B + 63) / 64), dim3(64), 0, stream, ga);
         VMAS_AUX_HIP(hipGetLastError());

@@ -1,0 +1,214 @@
+// vmas_host.cpp -- the host half of a graph-mode step in C++ (a torch extension, _vmas_host):
+// the per-step work between two replays that runs no simulation code but, written in Python,
+// took more host time than the GPU took for the whole step ("Graph mode: host path"):
+//
+//   * OutputAlloc: the fresh output tensors of a replayed step (the reference returns new tensors
+//     every step, environment.py:394-412).  Per (dtype, shape) group one allocation [n, *shape]
+//     split into its n tensors, the address of every member written into the post-replay copy
+//     table (VmasCopySpan rows, simulator/environment/_graph.py _post_table), then ONE
+//     vmas_copy_spans launch for the outputs, the carried state and the backups.
+//   * UniformDraw: Environment.get_random_actions for continuous actions on a GPU (environment.py:
+//     524-606): one [A, B, n] allocation split per agent, the column table's output addresses, one
+//     vmas_uniform_columns launch at the device generator's (seed, offset) and the offset advanced
+//     exactly as the reference's per-column uniform_ calls advance it.
+//
+// Nothing here decides anything the Python layer does not: the plans are built there (once per
+// capture / table) and these objects only replay them.  The C ABI entry points are called through
+// function pointers handed over from the ctypes binding (_native.py), so the extension shares the
+// one loaded libvmas_mi355x.so and its state.
+#include <torch/extension.h>
+
+#include <ATen/hip/HIPGeneratorImpl.h>
+#include <c10/hip/HIPStream.h>
+
+#include <cstdint>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "vmas_mi355x.h"
+
+namespace py = pybind11;
+
+namespace {
+
+using CopySpansFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, void*);
+using UniformColumnsSnapFn = int32_t (*)(int32_t, int64_t, const VmasUniformColumn*, int32_t, uint64_t, uint64_t,
+                                         int32_t, int64_t, uint64_t*, void*);
+using LastErrorFn = const char* (*)(void);
+
+void* current_stream(int device) {
+    return (void*)c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+}
+
+// One (dtype, shape) group of a step's outputs: `n` tensors of `shape`, allocated as [n, *shape];
+// members `contig[k]` get table row r0 + (their rank among the contiguous members).
+struct Group {
+    std::vector<int64_t> shape;  // [n, *shape]
+    at::ScalarType dtype;
+    int64_t n = 0;
+    int64_t r0 = 0;
+    std::vector<int64_t> row_members;  // member index of each table row r0, r0 + 1, ...
+    int64_t member_bytes = 0;
+};
+
+class OutputAlloc {
+public:
+    // groups: [(sample tensor of the group's dtype, shape tuple, n, r0, [member index per row])]
+    // table: the copy table (numpy, VmasCopySpan rows), kept alive here
+    OutputAlloc(int device, py::list groups, py::object table, int64_t table_addr, int64_t copy_fn,
+                int64_t last_error_fn)
+        : device_(device), table_(std::move(table)), tbl_((VmasCopySpan*)table_addr),
+          copy_((CopySpansFn)copy_fn), last_error_((LastErrorFn)last_error_fn) {
+        for (py::handle g : groups) {
+            py::tuple t = g.cast<py::tuple>();
+            Group gr;
+            gr.dtype = t[0].cast<at::Tensor>().scalar_type();
+            std::vector<int64_t> shape = t[1].cast<std::vector<int64_t>>();
+            gr.n = t[2].cast<int64_t>();
+            gr.r0 = t[3].cast<int64_t>();
+            gr.row_members = t[4].cast<std::vector<int64_t>>();
+            int64_t numel = 1;
+            for (int64_t s : shape) numel *= s;
+            gr.member_bytes = numel * (int64_t)c10::elementSize(gr.dtype);
+            gr.shape.push_back(gr.n);
+            gr.shape.insert(gr.shape.end(), shape.begin(), shape.end());
+            groups_.push_back(std::move(gr));
+        }
+        opts_ = at::TensorOptions().device(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+    }
+
+    // Fresh tensors of every group (in group order, members in order), their addresses written
+    // into the table's output rows.
+    std::vector<at::Tensor> alloc() {
+        std::vector<at::Tensor> out;
+        out.reserve(count());
+        for (const Group& g : groups_) {
+            at::Tensor buf = at::empty(g.shape, opts_.dtype(g.dtype));
+            const uintptr_t base = (uintptr_t)buf.data_ptr();
+            for (size_t r = 0; r < g.row_members.size(); ++r)
+                tbl_[g.r0 + (int64_t)r].dst = (void*)(base + (uintptr_t)(g.row_members[r] * g.member_bytes));
+            for (int64_t k = 0; k < g.n; ++k) out.push_back(buf.select(0, k));
+        }
+        return out;
+    }
+
+    // One vmas_copy_spans launch of table rows [lo, hi) on the current stream.
+    void launch(int64_t lo, int64_t hi) {
+        if (hi <= lo) return;
+        const int32_t rc = copy_(device_, tbl_ + lo, (int32_t)(hi - lo), current_stream(device_));
+        if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans failed: ") + last_error_());
+    }
+
+    // alloc() then the launches: rows [0, mid) and [mid, hi) as two launches when mid > 0 (outputs
+    // that lie in a carry destination are copied before the carry), else [0, hi) as one.
+    std::vector<at::Tensor> post(int64_t mid, int64_t hi) {
+        std::vector<at::Tensor> out = alloc();
+        if (mid > 0) {
+            launch(0, mid);
+            launch(mid, hi);
+        } else {
+            launch(0, hi);
+        }
+        return out;
+    }
+
+    int64_t count() const {
+        int64_t n = 0;
+        for (const Group& g : groups_) n += g.n;
+        return n;
+    }
+
+private:
+    int device_;
+    py::object table_;
+    VmasCopySpan* tbl_;
+    CopySpansFn copy_;
+    LastErrorFn last_error_;
+    std::vector<Group> groups_;
+    at::TensorOptions opts_;
+};
+
+class UniformDraw {
+public:
+    // n_agents tensors [B, width] of one [n_agents, B, width] allocation; column k's output is
+    // out_offs[k] bytes into it (its `out` field in the column table at cols_addr)
+    UniformDraw(int device, int64_t batch, int64_t n_agents, int64_t width, py::object cols, int64_t cols_addr,
+                int64_t n_cols, std::vector<int64_t> out_offs, int mode, int64_t uniform_fn, int64_t last_error_fn)
+        : device_(device), batch_(batch), n_agents_(n_agents), width_(width), cols_obj_(std::move(cols)),
+          cols_((VmasUniformColumn*)cols_addr), n_cols_(n_cols), out_offs_(std::move(out_offs)), mode_(mode),
+          uniform_((UniformColumnsSnapFn)uniform_fn), last_error_((LastErrorFn)last_error_fn) {
+        if ((int64_t)out_offs_.size() != n_cols_) throw std::invalid_argument("UniformDraw: one offset per column");
+        opts_ = at::TensorOptions().device(at::Device(at::kCUDA, (c10::DeviceIndex)device)).dtype(at::kFloat);
+    }
+
+    // snap_numel > 0: the pre-applied columns' previous values (the buffer of snap_numel floats at
+    // snap_base that agents' actions view) are first copied into a fresh buffer, returned second
+    // (vmas_uniform_columns_snap)
+    std::pair<std::vector<at::Tensor>, c10::optional<at::Tensor>> draw(int64_t snap_base, int64_t snap_numel) {
+        at::Tensor buf = at::empty({n_agents_, batch_, width_}, opts_);
+        const uintptr_t base = (uintptr_t)buf.data_ptr();
+        for (int64_t k = 0; k < n_cols_; ++k) cols_[k].out = (float*)(base + (uintptr_t)out_offs_[k]);
+        c10::optional<at::Tensor> snap;
+        int64_t delta = 0;
+        if (snap_numel > 0) {
+            snap = at::empty({snap_numel}, opts_);
+            delta = (int64_t)((uintptr_t)snap->data_ptr() - (uintptr_t)snap_base);
+        }
+        at::Generator gen = at::cuda::detail::getDefaultCUDAGenerator((c10::DeviceIndex)device_);
+        {
+            // (the generator's own lock, as torch's distribution kernels take it)
+            std::lock_guard<std::mutex> lock(gen.mutex());
+            auto* impl = gen.get<at::CUDAGeneratorImpl>();
+            const uint64_t off = impl->get_offset();
+            uint64_t inc = 0;
+            const int32_t rc = uniform_(device_, batch_, cols_, (int32_t)n_cols_, impl->current_seed(), off, mode_,
+                                        delta, &inc, current_stream(device_));
+            if (rc != VMAS_OK)
+                throw std::runtime_error(std::string("vmas_uniform_columns failed: ") + last_error_());
+            impl->set_offset(off + inc);
+        }
+        std::vector<at::Tensor> out;
+        out.reserve(n_agents_);
+        for (int64_t a = 0; a < n_agents_; ++a) out.push_back(buf.select(0, a));
+        return {std::move(out), std::move(snap)};
+    }
+
+private:
+    int device_;
+    int64_t batch_, n_agents_, width_;
+    py::object cols_obj_;
+    VmasUniformColumn* cols_;
+    int64_t n_cols_;
+    std::vector<int64_t> out_offs_;
+    int mode_;
+    UniformColumnsSnapFn uniform_;
+    LastErrorFn last_error_;
+    at::TensorOptions opts_;
+};
+
+// (tensor._version of each, as a tuple: the version snapshots of the post-replay bookkeeping)
+py::tuple versions(const std::vector<at::Tensor>& ts) {
+    py::tuple out(ts.size());
+    for (size_t i = 0; i < ts.size(); ++i) out[i] = py::int_((int64_t)ts[i]._version());
+    return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_vmas_host, m) {
+    m.doc() = "Host path of a graph-mode step in C++ (csrc/vmas_host.cpp)";
+    m.attr("ABI_VERSION") = VMAS_ABI_VERSION;
+    py::class_<OutputAlloc>(m, "OutputAlloc")
+        .def(py::init<int, py::list, py::object, int64_t, int64_t, int64_t>())
+        .def("alloc", &OutputAlloc::alloc)
+        .def("launch", &OutputAlloc::launch)
+        .def("post", &OutputAlloc::post)
+        .def("count", &OutputAlloc::count);
+    py::class_<UniformDraw>(m, "UniformDraw")
+        .def(py::init<int, int64_t, int64_t, int64_t, py::object, int64_t, int64_t, std::vector<int64_t>, int, int64_t,
+                      int64_t>())
+        .def("draw", &UniformDraw::draw);
+    m.def("versions", &versions);
+}

@@ -1518,7 +1518,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     W->last_persistent = persistent;
     const size_t nwords = (size_t)io->substeps * W->W;
     // (the persistent kernel's control words need no reset: global pass numbers, vmas_jit_ops.hpp)
-    if (!persistent) JHIP(hipMemsetAsync(W->d_mask, 0, nwords * 4, stream));
+    if (!persistent) JHIP(vmas_aux::fill_u32_async(W->d_mask, 0u, nwords, stream));
     // Timing (vmas_jit_world_set_timing): the events ride on the kernel's own dispatch packet
     // (hipExtModuleLaunchKernel), so they bracket its execution alone, as rocprofv3's kernel
     // trace does -- events recorded around a launch on an idle queue also count the dispatch gap.

@@ -1207,7 +1207,7 @@ int32_t vmas_world_step(VmasWorld* W, const VmasStepIO* io, void* stream_, int32
     const size_t flags_bytes = align_up((size_t)2 * io->substeps * W->W * 4, 16);
     const size_t lds = flags_bytes + (W->global_scratch ? 0 : W->lds_state_floats * 4);
     const size_t nwords = (size_t)io->substeps * W->W;
-    HIP_TRY(hipMemsetAsync(W->d_mask, 0xFF, nwords * 4, stream));
+    HIP_TRY(vmas_aux::fill_u32_async(W->d_mask, 0xFFFFFFFFu, nwords, stream));
     const int max_it = batch_bp ? io->substeps + 2 : 1;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(stream, &cap));
@@ -1351,7 +1351,7 @@ int32_t vmas_check_actions(int32_t device, int32_t batch, const VmasActionRef* r
     }
     const void* dref = nullptr;
     if (int32_t rc = ring_upload(device, refs, sizeof(VmasActionRef) * n_refs, stream, &dref)) return rc;
-    HIP_TRY(hipMemsetAsync(cs->d_flags, 0, 8 * n_refs, stream));
+    HIP_TRY(vmas_aux::fill_u32_async(cs->d_flags, 0u, 2 * (size_t)n_refs, stream));
     const long per = (long)batch * 2;
     const unsigned gx = (unsigned)std::max(1L, std::min(64L, (per + 4095) / 4096));
     hipLaunchKernelGGL(k_check_actions, dim3(gx, n_refs), dim3(256), 0, stream, (const VmasActionRef*)dref,

@@ -83,8 +83,12 @@ VHD Real tclamp(Real x, Real lo, Real hi) { return tmin(tmax(x, lo), hi); }
 // double-float log1pf (~110 VALU instructions per contact) and its range-reduced sin/cos
 // (~100 each).  Every other build keeps the correctly rounded library functions.
 #ifdef VMAS_PHYS_RELAXED
-VHD Real tsin(Real x) { return __sinf(x); }
-VHD Real tcos(Real x) { return __cosf(x); }
+// v_sin / v_cos_f32 take revolutions: the x * (1 / 2 pi) product rounds to |x| * 2^-24 rad (1e-6
+// rad at 16 rad) and the instructions' domain ends at 256 revolutions.  The reference never wraps
+// an entity's rotation (core.py:2907), so a spinning body's angle grows without bound: beyond
+// 16 rad the correctly rounded library functions (a lane-divergent branch, taken only then).
+VHD Real tsin(Real x) { return fabsf(x) < 16.f ? __sinf(x) : sinf(x); }
+VHD Real tcos(Real x) { return fabsf(x) < 16.f ? __cosf(x) : cosf(x); }
 VHD Real tlog1p(Real y) {
     const Real u = 1.f + y;
     return u == 1.f ? y : __logf(u) * (y / (u - 1.f));

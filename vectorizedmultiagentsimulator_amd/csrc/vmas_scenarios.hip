@@ -19,6 +19,12 @@ using namespace vmas;
 
 namespace {
 
+// __sinf / __cosf (v_sin_f32 / v_cos_f32) take the angle in revolutions: x * (1 / 2 pi) rounds to
+// |x| * 2^-24 rad, i.e. 1e-6 rad at 16 rad (the LIDAR certification's turn, tests/_parity.py) and
+// 1.5e-5 rad at 256.  Below this bound the fast LIDAR programs use them; above it ocml's
+// range-reduced sincosf.  (Ray angles are the sensor's [0, 2 pi) plus the agent's rotation.)
+constexpr float kFastTrigMaxAngle = 16.f;
+
 __device__ __forceinline__ V2 ld_vec2(const VmasVec& v, int b) {
     return mk(v.p[(long)b * v.s0], v.p[(long)b * v.s0 + v.s1]);
 }
@@ -326,11 +332,10 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const float a = A[r] + rot;
-                // hardware sin / cos (v_sin / v_cos_f32: a few 1e-7 rad at these angles, within
-                // the LIDAR certification's 1e-6 rad) instead of ocml's range-reduced sincosf;
-                // large angles keep sincosf
+                // hardware sin / cos (v_sin / v_cos_f32) below kFastTrigMaxAngle, ocml's
+                // range-reduced sincosf above (see kFastTrigMaxAngle)
                 float ds, dc;
-                if (fabsf(a) < 256.f) {
+                if (fabsf(a) < kFastTrigMaxAngle) {
                     ds = __sinf(a);
                     dc = __cosf(a);
                 } else {
@@ -352,7 +357,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
             for (int r = 0; r < nr; ++r) {
                 const float a = S[w][row + 6 + r];
                 float ds, dc;
-                if (fabsf(a) < 256.f) {
+                if (fabsf(a) < kFastTrigMaxAngle) {
                     ds = __sinf(a);
                     dc = __cosf(a);
                 } else {
@@ -737,7 +742,7 @@ __global__ void __launch_bounds__(256) k_discovery_obs_fast(VmasDiscoveryIO io_a
         for (int r = 0; r < RM; ++r)
             if (r < nr) S[w][row + col + r] = ang[(long)r * as1] + rot;
         auto sc = [](float th, float& ds, float& dc) {
-            if (fabsf(th) < 256.f) {
+            if (fabsf(th) < kFastTrigMaxAngle) {
                 ds = __sinf(th);
                 dc = __cosf(th);
             } else {

@@ -661,7 +661,7 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
         VMAS_AUX_HIP(hipHostMalloc((void**)&s.h_out, 2 * sizeof(int32_t), hipHostMallocDefault));
     }
     hipStream_t st = (hipStream_t)stream;
-    VMAS_AUX_HIP(hipMemsetAsync(s.d_out, 0, 2 * sizeof(int32_t), st));
+    VMAS_AUX_HIP(vmas_aux::fill_u32_async(s.d_out, 0u, 2, st));
     hipLaunchKernelGGL(k_spawn_resolve, dim3((batch + 255) / 256), dim3(256), 0, st, a, s.d_out);
     VMAS_AUX_HIP(hipGetLastError());
     VMAS_AUX_HIP(hipMemcpyAsync(s.h_out, s.d_out, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));

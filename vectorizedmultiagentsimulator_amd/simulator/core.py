@@ -184,6 +184,11 @@ def _check_state_set(obj, value: Tensor):
 
 
 class EntityState(TorchVectorizedObject):
+    # graph mode: the StepGraph's _FreshState (simulator/environment/_graph.py) -- after a replay
+    # the first read of a state attribute re-binds the states to fresh tensors, as the reference's
+    # integration creates new ones every step (core.py:2866-2907)
+    _fresh = None
+
     def __init__(self):
         super().__init__()
         self._pos = None
@@ -193,6 +198,9 @@ class EntityState(TorchVectorizedObject):
 
     @property
     def pos(self):
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._pos
 
     @pos.setter
@@ -206,6 +214,9 @@ class EntityState(TorchVectorizedObject):
 
     @property
     def vel(self):
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._vel
 
     @vel.setter
@@ -219,6 +230,9 @@ class EntityState(TorchVectorizedObject):
 
     @property
     def ang_vel(self):
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._ang_vel
 
     @ang_vel.setter
@@ -228,6 +242,9 @@ class EntityState(TorchVectorizedObject):
 
     @property
     def rot(self):
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._rot
 
     @rot.setter
@@ -273,8 +290,16 @@ class AgentState(EntityState):
         _check_state_set(self, c)
         self._c = c.to(self._device)
 
+    _shadow = None  # graph mode: the environment's _ActionShadow (see Action.u)
+
     @property
     def force(self):
+        sh = self._shadow
+        if sh is not None and sh.active:
+            return sh.view(self._force)
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._force
 
     @force.setter
@@ -284,6 +309,9 @@ class AgentState(EntityState):
 
     @property
     def torque(self):
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._torque
 
     @torque.setter
@@ -340,8 +368,21 @@ class Action(TorchVectorizedObject):
                     " (one per action) all with same length"
                 )
 
+    # Graph mode: between a random-action draw that pre-applies its actions into the persistent
+    # action buffer and the step that consumes them, u (and a holonomic agent's state.force, a view
+    # of u) shows the draw's snapshot of the buffer -- the values of the last step, as the
+    # reference, whose draw leaves the agents alone (environment/environment.py _ActionShadow).
+    _shadow = None
+    _fresh = None  # graph mode: see EntityState._fresh
+
     @property
     def u(self):
+        sh = self._shadow
+        if sh is not None and sh.active:
+            return sh.view(self._u)
+        f = self._fresh
+        if f is not None and f.pending:
+            f.materialize()
         return self._u
 
     @u.setter

@@ -349,6 +349,112 @@ class _Segments:
         return res
 
 
+_STATE_KEYS = ("_pos", "_vel", "_rot", "_ang_vel", "_force", "_torque")
+
+
+class _FreshState:
+    """Fresh entity-state tensors after every replay, made on first use.
+
+    A replay writes the integrated state into the same graph-pool tensors Y every step, and the
+    entity states stay bound to views of Y.  The reference creates new state tensors every step
+    (core.py:2866-2907): a reference kept to ``entity.state.pos`` from an earlier step keeps that
+    step's values.  So after each replay this holder is marked pending, and the first read of any
+    entity state attribute (EntityState / AgentState getters) materialises the step: every carried
+    state attribute is re-bound to a view of a fresh copy F of its Y storage (one vmas_copy_spans
+    launch, stream-ordered between this replay and the next).  Until then a step costs nothing
+    extra.  Before the next replay (StepGraph.before_actions) the attributes are bound back to Y;
+    if F was written in place meanwhile (reset_at -> set_pos(batch_index)) F is copied back to Y
+    first.  References the caller kept point into F and keep their values."""
+
+    def __init__(self, graph: "StepGraph", items, persist_items=()):
+        self.g = graph
+        self.items = items  # [(state object's __dict__, key, the Y view bound after the capture)]
+        # agents' action._u / a holonomic state._force: views of the persistent action buffer P
+        # (the same views every step, not carried); fresh copies of P on first use, never copied
+        # back (every step rewrites P from its actions)
+        self.persist_items = list(persist_items)
+        self.pending = False
+        self.bound = None  # after materialize: ([(dict, key, y, f)], [(F, version, Y bytes, F bytes)])
+
+    def materialize(self) -> None:
+        self.pending = False
+        if self.bound is not None:
+            return
+        by_storage: Dict[int, list] = {}
+        for d, k, y in self.items:
+            if d.get(k) is y:  # (an attribute the caller re-bound keeps the caller's tensor)
+                by_storage.setdefault(_storage_key(y), []).append((d, k, y))
+        items, stor, spans = [], [], []
+        self._materialize_persist(items, spans)
+        for _, group in by_storage.items():
+            y0 = group[0][2]
+            ys = y0.untyped_storage()
+            nb = ys.nbytes()
+            if all(y.dtype is torch.float32 for _, _, y in group) and nb % 4 == 0:
+                f = torch.empty(nb // 4, dtype=torch.float32, device=y0.device)
+                for d, k, y in group:
+                    v = f.as_strided(y.shape, y.stride(), y.storage_offset())
+                    d[k] = v
+                    items.append((d, k, y, v))
+            else:  # (mixed dtypes: one byte buffer, a view of it per attribute)
+                f = torch.empty(nb, dtype=torch.uint8, device=y0.device)
+                for d, k, y in group:
+                    v = torch.empty(0, dtype=y.dtype, device=y.device).set_(
+                        f.untyped_storage(), y.storage_offset(), y.shape, y.stride())
+                    d[k] = v
+                    items.append((d, k, y, v))
+            spans.append((ys.data_ptr(), f.data_ptr(), nb))
+            stor.append((f, ys.data_ptr(), nb, items[-len(group):]))
+        if spans:
+            N.copy_raw(self.g._dev_index(), spans, self.g._stream())
+        self.bound = (items, [(f, tuple(map(_VERSION, [v for *_, v in its])), yp, nb) for f, yp, nb, its in stor])
+
+    def _materialize_persist(self, items, spans) -> None:
+        env = self.g.env
+        pc = env._u_persist
+        if not self.persist_items or pc is None:
+            return
+        P = pc[1]
+        live = [(d, k, y) for d, k, y in self.persist_items
+                if d.get(k) is y and y.untyped_storage().data_ptr() == P.untyped_storage().data_ptr()]
+        if not live:
+            return
+        sh = env._ushadow
+        if sh.active:  # (a draw already rewrote P: its snapshot, itself a fresh tensor, holds the step's values)
+            for d, k, y in live:
+                v = sh.view(y)
+                d[k] = v
+                items.append((d, k, y, v))
+            return
+        f = torch.empty(P.numel(), dtype=torch.float32, device=P.device)
+        spans.append((P.data_ptr(), f.data_ptr(), 4 * P.numel()))
+        base = P.storage_offset()
+        for d, k, y in live:
+            v = f.as_strided(y.shape, y.stride(), y.storage_offset() - base)
+            d[k] = v
+            items.append((d, k, y, v))
+
+    def unbind(self) -> bool:
+        """Bind the attributes back to Y before a replay; F copied back to Y where it was written
+        in place.  Returns whether Y changed."""
+        self.pending = False
+        b, self.bound = self.bound, None
+        if b is None:
+            return False
+        items, stor = b
+        spans = []
+        for f, vers, yp, nb in stor:
+            its = [v for (_, _, _, v) in items if v.untyped_storage().data_ptr() == f.untyped_storage().data_ptr()]
+            if tuple(map(_VERSION, its)) != vers:
+                spans.append((f.data_ptr(), yp, nb))
+        if spans:
+            N.copy_raw(self.g._dev_index(), spans, self.g._stream())
+        for d, k, y, v in items:
+            if d.get(k) is v:
+                d[k] = y
+        return bool(spans)
+
+
 class StepGraph:
     """Capture / replay state of one Environment (see the module docstring)."""
 
@@ -385,6 +491,7 @@ class StepGraph:
         self._folding = False
         self._steps_folded = False
         self._steps_t = None
+        self._fresh: Optional[_FreshState] = None  # fresh entity states on first use after a replay
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -409,6 +516,10 @@ class StepGraph:
         self.copied = False
         if self.graph is None:
             return
+        fr = self._fresh
+        if fr is not None and fr.bound is not None and fr.unbind():
+            self.copied = True  # (Y written from F: the carry Y -> X runs again)
+            self._post = None
         self.env.world.engine.check_device_errors()
         if not self._still_valid():
             self.drop("world or entity parameters changed")
@@ -544,6 +655,12 @@ class StepGraph:
             raise err
 
     def drop(self, why: str):
+        fr, self._fresh = self._fresh, None
+        if fr is not None:  # (eager steps read the attributes as bound: F views hold the values)
+            fr.pending = False
+            for d, k, y in fr.items + fr.persist_items:
+                if d.get("_fresh") is fr:
+                    d.pop("_fresh")
         self._finish_deferred(apply=False)
         self._deferred = []
         self.graph = None
@@ -666,6 +783,19 @@ class StepGraph:
         del contents
         self._steps_folded, self._folding = self._folding, False
         self._steps_t = env.steps
+        persist = []
+        pc = env._u_persist
+        if pc is not None and pc[2] is not None:
+            pkey = _storage_key(pc[1])
+            for ag in env.world.agents:
+                for o, k in ((ag._action, "_u"), (ag._state, "_force")):
+                    t = o.__dict__.get(k)
+                    if isinstance(t, Tensor) and _storage_key(t) == pkey:
+                        persist.append((o.__dict__, k, t))
+        if (self._fresh_items or persist) and self._FRESH_STATES:
+            self._fresh = _FreshState(self, self._fresh_items, persist)
+            for d, _, _ in self._fresh_items + persist:
+                d["_fresh"] = self._fresh
         self._deferred = deferred
         self.graph = g
         self._segments, self._holes = segs.graphs, segs.holes
@@ -681,6 +811,7 @@ class StepGraph:
     def _plan(self, objs, snap, out):
         carry: List[Tuple[Tensor, Tensor]] = []
         names: List[str] = []
+        fresh = []  # carried entity-state attributes: re-bound to fresh tensors on first use (_FreshState)
         for o, before in snap:
             after = o.__dict__
             for k, v0 in before.items():
@@ -697,6 +828,8 @@ class StepGraph:
                     continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
                 carry.append((v0, v1))
                 names.append(f"{type(o).__name__}.{k}")
+                if k in _STATE_KEYS and hasattr(type(o), "_fresh"):  # (an EntityState / AgentState)
+                    fresh.append((after, k, v1))
         self._carry_ys = [y for _, y in carry]
         x_keys = {_storage_key(x): n for (x, _), n in zip(carry, names)}
         for (_, y), n in zip(carry, names):
@@ -741,6 +874,7 @@ class StepGraph:
                     self._watch.append((d, k, v))
         self._watch_cols = (tuple(d for d, _, _ in self._watch), tuple(k for _, k, _ in self._watch),
                             tuple(t for _, _, t in self._watch))
+        self._fresh_items = fresh
         self._out_tree = out
         # an output marked constant (BaseScenario.done's all-False view of one element made outside
         # the capture, which no replay writes) is copied from a contiguous copy made once here:
@@ -757,6 +891,8 @@ class StepGraph:
         that captured random ops read); if it did not advance the device generator, the graph
         draws no random numbers and later replays launch the instantiated graph directly
         (vmas_graph_launch), without the prologue's two fill kernels."""
+        if self._fresh is not None:  # (this replay's states: fresh tensors on first use)
+            self._fresh.pending = True
         for d in self._deferred:  # the generator state the captured launches read
             d.arm()
         if self._holes:  # segmented step: graph, host hole, graph, ... (torch replays)
@@ -781,6 +917,9 @@ class StepGraph:
             self._raw_exec = ctypes.c_void_p(self.graph.raw_cuda_graph_exec())
 
     _RAW_LAUNCH = os.environ.get("VMAS_GRAPH_RAW_LAUNCH", "1") != "0"  # (A/B knob)
+    # fresh entity-state tensors on first use after each replay (_FreshState); 0: the states stay
+    # views of the graph's buffers (an alias kept across a step then sees later steps' values)
+    _FRESH_STATES = os.environ.get("VMAS_GRAPH_FRESH_STATES", "1") != "0"
 
     def _replay(self):
         asserts = self._asserts is not None and bool(self._asserts.msgs)
@@ -938,6 +1077,20 @@ class StepGraph:
         while no in-place tensor changes).  The outputs are copied before the carry when one
         of them lies in a carry destination (two launches).  The span table is built once per
         (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
+        t = self._post_table() if prep is None else None
+        if t is not None and not t["plain"]:
+            # the common case in one C++ call (csrc/vmas_host.cpp OutputAlloc.post): fresh outputs,
+            # their addresses into the table, the launch(es)
+            if t["steps_row"] is not None:
+                self._steps_current(t)
+            host = t.get("host") or self._host_alloc(t)
+            views = host.post(t["n_out"] if t["clash"] else 0, t["n_all"])
+            rest = [(views[k], s) for k, s in t["loose"]]
+            self._clone_finish(rest)
+            self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),
+                          "bk_ver": tuple(map(_VERSION, self._inplace)), "bk_n": t["n_bk"]}
+            fn, consts = self._clone_build
+            return fn(views, consts)
         t, views, rest = prep if prep is not None else self._post_prepare()
         dev, st = self._dev_index(), self._stream()
         tbl, n_out, n_all = t["addr"], t["n_out"], t["n_all"]
@@ -997,9 +1150,30 @@ class StepGraph:
             t["tbl"][t["steps_row"]]["nbytes"] = st.numel() * 4
             t["steps"] = st
 
+    def _host_alloc(self, t):
+        """The table's OutputAlloc (csrc/vmas_host.cpp): per (dtype, shape) group one allocation
+        split into its members, the contiguous members' addresses into the table's output rows."""
+        groups, row, loose, start = [], 0, [], 0
+        for (dt, shape, n), (_, _, srcs), contig in zip(self._clone_groups, self._clone_group_srcs, t["contig"]):
+            ks = [k for k, c in enumerate(contig) if c]
+            groups.append((srcs[0], list(shape), n, row, ks))
+            loose += [(start + k, srcs[k]) for k, c in enumerate(contig) if not c]
+            row += len(ks)
+            start += n
+        host = N.load_host().OutputAlloc(self._dev_index(), groups, t["tbl"], t["addr"], N.fn_addr("vmas_copy_spans"),
+                                         N.fn_addr("vmas_aux_last_error"))
+        t["host"], t["loose"] = host, loose
+        return host
+
     def _clone_alloc(self, t):
         """Fresh output tensors for one step, their addresses written into the table's output
         rows: (views in the plan's order, the non-contiguous (dst, src) rest)."""
+        host = t.get("host") or self._host_alloc(t)
+        views = host.alloc()
+        return views, [(views[k], s) for k, s in t["loose"]]
+
+    def _clone_alloc_py(self, t):
+        """_clone_alloc in Python (kept as the statement of what OutputAlloc.alloc does)."""
         plan = t.get("alloc")
         if plan is None:  # per table: each group's rows and the byte offsets of its contiguous members
             plan, row = [], 0

@@ -87,6 +87,44 @@ def _owned_or_clone(value):
     return TorchUtils.recursive_clone(value)
 
 
+class _ActionShadow:
+    """Graph mode's random-action draw pre-applies the drawn actions into the persistent action
+    buffer P that the captured step reads (_preapply_columns) -- the buffer agents' action.u, and a
+    holonomic agent's state.force, view after a graph step.  The draw first copies P's current
+    values into a fresh snapshot (vmas_uniform_columns_snap); while armed (from that draw to the
+    step that consumes it) Action.u / AgentState.force return the matching view of the snapshot,
+    so reading them between get_random_actions() and step() gives the last step's values, as in
+    the reference."""
+
+    __slots__ = ("active", "base", "end", "snap", "views")
+
+    def __init__(self):
+        self.active = False
+        self.base = self.end = 0
+        self.snap = None
+        self.views = None
+
+    def arm(self, P: Tensor, snap: Tensor) -> None:
+        self.base, self.end = P.data_ptr(), P.data_ptr() + 4 * P.numel()
+        self.snap = snap
+        self.views = {}
+        self.active = True
+
+    def disarm(self) -> None:
+        self.active = False
+        self.snap = self.views = None
+
+    def view(self, t):
+        """The snapshot's view matching ``t`` (a view of P); ``t`` itself when it is elsewhere."""
+        if t is None or t.dtype is not torch.float32 or not (self.base <= t.data_ptr() < self.end):
+            return t
+        v = self.views.get(id(t))
+        if v is None or v[0] is not t:
+            off = (t.data_ptr() - self.base) // 4
+            v = self.views[id(t)] = (t, self.snap.as_strided(t.shape, t.stride(), off))
+        return v[1]
+
+
 class Environment(TorchVectorizedObject):
     metadata = {"render.modes": ["human", "rgb_array"], "runtime.vectorized": True}
     vmas_random_state = [torch.random.get_rng_state(), np.random.get_state(), random.getstate()]
@@ -132,6 +170,11 @@ class Environment(TorchVectorizedObject):
         self._spec_keep = None  # action tensors a speculative action launch reads
         self._draw_plans = {}  # agent -> cached column plan of its random actions
         self._uniform_cache = None  # see _fused_random_actions
+        self._uniform_host = None  # (column plan, its csrc/vmas_host.cpp UniformDraw)
+        self._ushadow = _ActionShadow()
+        for ag in self.world.agents:
+            ag._action._shadow = self._ushadow
+            ag._state._shadow = self._ushadow
         self._preapply = None  # see _preapply_columns
         self._drawn = None  # the last draw whose applied values are in the persistent buffer
         self.preapplied_steps = 0  # graph steps whose actions were applied by their draw
@@ -269,6 +312,7 @@ class Environment(TorchVectorizedObject):
         skipped; an exception raised there leaves the simulator's states swapped in, as the
         reference's swap does (its restore is not in a finally).
         """
+        self._ushadow.disarm()  # (the step sets the agents' actions: no snapshot is shown any more)
         g = self._graph
         if g is not None and g.graph is not None and self.continuous_actions:
             try:
@@ -663,6 +707,29 @@ class Environment(TorchVectorizedObject):
 
     def _uniform_draw(self, st):
         N, cols, widths, idx, mode, gen, cols_addr, B, dev, offs = st
+        if offs is not None:
+            # equal widths: one [A, B, n] allocation, the column table, the launch and the
+            # generator advance in one C++ call (csrc/vmas_host.cpp UniformDraw)
+            h = self._uniform_host
+            if h is None or h[0] is not st:
+                h = self._uniform_host = (st, N.load_host().UniformDraw(
+                    idx, B, len(widths), widths[0], cols, cols_addr, len(cols), [int(o) for o in offs], mode,
+                    N.fn_addr("vmas_uniform_columns_snap"), N.fn_addr("vmas_aux_last_error")))
+            pre = self._preapply_columns(st)
+            sh = self._ushadow
+            if pre and not sh.active:
+                # the draw rewrites the persistent action buffer that agents' action.u (and a
+                # holonomic agent's state.force) view until the step consumes the draw: their
+                # current values go to a snapshot first, which those attributes show meanwhile
+                # (the reference's draw has no side effect on the agents, environment.py:524-582)
+                P = self._u_persist[1]
+                outs, snap = h[1].draw(P.data_ptr(), P.numel())
+                sh.arm(P, snap)
+            else:
+                outs, _ = h[1].draw(0, 0)
+            self._drawn = (tuple(outs), tuple(o.data_ptr() for o in outs), tuple(o._version for o in outs),
+                           self._u_persist[1]) if pre else None
+            return outs
         f_out = cols["out"]
         if offs is not None:  # one allocation, one [B, n] view per agent (disjoint rows)
             buf = torch.empty(len(widths), B, widths[0], device=dev, dtype=torch.float32)
@@ -803,6 +870,7 @@ class Environment(TorchVectorizedObject):
         agents = self.agents
         n = len(agents)
         self._drawn = None  # (the persistent buffer is rewritten: a draw's applied values are stale)
+        self._ushadow.disarm()
         if n == 0:
             return False
         for a in actions:
