@@ -4,8 +4,9 @@ from .environment import Environment
 
 
 class Wrapper(Enum):
-    """Wrapper selector of make_env (environment/__init__.py:9-33).  The RL-library wrappers are
-    outside the MI355X engine's scope; selecting one raises."""
+    """Wrapper selector of make_env (ref vmas/simulator/environment/__init__.py:9-33).  Each
+    wrapper module imports its RL library at import time (gym; gymnasium + shimmy; ray), as the
+    reference does, so selecting one without the library installed raises ImportError."""
 
     RLLIB = 0
     GYM = 1
@@ -13,4 +14,20 @@ class Wrapper(Enum):
     GYMNASIUM_VEC = 3
 
     def get_env(self, env: Environment, **kwargs):
-        raise NotImplementedError(f"the {self.name} wrapper is not provided by the MI355X engine")
+        if self is Wrapper.RLLIB:
+            from .rllib import VectorEnvWrapper
+
+            return VectorEnvWrapper(env, **kwargs)
+        if self is Wrapper.GYM:
+            from .gym import GymWrapper
+
+            return GymWrapper(env, **kwargs)
+        if self is Wrapper.GYMNASIUM:
+            from .gym.gymnasium import GymnasiumWrapper
+
+            return GymnasiumWrapper(env, **kwargs)
+        if self is Wrapper.GYMNASIUM_VEC:
+            from .gym.gymnasium_vec import GymnasiumVectorizedWrapper
+
+            return GymnasiumVectorizedWrapper(env, **kwargs)
+        raise ValueError(self)
