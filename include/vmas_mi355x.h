@@ -40,8 +40,9 @@ extern "C" {
 #endif
 
 /* v3: VmasDiscoveryIO gained covered_count / all_time / done; increment spans (src NULL) in
- * vmas_copy_spans; VMAS_COPY_MAX_SPANS 160 */
-#define VMAS_ABI_VERSION 3
+ * vmas_copy_spans; VMAS_COPY_MAX_SPANS 160
+ * v4: VmasSpawnTargetsIO max_tries / backup; vmas_uniform_columns_snap */
+#define VMAS_ABI_VERSION 4
 
 /* error codes */
 #define VMAS_OK 0
@@ -398,15 +399,18 @@ int32_t vmas_spawn_resolve(int32_t device, int32_t batch, const float* occupied,
  * `stream` (workgroups claim (target, 64 envs) items in order; target i's items start once target
  * i - 1's are done), no host wait inside.  The caller reads max_accepted once afterwards and
  * advances the generator by sum_i consumed_i * per_try (*increment returns inc).
- * max_accepted[n_targets] counts envs that found no position within VMAS_SPAWN_MAX_TRIES tries
- * (the reference would loop on; the caller raises), max_accepted[VMAS_SPAWN_ERR_WORD] is
- * nonzero when the launch's bounded wait timed out (the caller raises). */
+ * max_accepted[n_targets] counts envs that found no position within max_tries tries (the
+ * reference loops on), max_accepted[VMAS_SPAWN_ERR_WORD] is nonzero when the launch's bounded
+ * wait timed out (a workgroup never ran); either way the caller restores the targets from
+ * `backup` and redoes the respawn with the reference's unbounded loop. */
 #define VMAS_SPAWN_MAX_TARGETS 16
 #define VMAS_SPAWN_MAX_TRIES 65536
 typedef struct VmasSpawnTargetsIO {
     int32_t batch, n_agents, n_targets, mode;
     const float* agents;                  /* [B, n_agents, 2] */
-    int32_t ag_s0, ag_s1, ag_s2, pad0;
+    int32_t ag_s0, ag_s1, ag_s2;
+    int32_t max_tries;                    /* tries per target before an env counts as unresolved (0:
+                                             VMAS_SPAWN_MAX_TRIES) */
     float* pos[VMAS_SPAWN_MAX_TARGETS];   /* target i's [B, 2] position, updated in place */
     int32_t pos_s0[VMAS_SPAWN_MAX_TARGETS], pos_s1[VMAS_SPAWN_MAX_TARGETS];
     const uint8_t* covered;               /* [B, n_targets] torch.bool */
@@ -420,6 +424,10 @@ typedef struct VmasSpawnTargetsIO {
                                              offset from it at run time (a captured launch replays with the
                                              generator state armed before each replay) and publishes its
                                              maxima there; seed / offset above are then ignored */
+    float* backup;                        /* optional [n_targets][B][2]: every target's position before the
+                                             launch (written by it), so that the caller can undo the launch:
+                                             an unresolved env or a timed-out wait is then redone by the
+                                             reference's unbounded loop (scenarios/discovery.py) */
 } VmasSpawnTargetsIO;
 #define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets) + 32 * 32)
 #define VMAS_SPAWN_ERR_WORD 64

@@ -59,18 +59,23 @@ CASES = [
     ("flocking", dict(n_agents=4), None, "graph"),     # scripted agent: range assert on the device
     ("discovery", dict(n_agents=4), None, "graph"),    # spawn sampler: inside the graph (spawn channel)
     ("discovery-hole", dict(n_agents=4), None, "graph"),  # the segmented form: a host hole, two graphs
+    # every respawn handed over to the reference loop (VMAS_SPAWN_TEST_MAX_TRIES=1): undone from the
+    # launch's backup and redone after the replay, the step's observations recomputed
+    ("discovery-redo", dict(n_agents=4), None, "graph"),
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps,expect", CASES, ids=[c[0] for c in CASES])
 def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, substeps, expect):
+    hole = False
     if name == "discovery-hole":
         monkeypatch.setenv("VMAS_GRAPH_DEFERRED_SPAWN", "0")
         name = "discovery"
         hole = True
-    else:
-        hole = False
+    elif name == "discovery-redo":
+        monkeypatch.setenv("VMAS_SPAWN_TEST_MAX_TRIES", "1")
+        name = "discovery"
     envs = []
     for graph in (False, True):
         saved = _rng_save()
@@ -464,3 +469,32 @@ def test_state_alias_keeps_its_step_values_gpu(gpu_device, monkeypatch, fresh):
     out_e, out_g = _step_both(eager, graph, eager.get_random_actions())
     _assert_same(out_e, out_g, "outputs after an in-place write between steps")
     _assert_same(_state(eager), _state(graph), "state after an in-place write between steps")
+
+
+@pytest.mark.gpu
+def test_deferred_respawn_with_other_device_draws_gpu(gpu_device):
+    """A step that draws device random numbers besides discovery's respawn (here one torch.rand in
+    post_step): the deferred (in-graph) respawn would read the generator before the
+    replay and share those numbers, so the capture keeps the respawn as a host hole.  Outputs,
+    state, the extra draw and the generator's consumption equal the eager step's, bit for bit."""
+    eager, graph = _twin_envs(gpu_device, "discovery", n_agents=4)
+    for env in (eager, graph):
+        sc = env.scenario
+
+        def post_step(sc=sc, env=env):
+            sc.noise = torch.rand(env.num_envs, 3, device=env.device)
+
+        sc.post_step = post_step
+    for t in range(8):
+        actions = eager.get_random_actions()
+        s = _rng_save()
+        out_e = eager.step([a.clone() for a in actions])
+        after_e = torch.cuda.get_rng_state()
+        _rng_load(s)
+        out_g = graph.step([a.clone() for a in actions])
+        assert torch.equal(torch.cuda.get_rng_state(), after_e), f"generator consumption step {t}"
+        _assert_same(out_e, out_g, f"outputs step {t}")
+        _assert_same(_state(eager), _state(graph), f"state step {t}")
+        assert torch.equal(eager.scenario.noise, graph.scenario.noise), t
+    assert graph.graph_status == "graph", graph.graph_reason
+    assert len(graph._graph._deferred) == 0 and len(graph._graph._holes) == 1

@@ -6,7 +6,7 @@ set -u
 export TMPDIR=/tmp
 O=gpurun_out/r4b
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_graph.py tests/test_fused.py tests/test_actions.py tests/test_rng.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_graph.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_graph.py tests/test_fused.py tests/test_actions.py tests/test_rng.py tests/test_spawn.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_graph.log 2>&1; rc=$?
 echo "graph tests rc=$rc"; tail -3 $O/pytest_graph.log
 case $rc in 0) ;; 1) grep -n "Error\|assert" $O/pytest_graph.log | head -20; exit 1;; *) exit $rc;; esac
 timeout -k 10 200 python tools/host_micro.py balance 32768 > $O/host_micro.log 2>&1 || exit $?
@@ -17,4 +17,5 @@ timeout -k 10 300 python bench.py --scenario flocking --envs 262144 --steps 50 -
 tail -1 $O/bench_c5_full.log | cut -c1-300
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 echo "suite rc=$rc"; tail -3 $O/pytest_gpu.log
+timeout -k 10 200 python tools/jit_phase_profile.py balance 32768 > $O/phase_profile.log 2>&1 || exit $?
 echo done

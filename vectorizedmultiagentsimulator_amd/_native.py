@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("VMAS_LIB_PATH") or Path(__file__).resolve().pare
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
-VMAS_ABI_VERSION = 3
+VMAS_ABI_VERSION = 4
 VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
 (
     VMAS_PAIR_JOINT,
@@ -261,12 +261,13 @@ def spawn_words(n_targets: int) -> int:  # VMAS_SPAWN_WORDS
 class VmasSpawnTargetsIO(ctypes.Structure):
     _fields_ = [
         ("batch", _i32), ("n_agents", _i32), ("n_targets", _i32), ("mode", _i32),
-        ("agents", _vp), ("ag_s0", _i32), ("ag_s1", _i32), ("ag_s2", _i32), ("pad0", _i32),
+        ("agents", _vp), ("ag_s0", _i32), ("ag_s1", _i32), ("ag_s2", _i32), ("max_tries", _i32),
         ("pos", _vp * VMAS_SPAWN_MAX_TARGETS), ("pos_s0", _i32 * VMAS_SPAWN_MAX_TARGETS),
         ("pos_s1", _i32 * VMAS_SPAWN_MAX_TARGETS),
         ("covered", _vp), ("cov_s0", _i32), ("cov_s1", _i32),
         ("min_dist", _f32), ("x_lo", _f32), ("x_hi", _f32), ("y_lo", _f32), ("y_hi", _f32), ("pad1", _f32),
         ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp), ("channel", _vp),
+        ("backup", _vp),
     ]
 
 

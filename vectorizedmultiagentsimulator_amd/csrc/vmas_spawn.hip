@@ -305,6 +305,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
     int32_t* const done = W + 96;  // target i's counter at done[32 * i]
     const unsigned long long per_try = 2ull * g.inc;
     const int n_occ = io.n_agents + T - 1;
+    const int MT = io.max_tries > 0 ? io.max_tries : VMAS_SPAWN_MAX_TRIES;
     if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);  // (read before the first barrier)
     // (Claiming one item ahead, to overlap the claim's round trip, made it slower: a workgroup
     // could hold two items of one target, serialising them -- 137 -> 218 us per call.)
@@ -360,7 +361,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
                 if (j < i) off += (unsigned long long)(mv[j] == 0 ? 1 : mv[j] + 2) * per_try;
             off_s = off;
         }
-        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+        if (wave == 0) best[lane] = MT;
         // the other targets (earlier ones already moved, by items that may have run on another XCD:
         // loaded with agent-scope atomics, sc1, as they were stored), with the maxima's round trip
         for (int m = io.n_agents + wave; m < n_occ; m += kSpawnWaves) {
@@ -376,9 +377,9 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
         // rejects 16 tries in a row).  (Without the rounds' barrier a wave whose try was rejected
         // went on to its next try before seeing another wave's earlier acceptance: 8 us per item
         // instead of one round's ~3.)
-        for (int base = 0; base < VMAS_SPAWN_MAX_TRIES; base += kSpawnWaves) {
+        for (int base = 0; base < MT; base += kSpawnWaves) {
             const int k = base + wave;
-            if (valid && best[lane] == VMAS_SPAWN_MAX_TRIES) {
+            if (valid && best[lane] == MT && k < MT) {
                 const unsigned long long o = off + (unsigned long long)k * per_try;
                 const float x = uniform_at(seed, o, g, b, io.x_lo, io.x_hi, io.mode);
                 const float y = uniform_at(seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
@@ -392,16 +393,22 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
                     atomicMin(&best[lane], k);
                 }
             }
-            if (!__syncthreads_or(valid && best[lane] == VMAS_SPAWN_MAX_TRIES)) break;
+            if (!__syncthreads_or(valid && best[lane] == MT)) break;
         }
         if (prof && threadIdx.x == 0) prof[(long)it * 6 + 3] = __builtin_amdgcn_s_memrealtime();
         if (wave == 0) {
             const int k = valid ? best[lane] : 0;
-            const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
+            const bool unresolved = valid && k == MT;
             if (unresolved) atomicAdd(&W[T], 1);
             int km = unresolved ? 0 : k;  // one atomic per wave
             for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));
             if (lane == 0 && km > 0) atomicMax(&W[i], km);
+            if (io.backup && valid) {  // target i's position before the launch (only this item writes it)
+                const float* p = io.pos[i] + (long)b * io.pos_s0[i];
+                float* q = io.backup + ((long)i * io.batch + b) * 2;
+                q[0] = p[0];
+                q[1] = p[io.pos_s1[i]];
+            }
             if (cov && !unresolved) {  // try k was drawn and accepted by wave k % kSpawnWaves
                 const float2 xy = won[k % kSpawnWaves][lane];
                 float* p = io.pos[i] + (long)b * io.pos_s0[i];
@@ -445,6 +452,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
     int32_t* const done = W + 96;
     unsigned long long* const rep = reinterpret_cast<unsigned long long*>(W + 96 + 32 * T);  // 128-byte lines
     const unsigned long long per_try = 2ull * g.inc;
+    const int MT = io.max_tries > 0 ? io.max_tries : VMAS_SPAWN_MAX_TRIES;
     const int b = (int)blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
@@ -459,6 +467,11 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
             s1 = io.pos_s1[m - A];
         }
         occ[m][lane] = make_float2(p[0], p[s1]);
+        if (m >= A && io.backup && valid) {  // the targets' positions before the launch
+            float* q = io.backup + ((long)(m - A) * io.batch + b) * 2;
+            q[0] = occ[m][lane].x;
+            q[1] = occ[m][lane].y;
+        }
     }
     if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);  // (read before the first barrier)
     uint32_t covm = 0u;  // (wave 0) the lane's covered targets
@@ -502,7 +515,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
             }
             off_s = rng_s[1] + tries * per_try;
         }
-        if (wave == 0) best[lane] = VMAS_SPAWN_MAX_TRIES;
+        if (wave == 0) best[lane] = MT;
         __syncthreads();
         if (abort_s) {
             if (wave == 0) store_moved();  // (the targets done before the timeout, as they were)
@@ -510,9 +523,9 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
         }
         if (prof && threadIdx.x == 0) prof[it * 6 + 2] = __builtin_amdgcn_s_memrealtime();
         const unsigned long long off = off_s, seed = rng_s[0];
-        for (int base = 0; base < VMAS_SPAWN_MAX_TRIES; base += kSpawnWaves) {  // (as k_spawn_targets)
+        for (int base = 0; base < MT; base += kSpawnWaves) {  // (as k_spawn_targets)
             const int k = base + wave;
-            if (valid && best[lane] == VMAS_SPAWN_MAX_TRIES) {
+            if (valid && best[lane] == MT && k < MT) {
                 const unsigned long long o = off + (unsigned long long)k * per_try;
                 const float x = uniform_at(seed, o, g, b, io.x_lo, io.x_hi, io.mode);
                 const float y = uniform_at(seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode);
@@ -527,12 +540,12 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
                     atomicMin(&best[lane], k);
                 }
             }
-            if (!__syncthreads_or(valid && best[lane] == VMAS_SPAWN_MAX_TRIES)) break;
+            if (!__syncthreads_or(valid && best[lane] == MT)) break;
         }
         if (prof && threadIdx.x == 0) prof[it * 6 + 3] = __builtin_amdgcn_s_memrealtime();
         if (wave == 0) {
             const int k = valid ? best[lane] : 0;
-            const bool unresolved = valid && k == VMAS_SPAWN_MAX_TRIES;
+            const bool unresolved = valid && k == MT;
             if (unresolved) atomicAdd(&W[T], 1);
             int km = unresolved ? 0 : k;
             for (int s = 32; s > 0; s >>= 1) km = max(km, __shfl_xor(km, s));

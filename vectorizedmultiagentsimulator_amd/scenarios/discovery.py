@@ -183,8 +183,11 @@ class Scenario(BaseScenario):
         sink = getattr(w, "_hole_sink", None)
         if deferred and not torch.cuda.is_current_stream_capturing() and \
                 getattr(self, "_spawn_channel", None) is None:
-            self._spawn_channel = SpawnChannel(dev, len(self._targets))  # (pinned memory: not in a capture)
-        if dsink is not None and getattr(self, "_spawn_channel", None) is not None:
+            self._spawn_channel = SpawnChannel(dev, len(self._targets), w.batch_dim)  # (pinned memory: not in a capture)
+        ch = getattr(self, "_spawn_channel", None)
+        if ch is not None and (ch.backup.shape[0] != len(self._targets) or ch.backup.shape[1] != w.batch_dim):
+            ch = None
+        if dsink is not None and ch is not None:
             # a graph-mode capture: the launch stays inside the step's graph
             dsink(DeferredRespawn(args, self._spawn_channel))
         elif sink is not None:  # (the segmented form: the host read is a hole of the step)
@@ -466,8 +469,14 @@ class HeuristicPolicy(BaseHeuristicPolicy):
         return torch.clamp((des_pos - current_pos) * 10, min=-u_range, max=u_range)
 
 
+def spawn_max_tries() -> int:
+    """Tries per target before the one-launch respawn hands an env over to the reference's loop
+    (VMAS_SPAWN_MAX_TRIES; VMAS_SPAWN_TEST_MAX_TRIES lowers it for tests of that hand-over)."""
+    return int(os.environ.get("VMAS_SPAWN_TEST_MAX_TRIES", "0") or 0)
+
+
 def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
-                  target_pos, mx: Tensor, channel=None):
+                  target_pos, mx: Tensor, channel=None, backup: Tensor = None):
     """One vmas_spawn_targets launch on the current stream; returns (io, philox increment)."""
     import numpy as np
 
@@ -495,6 +504,8 @@ def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidi
         io.seed, io.offset = gen.initial_seed(), gen.get_offset()
     io.max_accepted = mx.data_ptr()
     io.channel = channel
+    io.max_tries = spawn_max_tries()
+    io.backup = backup.data_ptr() if backup is not None else None
     inc = ctypes.c_uint64(0)
     N.check_aux(N.load_library().vmas_spawn_targets(idx, ctypes.byref(io), ctypes.byref(inc),
                                                       ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
@@ -503,17 +514,36 @@ def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidi
 
 
 def _spawn_consumed(h, T: int, offset: int, inc: int, gen) -> None:
-    """Advance the generator by the tries the reference loop consumes (h: the launch's maxima,
-    unresolved count); raise where an env found no position."""
-    # the generator is left where the tries it consumed put it, also when an env found no free
-    # position (the reference warns and keeps trying forever, utils.py:285-317; here the kernels
-    # stop after VMAS_SPAWN_MAX_TRIES tries and the call raises, with the targets of the resolved
-    # envs moved and the generator consistent with the tries drawn)
+    """Advance the generator by the tries the reference loop consumes (h: the launch's maxima)."""
     gen.set_offset(offset + sum(1 if m == 0 else m + 2 for m in h[:T]) * 2 * inc)
-    if h[T]:
-        raise RuntimeError(
-            f"find_random_pos_for_entity: {h[T]} env(s) found no free position within {N.VMAS_SPAWN_MAX_TRIES} "
-            "tries; make sure the bounds or the min_dist_between_entities are not too tight to fit all entities")
+
+
+def respawn_reference_loop(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
+                           target_pos) -> None:
+    """The reference's respawn loop (ref discovery.py:180-204): for each target in order,
+    find_random_pos_for_entity over every env against the agents and the other targets, and the
+    covered envs take the new position.  The sampler is the generic one (ScenarioUtils: the same
+    numbers and generator use, unbounded, a warning past 50 000 tries, as ref utils.py:285-317)."""
+    from types import SimpleNamespace
+
+    world = SimpleNamespace(batch_dim=agents_pos.shape[0], device=agents_pos.device)
+    for i, tp in enumerate(target_pos):
+        occupied = torch.cat([agents_pos] + [o.unsqueeze(1) for j, o in enumerate(target_pos) if j != i], dim=1)
+        pos = ScenarioUtils._find_random_pos_native(occupied, None, world, min_dist, (-x_semidim, x_semidim),
+                                                    (-y_semidim, y_semidim))
+        tp.copy_(torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), tp))
+
+
+def _respawn_redo(args, backup: Tensor, offset: int, gen) -> None:
+    """Undo a one-launch respawn that left an env unresolved after max_tries tries, or whose
+    bounded wait timed out (a workgroup never ran: the co-residency the resident kernel assumes did
+    not hold), and redo it with the reference's loop: the targets back from the launch's backup,
+    the generator back to the launch's offset."""
+    targets = args[5:]
+    for i, tp in enumerate(targets):
+        tp.copy_(backup[i])
+    gen.set_offset(offset)
+    respawn_reference_loop(*args[:5], targets)
 
 
 def deferred_respawn() -> bool:
@@ -526,11 +556,12 @@ def deferred_respawn() -> bool:
 class SpawnChannel:
     """Owner of a vmas_spawn_channel (mapped pinned host words), created outside any capture."""
 
-    def __init__(self, dev: torch.device, n_targets: int):
+    def __init__(self, dev: torch.device, n_targets: int, batch: int):
         self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
         # the launch's device words, owned here (allocated outside any capture: a buffer from a
         # capture's private pool was found overwritten after a later replay)
         self.mx = torch.zeros(N.spawn_words(n_targets), dtype=torch.int32, device=dev)
+        self.backup = torch.empty((n_targets, batch, 2), dtype=torch.float32, device=dev)  # (see _respawn_redo)
         ch = ctypes.c_void_p()
         N.check_aux(N.load_library().vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
         self.ptr = ch
@@ -569,7 +600,8 @@ class DeferredRespawn:
     def capture(self):
         a = self.args
         self.mx = self.chan.mx
-        _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch)
+        _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch,
+                                    backup=self.chan.backup)
 
     def arm(self):
         if self.chan.busy is not None:  # (an earlier replay never finished: drain it first)
@@ -582,25 +614,34 @@ class DeferredRespawn:
         self.pending = self.chan.seq
         self.chan.busy = self
 
-    def finish(self, apply: bool = True):
+    def finish(self, apply: bool = True) -> bool:
+        """Waits for the replayed launch's words and advances the generator.  Returns True when the
+        launch left an env unresolved or its bounded wait timed out: the respawn was then undone
+        and redone with the reference's loop (_respawn_redo), and the step's observations, computed
+        inside the graph after the respawn, must be recomputed (StepGraph._finish_deferred)."""
         if self.pending is None:
-            return
+            return False
         seq, self.pending = self.pending, None
         if self.chan.busy is self:
             self.chan.busy = None
         words = (ctypes.c_int32 * (self.T + 2))()
         rc = N.load_library().vmas_spawn_channel_wait(self.ch, seq, words, self.T,
                                                       ctypes.c_void_p(torch.cuda.current_stream(self.idx).cuda_stream))
+        timed_out = False
         if rc < 0:
             torch.cuda.synchronize(self.idx)
-            if self.mx is not None and int(self.mx[N.VMAS_SPAWN_ERR_WORD].item()):
-                raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
-            N.check_aux(rc, "vmas_spawn_channel_wait")
+            timed_out = self.mx is not None and bool(int(self.mx[N.VMAS_SPAWN_ERR_WORD].item()))
+            if not timed_out:
+                N.check_aux(rc, "vmas_spawn_channel_wait")
         h = list(words)
-        if h[self.T + 1]:
-            raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
-        if apply:
-            _spawn_consumed(h, self.T, self.offset, self.inc, torch.cuda.default_generators[self.idx])
+        if not apply:
+            return False
+        gen = torch.cuda.default_generators[self.idx]
+        if timed_out or h[self.T + 1] or h[self.T]:
+            _respawn_redo(self.args, self.chan.backup, self.offset, gen)
+            return True
+        _spawn_consumed(h, self.T, self.offset, self.inc, gen)
+        return False
 
 
 
@@ -616,9 +657,12 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     T = len(target_pos)
     mx = out if out is not None else torch.empty(N.spawn_words(T), dtype=torch.int32, device=dev)
-    io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx)
+    backup = torch.empty((T, agents_pos.shape[0], 2), dtype=torch.float32, device=dev)
+    io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx, backup=backup)
     h = mx[:N.VMAS_SPAWN_ERR_WORD + 1].tolist()  # the step's one host wait (maxima, unresolved, error)
-    if h[N.VMAS_SPAWN_ERR_WORD]:
-        raise RuntimeError("vmas_spawn_targets: the launch's wait for the previous target timed out")
-    _spawn_consumed(h, T, io.offset, inc, torch.cuda.default_generators[idx])
+    gen = torch.cuda.default_generators[idx]
+    if h[N.VMAS_SPAWN_ERR_WORD] or h[T]:
+        _respawn_redo((agents_pos, covered, min_dist, x_semidim, y_semidim, *target_pos), backup, io.offset, gen)
+        return mx
+    _spawn_consumed(h, T, io.offset, inc, gen)
     return mx

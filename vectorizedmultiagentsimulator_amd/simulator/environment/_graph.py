@@ -602,14 +602,21 @@ class StepGraph:
 
             rng_cur = [_host_rng_states()]
             rng_used = [None]
+            # device generator use outside the holes: a captured step that draws device random
+            # numbers besides the respawn keeps the respawn as a host hole (a deferred
+            # respawn reads the generator before the replay, so it would share those numbers)
+            dgen = torch.cuda.default_generators[torch.device(self.env.device).index or 0]
+            d_off0, hole_adv = dgen.get_offset(), [0]
 
             def hole(fn, args, _inner=hole):  # host RNG use inside a hole is replayed eagerly too
                 if rng_used[0] is None:
                     rng_used[0] = _host_rng_changed(rng_cur[0], _host_rng_states())
+                o0 = dgen.get_offset()
                 try:
                     return _inner(fn, args)
                 finally:
                     rng_cur[0] = _host_rng_states()
+                    hole_adv[0] += dgen.get_offset() - o0
 
             self.env.world._hole_sink = hole
             objs = _tracked_objects(self.env)
@@ -623,6 +630,7 @@ class StepGraph:
                 torch.cuda.set_sync_debug_mode(mode)
             if rng_used[0] is None:
                 rng_used[0] = _host_rng_changed(rng_cur[0], _host_rng_states())
+            self._device_rng_outside_holes = (dgen.get_offset() - d_off0 - hole_adv[0]) != 0
             plain1 = _plain_attrs(objs)
             changed = sorted(k for k in set(plain0) | set(plain1) if plain0.get(k) != plain1.get(k))
         self._trial_consts = consts  # the arena outlives the copies that read it
@@ -644,15 +652,26 @@ class StepGraph:
                         + ", ".join(f"{names.get(i, '?')}.{k}" for i, k in changed[:4]))[:300]
         return out
 
-    def _finish_deferred(self, apply: bool = True):
-        err = None
+    def _finish_deferred(self, apply: bool = True, out=None):
+        """The host side of the captured deferred launches (discovery's respawn).  One that had to
+        be redone on the host (DeferredRespawn.finish) changed state the graph's observations had
+        already read: the step's observations in ``out`` are recomputed eagerly."""
+        err, redone = None, False
         for d in self._deferred:
             try:
-                d.finish(apply)
+                redone |= bool(d.finish(apply))
             except Exception as ex:  # noqa: BLE001 -- drain every channel, then raise the first
                 err = err or ex
         if err is not None:
             raise err
+        if redone and out is not None:
+            env = self.env
+            obs = env._get_from_scenario(get_observations=True, get_rewards=False, get_infos=False,
+                                         get_dones=False)[0]
+            dst = out[0]
+            for a, b in (zip(dst.values(), obs.values()) if isinstance(dst, dict) else zip(dst, obs)):
+                for x, y in zip(_tensors(a, []), _tensors(b, [])):
+                    x.copy_(y)
 
     def drop(self, why: str):
         fr, self._fresh = self._fresh, None
@@ -729,7 +748,8 @@ class StepGraph:
             env.world._assert_sink = asserts.capture_sink
             env.world._assert_range_sink = asserts.capture_range
             env.world._hole_sink = segs.hole
-            env.world._deferred_sink = deferred_sink
+            # (the deferred form only when the step draws no other device random numbers)
+            env.world._deferred_sink = None if getattr(self, "_device_rng_outside_holes", True) else deferred_sink
             torch.cuda.synchronize(dev)
             self._folding = self._fold_steps_ok()
             with torch.cuda.stream(side), consts:
@@ -937,7 +957,7 @@ class StepGraph:
                 self._rollback(rng, restore_actions=False)
                 raise
         out = self._post_replay()
-        self._finish_deferred()
+        self._finish_deferred(out=out)
         return out
 
     # ---- speculative replay ---------------------------------------------------------------------
@@ -972,7 +992,7 @@ class StepGraph:
         self._launch()
         self.replays += 1
         out = self._post_replay()
-        self._finish_deferred()
+        self._finish_deferred(out=out)
         return out
 
     def replay_speculative(self, flags_ok):
@@ -1005,7 +1025,7 @@ class StepGraph:
             raise
         # only now: the post-replay carry overwrites X, which a rollback restores Y from
         out = self._post_replay(prep)
-        self._finish_deferred()
+        self._finish_deferred(out=out)
         return out
 
     def _rollback(self, rng: Tensor, restore_actions: bool):
