@@ -162,3 +162,29 @@ def test_force_dicts_graph_mode_gpu(gpu_device):
             assert torch.equal(ga.forces_dict[x], ea.forces_dict[y]), x.name
             assert torch.equal(ga.torques_dict[x], ea.torques_dict[y]), x.name
     assert envs[0].graph_status == "graph"
+
+
+def test_static_rows_are_the_steps_values_host():
+    """Rows of entities that neither move nor rotate: zeros, or the friction of their
+    constant velocity as it was AT THE STEP (ref core.py:2053-2101) -- a later set_vel or friction
+    change before the dict is read does not change them."""
+    env = make("balance", dict(n_agents=4), 2, "cpu", num_envs=16, seed=0)
+    w = env.world
+    static = [e for e in w.entities if not (e.movable or e.rotatable)]
+    assert static
+    e = static[0]
+    e.linear_friction = 0.3
+    vel = torch.linspace(-0.5, 0.5, 32).view(16, 2)
+    e.set_vel(vel, batch_index=None)
+    env.step(env.get_random_actions())
+    e.set_vel(torch.zeros(16, 2), batch_index=None)  # changed after the step, before the read
+    e.linear_friction = 0.9
+    expect = torch.zeros(16, 2)
+    w.engine._static_forces(type("E", (), {"state": type("S", (), {"vel": vel, "ang_vel": None})(),
+                                            "linear_friction": 0.3, "angular_friction": None, "mass": e.mass,
+                                            "moment_of_inertia": e.moment_of_inertia})(),
+                            expect, torch.zeros(16, 1), w)
+    got = w.forces_dict[e]
+    assert torch.equal(got, expect) and float(got.abs().max()) > 0
+    for other in static[1:]:
+        assert float(w.forces_dict[other].abs().max()) == 0.0 and float(w.torques_dict[other].abs().max()) == 0.0

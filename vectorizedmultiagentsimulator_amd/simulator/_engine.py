@@ -665,28 +665,52 @@ class PhysicsEngine:
                                              ctypes.byref(iters)), "vmas_world_step")
         self._last_iterations = iters.value
         # the dicts are built from the buffer when first read (World.forces_dict); a step that did
-        # not export leaves none (stale dicts of an earlier step must not be read as this one's)
-        w._force_buf = (fd, B, self) if fd is not None else None
+        # not export leaves none (stale dicts of an earlier step must not be read as this one's).
+        # Rows of entities that neither move nor rotate: zeros, set on first read, except where
+        # friction acts on their (constant) velocity -- computed here, from the state and
+        # coefficients of this step (a read after a later change must see this step's values)
+        done = ()
+        if fd is not None:
+            done = self._static_friction_rows(fd, B, w)
+        w._force_buf = (fd, B, self, done) if fd is not None else None
         w._forces_dict = w._torques_dict = None
         self.steps += 1
         self._last_keep = keep
         return out
 
-    def force_dicts(self, fd: torch.Tensor, B: int):
+    def _static_friction_rows(self, fd: torch.Tensor, B: int, w):
+        """Step time: the rows of static entities on which friction acts (see force_dicts);
+        returns their entity indices."""
+        done = []
+        for i, e in enumerate(self.entities):
+            if e.movable or e.rotatable:
+                continue
+            lin = e.linear_friction is not None or w._linear_friction > 0
+            ang = e.angular_friction is not None or w._angular_friction > 0
+            if lin or ang:
+                E = len(self.entities)
+                f2 = fd[: E * B * 2].view(E, B, 2)
+                f1 = fd[E * B * 2:].view(E, B, 1)
+                f2[i].zero_()
+                f1[i].zero_()
+                self._static_forces(e, f2[i], f1[i], w)
+                done.append(i)
+        return tuple(done)
+
+    def force_dicts(self, fd: torch.Tensor, B: int, done=()):
         """World.forces_dict / torques_dict (ref core.py:1975-1992) of the step that wrote ``fd``:
-        per entity, views of its last-substep force [B,2] and torque [B,1] totals; the rows of
-        entities that neither move nor rotate are set here (the kernels do not write them)."""
-        w = self.world
+        per entity, views of its last-substep force [B,2] and torque [B,1] totals.  Rows of
+        entities that neither move nor rotate (the kernels do not write them): friction rows
+        (``done``) were set at step time, the others are zeros, set here."""
         E = len(self.entities)
         f2 = fd[: E * B * 2].view(E, B, 2)
         f1 = fd[E * B * 2:].view(E, B, 1)
         forces, torques = {}, {}
         for i, e in enumerate(self.entities):
             forces[e], torques[e] = f2[i], f1[i]
-            if not (e.movable or e.rotatable):
+            if not (e.movable or e.rotatable) and i not in done:
                 f2[i].zero_()
                 f1[i].zero_()
-                self._static_forces(e, f2[i], f1[i], w)
         return forces, torques
 
     @staticmethod

@@ -1119,8 +1119,8 @@ class World(TorchVectorizedObject):
         if buf is None:
             raise AttributeError("forces_dict: no step has exported force totals yet (world.export_forces "
                                  "was False at the last step, or no step ran)")
-        fd, B, engine = buf
-        self._forces_dict, self._torques_dict = engine.force_dicts(fd, B)
+        fd, B, engine, done = buf
+        self._forces_dict, self._torques_dict = engine.force_dicts(fd, B, done)
 
     def step(self):
         self.entity_index_map = {e: i for i, e in enumerate(self.entities)}
