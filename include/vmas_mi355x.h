@@ -633,6 +633,13 @@ typedef struct VmasCopySpan {
     int64_t nbytes;
 } VmasCopySpan;
 int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, void* stream);
+/* The copies of vmas_copy_spans (at most 96 spans) and the draw of vmas_uniform_columns_snap (at
+ * most 16 columns) in ONE launch: graph mode's post-replay copies together with the next step's
+ * random actions drawn ahead (simulator/environment/_graph.py); the numbers and the generator
+ * increment are those of vmas_uniform_columns (no reference counterpart beyond those two). */
+int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* spans, int32_t n_spans, int64_t numel,
+                             const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed, uint64_t offset,
+                             int32_t mode, int64_t u_snap_delta, uint64_t* increment, void* stream);
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);

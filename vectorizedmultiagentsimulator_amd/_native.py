@@ -85,6 +85,7 @@ EXPORTED_SYMBOLS = (
     "vmas_apply_actions_flags",
     "vmas_uniform_columns",
     "vmas_uniform_columns_snap",
+    "vmas_copy_spans_draw",
     "vmas_assert_create",
     "vmas_assert_destroy",
     "vmas_assert_publish",
@@ -548,6 +549,9 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_spawn_profile.argtypes = [_vp, ctypes.c_int64]
     lib.vmas_copy_spans.restype = _i32
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
+    lib.vmas_copy_spans_draw.restype = _i32
+    lib.vmas_copy_spans_draw.argtypes = [_i32, _vp, _i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64, ctypes.c_uint64,
+                                         _i32, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64), _vp]
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_graph_launch.restype = _i32

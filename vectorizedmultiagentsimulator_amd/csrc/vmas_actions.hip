@@ -23,6 +23,7 @@
 
 #include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
+#include "vmas_uniform.hpp"
 
 namespace {
 
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(kRangeThreads) k_assert_range(const float* u, 
 // host picks the mode that reproduces torch's draws bit for bit on this device (probe), or does
 // not use the kernel.
 constexpr int kMaxUniformCols = 32;
-constexpr int kUniformThreads = 256;
+constexpr int kUniformThreads = vmas_uniform::kThreads;
 
 struct UniformArgs {
     VmasUniformColumn c[kMaxUniformCols];
@@ -236,40 +237,8 @@ struct UniformArgs {
     int mode;  // bit 0: fused (0, 1] mapping; bit 1: fused affine transform
 };
 
-__device__ __forceinline__ float unit_float(unsigned int v, bool fused) {
-    const float inv = 2.3283064e-10f;  // ROCRAND_2POW32_INV
-    return fused ? __builtin_fmaf((float)v, inv, inv) : inv + (float)v * inv;
-}
-
 __global__ void __launch_bounds__(kUniformThreads) k_uniform_columns(UniformArgs a) {
-    const VmasUniformColumn& col = a.c[blockIdx.y];
-    const long long idx = (long long)blockIdx.x * kUniformThreads + threadIdx.x;
-    rocrand_state_philox4x32_10 st;
-    rocrand_init(a.seed, (unsigned long long)idx, col.offset, &st);
-    const long long step = (long long)kUniformThreads * gridDim.x;
-    const long long rounded = ((a.numel - 1) / (step * 4) + 1) * step * 4;
-    const float from = col.from, to = col.to, range = to - from;
-    const bool fused_unit = a.mode & 1, fused_affine = a.mode & 2;
-    for (long long li0 = idx; li0 < rounded; li0 += step * 4) {
-        const uint4 v = rocrand4(&st);
-        const unsigned int vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const long long li = li0 + step * k;
-            if (li < a.numel) {
-                const float r = unit_float(vv[k], fused_unit);
-                const float val = fused_affine ? __builtin_fmaf(r, range, from) : r * range + from;
-                const float x = val == to ? from : val;  // (0, 1] -> [from, to)
-                col.out[li * col.stride] = x;
-                if (col.u_out) {  // apply_one's operations on the same value
-                    const float v = col.u_clamp ? fminf(fmaxf(x, -col.u_range), col.u_range) : x;
-                    float* uo = col.u_out + li * col.u_stride;
-                    if (a.snap) *reinterpret_cast<float*>(reinterpret_cast<char*>(uo) + a.snap) = *uo;
-                    *uo = v * col.u_mult;
-                }
-            }
-        }
-    }
+    vmas_uniform::draw_column(a.c[blockIdx.y], a.seed, a.numel, a.snap, a.mode, (int)gridDim.x, (int)blockIdx.x);
 }
 
 struct UniformGrid {

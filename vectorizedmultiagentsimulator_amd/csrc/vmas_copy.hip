@@ -13,6 +13,7 @@
 
 #include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
+#include "vmas_uniform.hpp"
 
 namespace {
 
@@ -38,8 +39,7 @@ __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restr
     for (; i < n; i += step) dst[i] = src[i];
 }
 
-__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) {
-    const VmasCopySpan& s = a.s[blockIdx.y];
+__device__ __forceinline__ void copy_span(const VmasCopySpan& s) {
     if (!s.src) {  // an increment span: dst[i] += 1.0f
         float* d = reinterpret_cast<float*>(s.dst);
         const int64_t n = s.nbytes / 4;
@@ -54,6 +54,31 @@ __global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) {
         copy_units(reinterpret_cast<const uint32_t*>(s.src), reinterpret_cast<uint32_t*>(s.dst), s.nbytes / 4);
     else
         copy_units(reinterpret_cast<const uint8_t*>(s.src), reinterpret_cast<uint8_t*>(s.dst), s.nbytes);
+}
+
+__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) { copy_span(a.s[blockIdx.y]); }
+
+// The post-replay copies and the next step's random-action draw in ONE launch (vmas_copy_spans_draw):
+// blockIdx.y < n_spans copies span y (grid-stride over gridDim.x), the rest draw column
+// y - n_spans with torch's grid of gx_draw blocks (blocks beyond it leave).
+constexpr int kMergedSpans = 96, kMergedCols = 16;
+struct CopyDrawArgs {
+    VmasCopySpan s[kMergedSpans];
+    VmasUniformColumn c[kMergedCols];
+    unsigned long long seed;
+    long long numel, snap;
+    int n_spans, gx_draw, mode, pad;
+};
+static_assert(sizeof(CopyDrawArgs) <= 4096, "kernel argument block");
+
+__global__ void __launch_bounds__(kCopyThreads) k_copy_draw(CopyDrawArgs a) {
+    const int y = (int)blockIdx.y;
+    if (y < a.n_spans) {
+        copy_span(a.s[y]);
+        return;
+    }
+    if ((int)blockIdx.x >= a.gx_draw) return;
+    vmas_uniform::draw_column(a.c[y - a.n_spans], a.seed, a.numel, a.snap, a.mode, a.gx_draw, (int)blockIdx.x);
 }
 
 constexpr int kFillThreads = 256;
@@ -95,5 +120,54 @@ extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, in
         hipLaunchKernelGGL(k_copy_spans, dim3(gx, a.n), dim3(kCopyThreads), 0, (hipStream_t)stream, a);
         VMAS_AUX_HIP(hipGetLastError());
     }
+    return VMAS_OK;
+}
+
+extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* spans, int32_t n_spans, int64_t numel,
+                                        const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed, uint64_t offset,
+                                        int32_t mode, int64_t u_snap_delta, uint64_t* increment, void* stream) {
+    if (device < 0 || n_spans < 0 || n_spans > kMergedSpans || (n_spans > 0 && !spans) || n_cols <= 0 ||
+        n_cols > kMergedCols || !cols || numel <= 0 || !increment || mode < 0 || mode > 3)
+        return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: bad arguments");
+    VMAS_AUX_HIP(hipSetDevice(device));
+    static int max_blocks[64] = {0};
+    if (device >= 64) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: device %d", device);
+    if (!max_blocks[device]) {
+        hipDeviceProp_t prop;
+        VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
+        max_blocks[device] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / vmas_uniform::kThreads);
+        if (max_blocks[device] <= 0) return vmas_aux::fail(VMAS_E_HIP, "vmas_copy_spans_draw: device properties");
+    }
+    int gx_draw = 0;
+    unsigned long long inc = 0;
+    vmas_uniform::grid_for(numel, max_blocks[device], &gx_draw, &inc);
+    CopyDrawArgs a{};
+    int64_t most = 0;
+    int n = 0;
+    for (int i = 0; i < n_spans; ++i) {
+        const VmasCopySpan& sp = spans[i];
+        if (sp.nbytes < 0 || (sp.nbytes > 0 && !sp.dst) || (!sp.src && (sp.nbytes % 4 != 0 || ((uintptr_t)sp.dst & 3) != 0)))
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: bad span %d", i);
+        if (sp.nbytes == 0 || sp.src == sp.dst) continue;
+        a.s[n++] = sp;
+        most = std::max<int64_t>(most, (sp.nbytes + 15) / 16);
+    }
+    for (int i = 0; i < n_cols; ++i) {
+        if (!cols[i].out) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: null column %d", i);
+        a.c[i] = cols[i];
+        a.c[i].offset = offset + inc * (unsigned long long)i;
+    }
+    a.seed = seed;
+    a.numel = numel;
+    a.snap = u_snap_delta;
+    a.n_spans = n;
+    a.gx_draw = gx_draw;
+    a.mode = mode;
+    const int64_t per_block = (int64_t)kCopyThreads * kCopyUnroll;
+    const int gx_copy = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (most + per_block - 1) / per_block));
+    hipLaunchKernelGGL(k_copy_draw, dim3((unsigned)std::max(gx_copy, gx_draw), n + n_cols), dim3(kCopyThreads), 0,
+                       (hipStream_t)stream, a);
+    VMAS_AUX_HIP(hipGetLastError());
+    *increment = inc * (unsigned long long)n_cols;
     return VMAS_OK;
 }

@@ -36,6 +36,8 @@ namespace {
 using CopySpansFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, void*);
 using UniformColumnsSnapFn = int32_t (*)(int32_t, int64_t, const VmasUniformColumn*, int32_t, uint64_t, uint64_t,
                                          int32_t, int64_t, uint64_t*, void*);
+using CopySpansDrawFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, int64_t, const VmasUniformColumn*, int32_t,
+                                    uint64_t, uint64_t, int32_t, int64_t, uint64_t*, void*);
 using LastErrorFn = const char* (*)(void);
 
 void* current_stream(int device) {
@@ -120,6 +122,9 @@ public:
         return n;
     }
 
+    VmasCopySpan* table() const { return tbl_; }
+    const char* last_error() const { return last_error_(); }
+
 private:
     int device_;
     py::object table_;
@@ -175,6 +180,31 @@ public:
         return {std::move(out), std::move(snap)};
     }
 
+    // The draw's buffers and column table without the launch (a speculative draw merged into the
+    // post-replay launch, OutputAlloc.post_draw): (per-agent tensors, snapshot, snap delta)
+    std::tuple<std::vector<at::Tensor>, c10::optional<at::Tensor>, int64_t> prepare(int64_t snap_base,
+                                                                                   int64_t snap_numel) {
+        at::Tensor buf = at::empty({n_agents_, batch_, width_}, opts_);
+        const uintptr_t base = (uintptr_t)buf.data_ptr();
+        for (int64_t k = 0; k < n_cols_; ++k) cols_[k].out = (float*)(base + (uintptr_t)out_offs_[k]);
+        c10::optional<at::Tensor> snap;
+        int64_t delta = 0;
+        if (snap_numel > 0) {
+            snap = at::empty({snap_numel}, opts_);
+            delta = (int64_t)((uintptr_t)snap->data_ptr() - (uintptr_t)snap_base);
+        }
+        std::vector<at::Tensor> out;
+        out.reserve(n_agents_);
+        for (int64_t a = 0; a < n_agents_; ++a) out.push_back(buf.select(0, a));
+        return {std::move(out), std::move(snap), delta};
+    }
+
+    int device() const { return device_; }
+    int64_t batch() const { return batch_; }
+    const VmasUniformColumn* cols() const { return cols_; }
+    int64_t n_cols() const { return n_cols_; }
+    int mode() const { return mode_; }
+
 private:
     int device_;
     int64_t batch_, n_agents_, width_;
@@ -187,6 +217,31 @@ private:
     LastErrorFn last_error_;
     at::TensorOptions opts_;
 };
+
+// OutputAlloc.post with the next step's random actions drawn in the same launch (speculatively:
+// the generator is NOT advanced here; the host hands the draw out and advances it by `increment`
+// only if get_random_actions is called next at the same generator state).  Returns (outputs,
+// drawn per-agent tensors, snapshot, seed, offset, increment).
+py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, int64_t snap_base, int64_t snap_numel,
+                    int64_t copy_draw_fn) {
+    std::vector<at::Tensor> outs = oa.alloc();
+    auto [acts, snap, delta] = d.prepare(snap_base, snap_numel);
+    if (mid > 0) oa.launch(0, mid);
+    const int64_t lo = mid > 0 ? mid : 0;
+    at::Generator gen = at::cuda::detail::getDefaultCUDAGenerator((c10::DeviceIndex)d.device());
+    uint64_t seed = 0, off = 0, inc = 0;
+    {
+        std::lock_guard<std::mutex> lock(gen.mutex());
+        auto* impl = gen.get<at::CUDAGeneratorImpl>();
+        seed = impl->current_seed();
+        off = impl->get_offset();
+    }
+    const int32_t rc = ((CopySpansDrawFn)copy_draw_fn)(d.device(), oa.table() + lo, (int32_t)(hi - lo), d.batch(),
+                                                       d.cols(), (int32_t)d.n_cols(), seed, off, d.mode(), delta, &inc,
+                                                       current_stream(d.device()));
+    if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
+    return py::make_tuple(outs, acts, snap, seed, off, inc);
+}
 
 // (tensor._version of each, as a tuple: the version snapshots of the post-replay bookkeeping)
 py::tuple versions(const std::vector<at::Tensor>& ts) {
@@ -210,5 +265,6 @@ PYBIND11_MODULE(_vmas_host, m) {
         .def(py::init<int, int64_t, int64_t, int64_t, py::object, int64_t, int64_t, std::vector<int64_t>, int, int64_t,
                       int64_t>())
         .def("draw", &UniformDraw::draw);
+    m.def("post_draw", &post_draw);
     m.def("versions", &versions);
 }

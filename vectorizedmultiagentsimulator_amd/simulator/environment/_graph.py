@@ -1104,7 +1104,16 @@ class StepGraph:
             if t["steps_row"] is not None:
                 self._steps_current(t)
             host = t.get("host") or self._host_alloc(t)
-            views = host.post(t["n_out"] if t["clash"] else 0, t["n_all"])
+            mid, hi = (t["n_out"] if t["clash"] else 0), t["n_all"]
+            # (not with deferred launches: their host side advances the generator after this)
+            ahead = self.env._draw_ahead_plan() if (hi - mid <= 96 and not t["n_bk"] and not self._deferred) else None
+            if ahead is not None:  # (+ the next step's random actions in the same launch)
+                st, drawer, P = ahead
+                views, acts, snap, seed, off, inc = N.load_host().post_draw(
+                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"))
+                self.env._drew_ahead(st, acts, snap, seed, off, inc)
+            else:
+                views = host.post(mid, hi)
             rest = [(views[k], s) for k, s in t["loose"]]
             self._clone_finish(rest)
             self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),

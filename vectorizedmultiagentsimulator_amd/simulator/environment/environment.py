@@ -172,6 +172,8 @@ class Environment(TorchVectorizedObject):
         self._uniform_cache = None  # see _fused_random_actions
         self._uniform_host = None  # (column plan, its csrc/vmas_host.cpp UniformDraw)
         self._ushadow = _ActionShadow()
+        self._spec = None  # a draw made ahead by the post-replay launch (_draw_ahead_plan)
+        self._spec_ok = False  # the last step consumed a draw applied by its own launch
         for ag in self.world.agents:
             ag._action._shadow = self._ushadow
             ag._state._shadow = self._ushadow
@@ -313,6 +315,7 @@ class Environment(TorchVectorizedObject):
         reference's swap does (its restore is not in a finally).
         """
         self._ushadow.disarm()  # (the step sets the agents' actions: no snapshot is shown any more)
+        self._spec_ok = False
         g = self._graph
         if g is not None and g.graph is not None and self.continuous_actions:
             try:
@@ -568,6 +571,11 @@ class Environment(TorchVectorizedObject):
             return None
         c = self._uniform_cache
         if c is not None and c[1] is not None and self._uniform_same(c[2]):
+            sp, self._spec = self._spec, None
+            if sp is not None and sp[0] is c[1]:
+                outs = self._take_spec(sp)
+                if outs is not None:
+                    return outs
             return self._uniform_draw(c[1])
         plans = [self._column_plan(a) for a in agents]
         B, dev = plans[0][0], plans[0][1]
@@ -600,6 +608,54 @@ class Environment(TorchVectorizedObject):
             return None
         self._uniform_cache = (c[0], c[1], self._uniform_sig())
         return self._uniform_draw(c[1])
+
+    # ---- random actions drawn ahead, inside the post-replay launch (graph mode) ------------------
+    # In the loop env.step(env.get_random_actions()) the draw of step t + 1 is the next device work
+    # after step t's post-replay copies.  When step t consumed a draw applied by its own launch,
+    # the post-replay launch also draws step t + 1's actions (vmas_copy_spans_draw: one launch
+    # instead of two) at the generator's current state, without advancing it; the next
+    # get_random_actions hands that draw out -- and advances the generator -- only if nothing
+    # changed the generator (seed and offset), the column plan or its applied-column fields in
+    # between, else it draws as usual.  The draw rewrote the persistent action buffer, so the
+    # agents' action.u / state.force show its snapshot meanwhile (_ActionShadow).
+    _SPEC_DRAW = os.environ.get("VMAS_GRAPH_DRAW_AHEAD", "1") != "0"
+
+    def _draw_ahead_plan(self):
+        """(column plan, its UniformDraw, P) when the next draw can be made ahead, else None."""
+        if not (self._SPEC_DRAW and self._spec_ok) or self._ushadow.active:
+            return None
+        c = self._uniform_cache
+        if c is None or c[1] is None or len(c) < 3 or not self._uniform_same(c[2]):
+            return None
+        st = c[1]
+        if st[9] is None or len(st[1]) > 16:  # (equal widths; at most 16 columns in the merged launch)
+            return None
+        N = st[0]
+        h = self._uniform_host
+        if h is None or h[0] is not st:
+            h = self._uniform_host = (st, N.load_host().UniformDraw(
+                st[3], st[7], len(st[2]), st[2][0], st[1], st[6], len(st[1]), [int(o) for o in st[9]], st[4],
+                N.fn_addr("vmas_uniform_columns_snap"), N.fn_addr("vmas_aux_last_error")))
+        if not self._preapply_columns(st):
+            return None
+        return st, h[1], self._u_persist[1]
+
+    def _drew_ahead(self, st, acts, snap, seed, offset, inc) -> None:
+        self._ushadow.arm(self._u_persist[1], snap)
+        self._spec = (st, acts, seed, offset, inc, self._preapply_tag)
+
+    def _take_spec(self, sp):
+        """The draw made ahead, if it is what a draw now would give: the same generator state, the
+        same column plan and applied-column fields."""
+        st, acts, seed, offset, inc, tag = sp
+        gen = st[5]
+        if gen.initial_seed() != seed or gen.get_offset() != offset or not self._preapply_columns(st) \
+                or self._preapply_tag is not tag:
+            return None
+        gen.set_offset(offset + inc)
+        self._drawn = (tuple(acts), tuple(o.data_ptr() for o in acts), tuple(o._version for o in acts),
+                       self._u_persist[1])
+        return acts
 
     # ---- random actions drawn and applied in one launch (graph mode) -----------------------------
     def _preapply_columns(self, st):
@@ -680,6 +736,7 @@ class Environment(TorchVectorizedObject):
             if act._u is not us[i]:  # (bound by the previous step already: the setter's checks passed)
                 act.u = us[i]
         self.preapplied_steps += 1
+        self._spec_ok = True
         return True
 
     def _uniform_sig(self):
