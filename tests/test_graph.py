@@ -369,8 +369,12 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substep
             env.world._sub_dt = env.world._dt / substeps
     for t in range(12):
         s = _rng_save()
+        if t == 5:  # a device draw between the step and get_random_actions: the draw made ahead by
+            torch.rand(7, device=gpu_device)  # the post-replay launch is not handed out
         a_e = eager.get_random_actions()
         _rng_load(s)
+        if t == 5:
+            torch.rand(7, device=gpu_device)
         a_g = graph.get_random_actions()
         _assert_same(a_e, a_g, f"draws step {t}")
         # the draw leaves the agents alone: between the draw and the step, action.u
@@ -394,6 +398,8 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substep
         assert torch.equal(eager.steps, graph.steps), (name, t)
     assert graph.graph_status == "graph", graph.graph_reason
     assert graph.preapplied_steps >= 5
+    if name == "balance":  # (no device asserts, no deferred launch: the last step drew the next actions ahead)
+        assert graph._SPEC_DRAW and graph._spec is not None
 
 
 @pytest.mark.gpu
