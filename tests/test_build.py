@@ -49,3 +49,13 @@ def test_kernels_use_no_scratch(tmp_path):
     assert any("k_flocking_fast" in n for n in sizes)
     bad = {n: s for n, s in sizes.items() if s and n not in ALLOWED_SCRATCH}
     assert not bad, bad
+
+
+def test_no_memset_calls_that_a_capture_could_record():
+    """No hipMemsetAsync in the library's sources (a stream capture would record it as a memset
+    node; two graph-mode failures traced to captured memset nodes on ROCm 7.2 / MI355X, DESIGN.md
+    "Graph mode"): stream-ordered clears go through a kernel (vmas_aux::fill_u32_async)."""
+    csrc = ROOT / "vectorizedmultiagentsimulator_amd" / "csrc"
+    for f in sorted(csrc.glob("*.hip")) + sorted(csrc.glob("*.hpp")) + sorted(csrc.glob("*.cpp")):
+        code = re.sub(r"//[^\n]*", "", f.read_text())  # (comments may name it)
+        assert "hipMemsetAsync" not in code and "hipMemsetD" not in code, f.name

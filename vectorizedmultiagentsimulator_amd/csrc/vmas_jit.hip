@@ -184,6 +184,10 @@ struct Gen {
     int E, P, A, J, W, nfl;
     bool split_boxes = true;
     long lds_budget = kLdsTwoPerCu;
+    // rows in a global-memory slab (one per workgroup, a.rows) instead of LDS: worlds whose rows
+    // exceed one workgroup's LDS (hundreds of box pairs) still run the world-specialised step and
+    // its persistent fixed point; the rows' traffic then goes through L1 / L2
+    bool global_rows = false;
     int nw = kNW;         // waves per workgroup
     int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
     bool relaxed = false;  // relaxed fp32 math (VMAS_JIT_MATH=relaxed, worlds without joints; see compile())
@@ -356,8 +360,9 @@ struct Gen {
         for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : res_rows(p));
         // rows + FL + DONE + the pass's mask words + the fixed point's reduction words (in the
         // row buffer when it is large enough)
-        const long red = (long)std::max(n_rows, 1) * 64 >= nfl + 2 ? 0 : nfl + 2;
-        const long lds = (long)n_rows * 256 + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) + 4 * red;
+        const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 >= nfl + 2) ? 0 : nfl + 2;
+        const long lds = (global_rows ? 0L : (long)n_rows * 256) + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) +
+                         4 * red;
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
             return false;
@@ -397,7 +402,8 @@ struct Gen {
 
     size_t arg_bytes() const {  // layout of the generated struct Args
         // (+4 ints: B, S, sdt, max_pass; then the value slots; padded to the 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7) + 4 * (std::max<size_t>(str_src.size(), 2) + 4) +
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)) +
+                         4 * (std::max<size_t>(str_src.size(), 2) + 4) +
                          4 * prm_src.size();
         return (n + 7) & ~(size_t)7;
     }
@@ -901,7 +907,8 @@ struct Gen {
         o += "#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[" + it(n_out()) + "];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
-             "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n"
+             "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n" +
+             std::string(global_rows ? "    float* rows;\n" : "") +
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n"
              "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
              "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
@@ -948,7 +955,10 @@ struct Gen {
             o += "}\n\n";
         }
         o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
-        o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
+        if (global_rows)  // (this workgroup's slab: the same [row][lane] layout as the LDS rows)
+            o += "    float* L = a.rows + (size_t)blockIdx.x * " + it((long)std::max(n_rows, 1) * 64) + ";\n";
+        else
+            o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
@@ -956,7 +966,7 @@ struct Gen {
         const int red_words = nfl + 2;
         o += "    __shared__ uint32_t MSK[" + it(std::max(nfl / 2, 1)) + "];\n";
         o += "    __shared__ uint32_t QL[66];\n";
-        if ((long)std::max(n_rows, 1) * 64 >= red_words)
+        if (!global_rows && (long)std::max(n_rows, 1) * 64 >= red_words)
             o += "    uint32_t* RED = reinterpret_cast<uint32_t*>(L);\n";
         else
             o += "    __shared__ uint32_t RED[" + it(red_words) + "];\n";
@@ -1035,7 +1045,9 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
     const struct {
         bool split;
         long budget;
-    } tries[] = {{true, kLdsTwoPerCu}, {false, kLdsTwoPerCu}, {false, kLdsOnePerCu}};
+        bool global_rows;
+    } tries[] = {{true, kLdsTwoPerCu, false}, {false, kLdsTwoPerCu, false}, {false, kLdsOnePerCu, false},
+                 {false, kLdsOnePerCu, true}};
     for (const auto& t : tries) {
         if (t.split && !allow_split) continue;
         std::unique_ptr<Gen> g(new Gen(cfg, ed, pd, jd));
@@ -1046,6 +1058,7 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
         }
         g->split_boxes = t.split;
         g->lds_budget = t.budget;
+        g->global_rows = t.global_rows;
         // 16 waves per workgroup once there are enough pair tasks to spread (measured: flocking
         // 81 pairs 72 -> 59 us, discovery 19.2 -> 16.3 us; balance's 24 tasks 67.7 -> 69.7 us)
         int n_tasks = 0;
@@ -1223,6 +1236,9 @@ struct VmasJitWorld {
     // from a HIP graph are timed too (HIP records no events inside a graph; vmas_jit_ops.hpp)
     unsigned long long* d_tm = nullptr;
     int wall_khz = 0;
+    // rows in global memory (Gen::global_rows): one slab of n_rows x 64 floats per workgroup
+    bool global_rows = false;
+    float* d_rows = nullptr;
 };
 
 extern "C" {
@@ -1246,6 +1262,7 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
         if (W->d_viol) (void)hipFree(W->d_viol);
         if (W->h_viol) (void)hipHostFree(W->h_viol);
         if (W->d_prof) (void)hipFree(W->d_prof);
+        if (W->d_rows) (void)hipFree(W->d_rows);
         if (W->d_ctl) (void)hipFree(W->d_ctl);
         if (W->d_err) (void)hipFree(W->d_err);
         if (W->h_err) (void)hipHostFree(W->h_err);
@@ -1355,6 +1372,11 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             if (const char* cap = getenv("VMAS_JIT_GRID_CAP")) W->grid = std::max(1, std::min(W->grid, atoi(cap)));
             if (const char* r = getenv("VMAS_JIT_MAX_PASSES")) W->max_passes = std::max(1, atoi(r));
         }
+    }
+    W->global_rows = g.global_rows;
+    if (g.global_rows) {  // (a slab per workgroup of the largest grid: the host-driven loop's nblk)
+        const size_t slab = (size_t)std::max(W->nblk, W->grid) * (size_t)std::max(g.n_rows, 1) * 64 * 4;
+        if (hipMalloc((void**)&W->d_rows, slab) != hipSuccess) return cleanup(jfail(VMAS_E_NOMEM, "hipMalloc row slabs"));
     }
     if (g.prof_block >= 0) {
         W->n_prof = ((size_t)cfg->max_substeps * 4 + 2) * kMaxNW + (size_t)kProfBlocks * kProfRec;
@@ -1470,6 +1492,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(W->d_err);
     put_ptr(W->dh_err);
     put_ptr(W->timing && persistent ? W->d_tm : nullptr);
+    if (W->global_rows) put_ptr(W->d_rows);
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
         int32_t v = 0;
