@@ -132,3 +132,14 @@ def distance_parity(env, atol=2e-5):
             eo = ow.is_overlapping(ow.ents[i], ow.ents[j])
             mism += int((go != eo).sum())
     return {"ok": worst <= atol and mism == 0, "max_abs": worst, "overlap_mismatch": mism}
+
+
+def assert_aggregate(rec, p999_bound, mean_bound):
+    """Aggregate error guard over envs: the per-step tolerance admits a
+    contact-cut-off env's large error, so a systematic error of 100x could pass it; the 99.9th
+    percentile and the mean over envs of the per-env max |diff| cannot move that far without a
+    real regression.  Bounds are ~10x the values measured on gfx950."""
+    for k, bnd in p999_bound.items():
+        assert rec["p999_abs"].get(k, 0.0) <= bnd, (rec["config"], "p99.9", k, rec["p999_abs"].get(k), bnd)
+    for k, bnd in mean_bound.items():
+        assert rec["mean_abs"].get(k, 0.0) <= bnd, (rec["config"], "mean", k, rec["mean_abs"].get(k), bnd)
