@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
@@ -22,10 +23,12 @@ constexpr int kCopyThreads = 256, kCopyUnroll = 4, kMaxCopyBlocks = 1024;
 struct CopyArgs {
     VmasCopySpan s[VMAS_COPY_MAX_SPANS];
     int n;
+    int nt;  // non-temporal stores (VMAS_COPY_NT=1, an A/B knob): the destinations are fresh tensors
 };
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 static_assert(sizeof(CopyArgs) <= 4096, "kernel argument block");
 
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restrict__ dst, int64_t n) {
     const int64_t step = (int64_t)gridDim.x * kCopyThreads;
     int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x;
@@ -34,12 +37,15 @@ __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restr
 #pragma unroll
         for (int k = 0; k < kCopyUnroll; ++k) v[k] = src[i + k * step];  // independent loads in flight
 #pragma unroll
-        for (int k = 0; k < kCopyUnroll; ++k) dst[i + k * step] = v[k];
+        for (int k = 0; k < kCopyUnroll; ++k) {
+            if constexpr (NT) __builtin_nontemporal_store(v[k], dst + i + k * step);
+            else dst[i + k * step] = v[k];
+        }
     }
     for (; i < n; i += step) dst[i] = src[i];
 }
 
-__device__ __forceinline__ void copy_span(const VmasCopySpan& s) {
+__device__ __forceinline__ void copy_span(const VmasCopySpan& s, bool nt = false) {
     if (!s.src) {  // an increment span: dst[i] += 1.0f
         float* d = reinterpret_cast<float*>(s.dst);
         const int64_t n = s.nbytes / 4;
@@ -48,7 +54,9 @@ __device__ __forceinline__ void copy_span(const VmasCopySpan& s) {
         return;
     }
     const uintptr_t al = (uintptr_t)s.src | (uintptr_t)s.dst | (uintptr_t)s.nbytes;
-    if ((al & 15) == 0)
+    if ((al & 15) == 0 && nt)
+        copy_units<u32x4, true>(reinterpret_cast<const u32x4*>(s.src), reinterpret_cast<u32x4*>(s.dst), s.nbytes / 16);
+    else if ((al & 15) == 0)
         copy_units(reinterpret_cast<const uint4*>(s.src), reinterpret_cast<uint4*>(s.dst), s.nbytes / 16);
     else if ((al & 3) == 0)
         copy_units(reinterpret_cast<const uint32_t*>(s.src), reinterpret_cast<uint32_t*>(s.dst), s.nbytes / 4);
@@ -56,7 +64,7 @@ __device__ __forceinline__ void copy_span(const VmasCopySpan& s) {
         copy_units(reinterpret_cast<const uint8_t*>(s.src), reinterpret_cast<uint8_t*>(s.dst), s.nbytes);
 }
 
-__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) { copy_span(a.s[blockIdx.y]); }
+__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) { copy_span(a.s[blockIdx.y], a.nt != 0); }
 
 // The post-replay copies and the next step's random-action draw in ONE launch (vmas_copy_spans_draw):
 // blockIdx.y < n_spans copies span y (grid-stride over gridDim.x), the rest draw column
@@ -101,9 +109,11 @@ hipError_t vmas_aux::fill_u32_async(void* dst, uint32_t value, size_t n_words, h
 extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, void* stream) {
     if (n < 0 || (n > 0 && !spans) || device < 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad arguments");
     VMAS_AUX_HIP(hipSetDevice(device));
+    static const int nt = getenv("VMAS_COPY_NT") && getenv("VMAS_COPY_NT")[0] == '1';
     for (int first = 0; first < n; first += VMAS_COPY_MAX_SPANS) {
         CopyArgs a{};
         a.n = 0;
+        a.nt = nt;
         int64_t most = 0;  // units of the largest span (16-byte units: sets the grid)
         for (int i = first; i < std::min(n, first + VMAS_COPY_MAX_SPANS); ++i) {
             const VmasCopySpan& s = spans[i];
