@@ -398,8 +398,8 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substep
         assert torch.equal(eager.steps, graph.steps), (name, t)
     assert graph.graph_status == "graph", graph.graph_reason
     assert graph.preapplied_steps >= 5
-    if name == "balance":  # (no device asserts, no deferred launch: the last step drew the next actions ahead)
-        assert graph._SPEC_DRAW and graph._spec is not None
+    if name == "balance":  # (no device asserts, no deferred launch: draws were made ahead and handed out)
+        assert graph._SPEC_DRAW and getattr(graph, "drawn_ahead", 0) >= 3
 
 
 @pytest.mark.gpu

@@ -655,6 +655,7 @@ class Environment(TorchVectorizedObject):
         gen.set_offset(offset + inc)
         self._drawn = (tuple(acts), tuple(o.data_ptr() for o in acts), tuple(o._version for o in acts),
                        self._u_persist[1])
+        self.drawn_ahead = getattr(self, "drawn_ahead", 0) + 1
         return acts
 
     # ---- random actions drawn and applied in one launch (graph mode) -----------------------------
