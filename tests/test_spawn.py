@@ -97,3 +97,43 @@ def test_respawn_targets_matches_reference_loop_gpu(gpu_device, monkeypatch, b, 
         for i, (e, x) in enumerate(zip(exp, got)):
             assert torch.equal(e, x), f"target {i}"
         assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"
+
+
+@pytest.mark.gpu
+def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device):
+    """The one-launch respawn's resident kernel needs every 64-env group's workgroup running at
+    once.  Here a kernel on a second stream holds 250 CUs for 1.5 s -- longer than the
+    launch's 1 s bounded wait -- so the groups that cannot start make the others time out.  The
+    call then undoes the launch from its backup and redoes the respawn with the reference's loop:
+    the reference's positions and generator use, no error."""
+    import ctypes
+
+    from vectorizedmultiagentsimulator_amd import _native as N
+    from vectorizedmultiagentsimulator_amd.scenarios.discovery import respawn_targets_native
+
+    dev, b, a, t, min_dist = gpu_device, 16384, 8, 7, 0.2
+    g = _gen(dev)
+    g.manual_seed(11)
+    agents = torch.empty((b, a, 2), device=dev).uniform_(-1, 1)
+    tpos0 = [torch.empty((b, 2), device=dev).uniform_(-1, 1) for _ in range(t)]
+    covered = torch.rand(b, t, device=dev) < 0.3
+    exp = [p.clone() for p in tpos0]
+    g.manual_seed(12)
+    for i in range(t):
+        occ = torch.cat([agents] + [exp[j].unsqueeze(1) for j in range(t) if j != i], dim=1)
+        pos = O.find_random_pos_for_entity(occ, b, dev, min_dist, (-1.0, 1.0), (-1.0, 1.0))
+        exp[i] = torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), exp[i])
+    after_ref = torch.rand(4, device=dev)
+    got = [p.clone() for p in tpos0]
+    g.manual_seed(12)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    N.check_aux(N.load_library().vmas_test_hold(0, 250, 1_500_000, ctypes.c_void_p(side.cuda_stream)),
+                "vmas_test_hold")
+    mx = respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
+    after_native = torch.rand(4, device=dev)
+    torch.cuda.synchronize()
+    for i, (e, x) in enumerate(zip(exp, got)):
+        assert torch.equal(e, x), f"target {i}"
+    assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"
+    assert int(mx[N.VMAS_SPAWN_ERR_WORD].item()) == 1  # (the contended launch did time out)
