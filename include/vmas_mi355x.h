@@ -41,8 +41,9 @@ extern "C" {
 
 /* v3: VmasDiscoveryIO gained covered_count / all_time / done; increment spans (src NULL) in
  * vmas_copy_spans; VMAS_COPY_MAX_SPANS 160
- * v4: VmasSpawnTargetsIO max_tries / backup; vmas_uniform_columns_snap */
-#define VMAS_ABI_VERSION 4
+ * v4: VmasSpawnTargetsIO max_tries / backup; vmas_uniform_columns_snap
+ * v5: VmasSpawnTargetsIO scratch / scratch_words (the windowed respawn), vmas_spawn_scratch_words */
+#define VMAS_ABI_VERSION 5
 
 /* error codes */
 #define VMAS_OK 0
@@ -428,9 +429,18 @@ typedef struct VmasSpawnTargetsIO {
                                              launch (written by it), so that the caller can undo the launch:
                                              an unresolved env or a timed-out wait is then redone by the
                                              reference's unbounded loop (scenarios/discovery.py) */
+    int32_t* scratch;                     /* optional (v5) device words for the windowed kernel (one hand-off
+                                             between workgroups per call instead of one per target): at least
+                                             vmas_spawn_scratch_words(batch, n_targets); null: the per-target
+                                             kernels.  An env left without an accepted try inside the window
+                                             (128 tries of the call's shared stream, VMAS_SPAWN_WINDOW) counts
+                                             as unresolved, as past max_tries */
+    int64_t scratch_words;
 } VmasSpawnTargetsIO;
 #define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets) + 32 * 32)
 #define VMAS_SPAWN_ERR_WORD 64
+/* scratch words of the windowed kernel for (batch, n_targets); -1 for bad arguments */
+int64_t vmas_spawn_scratch_words(int32_t batch, int32_t n_targets);
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream);
 /* Spawn channel: mapped pinned host words between the host and a (captured) vmas_spawn_targets
  * launch, so that a graph-mode step keeps the respawn inside its one graph: the host arms the

@@ -12,7 +12,7 @@ ROOT = Path(__file__).resolve().parent.parent
 
 def declared_functions():
     text = (ROOT / "include" / "vmas_mi355x.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(vmas_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(vmas_\w+)\s*\(", text, re.M)))
 
 
 def test_library_loads_and_abi_version():

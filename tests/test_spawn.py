@@ -59,10 +59,68 @@ def test_spawn_matches_reference_loop_gpu(gpu_device, b, n_occ, min_dist):
         assert _uniform.MODES.get((str(torch.device(gpu_device)), b)) is not None
 
 
+def _respawn_case(dev, b, a, t, min_dist, seed, cov_p):
+    """The reference loop and the native call on the same inputs: (expected, got, generator states
+    after each, the native call's words)."""
+    from vectorizedmultiagentsimulator_amd.scenarios.discovery import respawn_targets_native
+
+    g = _gen(dev)
+    g.manual_seed(seed)
+    agents = torch.empty((b, a, 2), device=dev).uniform_(-1, 1)
+    tpos0 = [torch.empty((b, 2), device=dev).uniform_(-1, 1) for _ in range(t)]
+    covered = torch.rand(b, t, device=dev) < cov_p
+    exp = [p.clone() for p in tpos0]
+    g.manual_seed(seed + 1)
+    for i in range(t):
+        occ = torch.cat([agents] + [exp[j].unsqueeze(1) for j in range(t) if j != i], dim=1)
+        pos = O.find_random_pos_for_entity(occ, b, dev, min_dist, (-1.0, 1.0), (-1.0, 1.0))
+        exp[i] = torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), exp[i])
+    after_ref = torch.rand(4, device=dev)
+    got = [p.clone() for p in tpos0]
+    g.manual_seed(seed + 1)
+    mx = respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
+    after_native = torch.rand(4, device=dev)
+    for i, (e, x) in enumerate(zip(exp, got)):
+        assert torch.equal(e, x), f"target {i}"
+    assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"
+    return mx
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("b,a,t,min_dist,cov_p,window,resolves", [
+    (16384, 8, 7, 0.2, 0.001, 128, True),    # C4: ~0.7 % of envs with a covered target
+    (16384, 8, 7, 0.2, 0.003, 128, True),    # ~340 listed envs (the chain holds 480 at 7 targets)
+    (131072, 8, 7, 0.2, 0.0004, 128, True),  # 2 048 groups
+    (333, 4, 16, 0.2, 0.02, 128, None),      # 16 targets (~16 x 9 tries: past the window, handed over)
+    (333, 4, 16, 0.1, 0.02, 128, True),      # 16 targets that fit the window
+    (1, 3, 2, 0.2, 1.0, 128, True),          # one env, both targets covered
+    (64, 0, 1, 0.2, 0.5, 128, True),         # nothing occupied: one try
+    (4096, 5, 7, 0.45, 0.01, 128, None),     # dense: the window may run out (then the hand-over)
+    (16384, 8, 7, 0.2, 0.001, 16, False),    # a 16-try window: unresolved, handed over
+    (16384, 8, 7, 0.2, 0.3, 128, False),     # most envs covered: the list overflows, handed over
+])
+def test_respawn_window_matches_reference_loop_gpu(gpu_device, monkeypatch, b, a, t, min_dist, cov_p, window,
+                                                   resolves):
+    """The windowed respawn (k_spawn_window: every group evaluates the tries [0, window) of its envs
+    once, the last group walks the targets' chain): the reference loop's positions bit for bit and
+    its generator use -- resolved inside the launch (words[T] == 0) where the window and the list
+    capacity hold, else handed over to the reference loop with the same result."""
+    from vectorizedmultiagentsimulator_amd import _native as N
+
+    monkeypatch.setenv("VMAS_SPAWN_KERNEL", "window")
+    monkeypatch.setenv("VMAS_SPAWN_WINDOW", str(window))
+    for seed in range(3):
+        mx = _respawn_case(gpu_device, b, a, t, min_dist, seed, cov_p)
+        if resolves is not None:
+            assert (int(mx[t].item()) == 0) == resolves, int(mx[t].item())
+        assert int(mx[N.VMAS_SPAWN_ERR_WORD].item()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["window", "resident"])
 @pytest.mark.parametrize("max_tries", [0, 2, 7], ids=["bounded65536", "handover2", "handover7"])
 @pytest.mark.parametrize("b,a,t,min_dist", [(1, 3, 2, 0.2), (16384, 8, 7, 0.2), (4096, 5, 7, 0.45), (333, 4, 16, 0.2), (131072, 8, 7, 0.2)])
-def test_respawn_targets_matches_reference_loop_gpu(gpu_device, monkeypatch, b, a, t, min_dist, max_tries):
+def test_respawn_targets_matches_reference_loop_gpu(gpu_device, monkeypatch, b, a, t, min_dist, max_tries, kernel):
     """Discovery's respawn loop (discovery.py:237-252: per target, find_random_pos_for_entity over
     the agents and every other target, then where(covered)) as ONE stream-ordered native call
     (vmas_spawn_targets, tries drawn on the device): the loop's positions bit for bit and the
@@ -70,37 +128,16 @@ def test_respawn_targets_matches_reference_loop_gpu(gpu_device, monkeypatch, b, 
     left unresolved after that many tries hand the call over to the reference's unbounded loop
     (the launch undone from its backup; ref utils.py:285-318 warns and keeps trying) -- the same
     positions and generator use, never a half-moved set of targets."""
-    from vectorizedmultiagentsimulator_amd.scenarios.discovery import respawn_targets_native
-
     monkeypatch.setenv("VMAS_SPAWN_TEST_MAX_TRIES", str(max_tries))
+    monkeypatch.setenv("VMAS_SPAWN_KERNEL", kernel)
     if max_tries and b > 16384:
         pytest.skip("(the hand-over's host loop at this size only repeats the 16 384-env case)")
-
-    dev = gpu_device
     for seed in range(3):
-        g = _gen(dev)
-        g.manual_seed(seed)
-        agents = torch.empty((b, a, 2), device=dev).uniform_(-1, 1)
-        tpos0 = [torch.empty((b, 2), device=dev).uniform_(-1, 1) for _ in range(t)]
-        covered = torch.rand(b, t, device=dev) < 0.3
-        exp = [p.clone() for p in tpos0]
-        g.manual_seed(seed + 1)
-        for i in range(t):
-            occ = torch.cat([agents] + [exp[j].unsqueeze(1) for j in range(t) if j != i], dim=1)
-            pos = O.find_random_pos_for_entity(occ, b, dev, min_dist, (-1.0, 1.0), (-1.0, 1.0))
-            exp[i] = torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), exp[i])
-        after_ref = torch.rand(4, device=dev)
-        got = [p.clone() for p in tpos0]
-        g.manual_seed(seed + 1)
-        respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
-        after_native = torch.rand(4, device=dev)
-        for i, (e, x) in enumerate(zip(exp, got)):
-            assert torch.equal(e, x), f"target {i}"
-        assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"
+        _respawn_case(gpu_device, b, a, t, min_dist, seed, 0.3 if kernel == "resident" else 0.002)
 
 
 @pytest.mark.gpu
-def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device):
+def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device, monkeypatch):
     """The one-launch respawn's resident kernel needs every 64-env group's workgroup running at
     once.  Here a kernel on a second stream holds 250 CUs for 1.5 s -- longer than the
     launch's 1 s bounded wait -- so the groups that cannot start make the others time out.  The
@@ -111,6 +148,7 @@ def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device):
     from vectorizedmultiagentsimulator_amd import _native as N
     from vectorizedmultiagentsimulator_amd.scenarios.discovery import respawn_targets_native
 
+    monkeypatch.setenv("VMAS_SPAWN_KERNEL", "resident")  # (the windowed kernel has no wait to time out)
     dev, b, a, t, min_dist = gpu_device, 16384, 8, 7, 0.2
     g = _gen(dev)
     g.manual_seed(11)

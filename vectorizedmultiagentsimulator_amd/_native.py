@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("VMAS_LIB_PATH") or Path(__file__).resolve().pare
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
-VMAS_ABI_VERSION = 4
+VMAS_ABI_VERSION = 5
 VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
 (
     VMAS_PAIR_JOINT,
@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "vmas_balance_outputs",
     "vmas_copy_spans",
     "vmas_spawn_targets",
+    "vmas_spawn_scratch_words",
     "vmas_spawn_channel_create",
     "vmas_spawn_channel_destroy",
     "vmas_spawn_channel_arm",
@@ -268,7 +269,7 @@ class VmasSpawnTargetsIO(ctypes.Structure):
         ("covered", _vp), ("cov_s0", _i32), ("cov_s1", _i32),
         ("min_dist", _f32), ("x_lo", _f32), ("x_hi", _f32), ("y_lo", _f32), ("y_hi", _f32), ("pad1", _f32),
         ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp), ("channel", _vp),
-        ("backup", _vp),
+        ("backup", _vp), ("scratch", _vp), ("scratch_words", ctypes.c_int64),
     ]
 
 
@@ -537,6 +538,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_world_step_vjp.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     lib.vmas_spawn_targets.restype = _i32
     lib.vmas_spawn_targets.argtypes = [_i32, _vp, ctypes.POINTER(ctypes.c_uint64), _vp]
+    lib.vmas_spawn_scratch_words.restype = ctypes.c_int64
+    lib.vmas_spawn_scratch_words.argtypes = [_i32, _i32]
     lib.vmas_spawn_channel_create.restype = _i32
     lib.vmas_spawn_channel_create.argtypes = [_i32, ctypes.POINTER(_vp)]
     lib.vmas_spawn_channel_destroy.restype = _i32

@@ -596,6 +596,543 @@ __global__ void __launch_bounds__(256) k_spawn_clear(int32_t* w, int n, const ui
             __hip_atomic_load(chan_in + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- the windowed respawn (k_spawn_cands + k_spawn_chain): no hand-off per target ---------------
+//
+// Every target draws from ONE stream of tries: try k of target i is pair p = P_i + k of the
+// generator stream (x at offset o + p * per_try, y at + inc), P_0 = 0, P_{i+1} = P_i + consumed_i.
+// So an env's candidates do not depend on the chain -- only WHICH pair each target starts at does,
+// through the earlier targets' batch-global maxima.  The resident kernel resolves the targets one
+// after another with a grid-wide hand-off per target (7 x ~9.5 us at C4).  Here k_spawn_cands
+// evaluates the pairs [0, W) of every env once (W = the window, 128 by default: C4 consumes ~84),
+// keeping per env and target a W-bit mask of the pairs that overlap nothing, and reduces per 64-env
+// group, for every (target i, start pair P), the max over its envs of the first accepted try after
+// P: k_e(i, P) = next_ok_e,i(P) - P.  k_spawn_chain (one workgroup) reduces those tables over the
+// groups and walks the chain P_0 -> P_1 -> ... with table lookups.
+//
+// The masks hold target i's occupied set before the call except that an env with a covered target
+// j < i ("dirty" for i) has j at its NEW position, which depends on P_j.  Those envs (every env with a
+// covered target; ~0.6 % at C4) leave the tables for the targets after their first covered one and
+// go to a list instead: their masks are taken against the agents and the targets that do not move
+// before i, and the chain tests the surviving candidates against the moved targets while it walks,
+// one thread per listed env, then writes every covered target's new position.  Nothing else
+// moves; no co-residency, no bounded wait.  An env with no accepted pair inside the window, a list
+// longer than the chain's capacity, or an env past max_tries marks the call unresolved: the caller
+// redoes it with the reference loop (scenarios/discovery.py).
+constexpr int kWinThreads = 1024, kWinWaves = kWinThreads / 64;
+constexpr int kWinMaxPairs = 128;  // the masks' width
+constexpr int kWinListWord = 33;   // (max_accepted words) listed envs
+constexpr int kWinChainLds = 150 * 1024;
+
+// listed envs the chain holds: masks (T x 16 B), new positions, two candidates (T x 3 x 8 B), their
+// pairs (T x 4 B), env + covered bits
+__host__ __device__ inline int win_list_cap(int T) {
+    const int c = (kWinChainLds - T * kWinMaxPairs) / (T * 44 + 8);
+    return (c > kWinThreads ? kWinThreads : c) & ~3;  // (even: the reduction buffer after it stays 16-byte aligned)
+}
+
+struct WinArgs {
+    uint32_t* part;   // [groups][T * 32]: a group's table, 4 start pairs (bytes) per word
+    uint32_t* crow;   // [clusters][T * 32]: a cluster's table
+    uint32_t* list;   // [cap][2 + 4 T]: env, covered bits, T 128-bit masks
+    int cap, pairs, q0;
+};
+constexpr int kWinCluster = 16;  // groups per cluster (the first reduction of the tables)
+// (max_accepted words) cluster c's count: the per-target kernels' replica words, free here
+__host__ __device__ inline int win_cluster_word(int T) { return 96 + 32 * T; }
+
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// per-byte maximum of two words (two packed 16-bit maxima)
+__device__ __forceinline__ uint32_t bytes_max(uint32_t a, uint32_t b) {
+    const u16x2 lo = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a & 0x00FF00FFu),
+                                               __builtin_bit_cast(u16x2, b & 0x00FF00FFu));
+    const u16x2 hi = __builtin_elementwise_max(__builtin_bit_cast(u16x2, (a >> 8) & 0x00FF00FFu),
+                                               __builtin_bit_cast(u16x2, (b >> 8) & 0x00FF00FFu));
+    return __builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8);
+}
+
+// max over the wave of non-negative v (DPP row shifts, then the row broadcasts)
+__device__ __forceinline__ int wave_max_nonneg(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// the first set bit >= P of a 128-bit mask (kWinMaxPairs when none)
+__device__ __forceinline__ int next_bit128(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3, int P) {
+    if (P >= kWinMaxPairs) return kWinMaxPairs;
+    const unsigned long long lo = ((unsigned long long)m1 << 32) | m0, hi = ((unsigned long long)m3 << 32) | m2;
+    if (P < 64) {
+        const unsigned long long x = lo & (~0ull << P);
+        if (x) return __builtin_ctzll(x);
+        return hi ? 64 + __builtin_ctzll(hi) : kWinMaxPairs;
+    }
+    const unsigned long long x = hi & (~0ull << (P - 64));
+    return x ? 64 + __builtin_ctzll(x) : kWinMaxPairs;
+}
+
+// uniform_at when torch's grid covers the batch in one round (B <= step, so q = 0): one philox
+// block, component off & 3 -- branch-free, so that the x and y draws of several pairs interleave
+__device__ __forceinline__ float draw_q0(unsigned long long seed, unsigned long long off, int b, float lo, float hi,
+                                         int mode) {
+    const unsigned long long c = off / 4;
+    const uint4 r = philox10(make_uint4((unsigned int)c, (unsigned int)(c >> 32), (unsigned int)b, 0u),
+                             make_uint2((unsigned int)seed, (unsigned int)(seed >> 32)));
+    const int sub = (int)(off & 3ull);
+    const unsigned int u = sub == 0 ? r.x : sub == 1 ? r.y : sub == 2 ? r.z : r.w;
+    const float inv = 2.3283064e-10f;  // ROCRAND_2POW32_INV
+    const float unit = (mode & 1) ? __builtin_fmaf((float)u, inv, inv) : inv + (float)u * inv;
+    const float range = hi - lo;
+    const float val = (mode & 2) ? __builtin_fmaf(unit, range, lo) : unit * range + lo;
+    return val == hi ? lo : val;
+}
+
+__device__ __forceinline__ float2 spawn_pair(const VmasSpawnTargetsIO& io, const DrawGrid& g, bool q0,
+                                             unsigned long long seed, unsigned long long off0, int p, int b) {
+    const unsigned long long o = off0 + (unsigned long long)p * 2ull * g.inc;
+    if (q0)
+        return make_float2(draw_q0(seed, o, b, io.x_lo, io.x_hi, io.mode),
+                           draw_q0(seed, o + g.inc, b, io.y_lo, io.y_hi, io.mode));
+    return make_float2(uniform_at(seed, o, g, b, io.x_lo, io.x_hi, io.mode),
+                       uniform_at(seed, o + g.inc, g, b, io.y_lo, io.y_hi, io.mode));
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// near() on packed pairs (v_pk_add_f32 / v_pk_mul_f32: each half rounds as the scalar form)
+__device__ __forceinline__ bool near_pk(f32x2 o, f32x2 c, float d2_min) {
+    const f32x2 d = o - c;
+    const f32x2 q = d * d;
+    return q.x + q.y < d2_min;
+}
+
+// (the chain's draws: one out-of-line copy -- the chain kernel runs on one CU, with a cold
+// instruction cache every call, so its code size is its latency)
+template <bool Q0>
+__device__ __noinline__ float2 spawn_pair_call(float x_lo, float x_hi, float y_lo, float y_hi, int mode,
+                                               long long step, unsigned long long inc, unsigned long long seed,
+                                               unsigned long long off0, int p, int b) {
+    const unsigned long long o = off0 + (unsigned long long)p * 2ull * inc;
+    if (Q0) return make_float2(draw_q0(seed, o, b, x_lo, x_hi, mode), draw_q0(seed, o + inc, b, y_lo, y_hi, mode));
+    const DrawGrid g{step, inc};
+    return make_float2(uniform_at(seed, o, g, b, x_lo, x_hi, mode), uniform_at(seed, o + inc, g, b, y_lo, y_hi, mode));
+}
+
+// ---- every group: candidates, masks, the group's table (and its listed envs) ----------------------
+// R pairs per wave (window 16 R); Q0: torch's grid covers the batch in one round (draw_q0)
+template <int R, bool Q0>
+__global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
+                                                             WinArgs wa, unsigned long long* prof, ChanArgs ch) {
+    extern __shared__ __align__(16) unsigned char win_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int T = io.n_targets, A = io.n_agents, n_occ = A + T, cols = T * 32;
+    const int b = (int)blockIdx.x * 64 + lane;
+    const bool valid = b < io.batch;
+    const int bb = valid ? b : io.batch - 1;
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+    float2* occ = reinterpret_cast<float2*>(win_lds);                // [n_occ][64]
+    uint32_t* okw = reinterpret_cast<uint32_t*>(occ + n_occ * 64);   // [T][64][4] the masks
+    uint32_t* covs = okw + T * 64 * 4;                               // [64] covered bits
+    unsigned long long* rng = reinterpret_cast<unsigned long long*>(covs + 64);  // [3]
+    for (int m = wave; m < n_occ; m += kWinWaves) {
+        const float* p;
+        int s1;
+        if (m < A) {
+            p = io.agents + (long)bb * io.ag_s0 + (long)m * io.ag_s1;
+            s1 = io.ag_s2;
+        } else {
+            p = io.pos[m - A] + (long)bb * io.pos_s0[m - A];
+            s1 = io.pos_s1[m - A];
+        }
+        const float2 v = make_float2(p[0], p[s1]);
+        occ[m * 64 + lane] = v;
+        if (m >= A && io.backup && valid) {  // the targets' positions before the call
+            float* q = io.backup + ((long)(m - A) * io.batch + b) * 2;
+            q[0] = v.x;
+            q[1] = v.y;
+        }
+    }
+    for (int q = (int)threadIdx.x; q < T * 64 * 4; q += kWinThreads) okw[q] = 0u;
+    if (wave == 0) {
+        uint32_t cm = 0u;
+        if (valid)
+            for (int i = 0; i < T; ++i) cm |= io.covered[(long)b * io.cov_s0 + (long)i * io.cov_s1] ? (1u << i) : 0u;
+        covs[lane] = cm;
+    }
+    if (threadIdx.x == 0) launch_rng(io, ch, &rng[0], &rng[1], &rng[2]);
+    __syncthreads();
+    const unsigned long long seed = rng[0], off0 = rng[1];
+    const uint32_t covm = covs[lane];
+    {
+        // this wave's R pairs, all drawn first (independent philox chains in flight), then tested
+        // against each occupied position once
+        const int p0 = __builtin_amdgcn_readfirstlane(wave) * R;
+        f32x2 c[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float2 v = spawn_pair(io, g, Q0, seed, off0, p0 + r, bb);
+            c[r] = f32x2{v.x, v.y};
+        }
+        uint32_t hit = 0u;  // bit r: pair r lands near an agent
+        for (int m = 0; m < A; ++m) {
+            const float2 o = occ[m * 64 + lane];
+            const f32x2 o2{o.x, o.y};
+#pragma unroll
+            for (int r = 0; r < R; ++r) hit |= near_pk(o2, c[r], d2_min) ? (1u << r) : 0u;
+        }
+        uint32_t far[VMAS_SPAWN_MAX_TARGETS];  // bit r: pair r clear of target j's position before the call
+#pragma unroll
+        for (int j = 0; j < VMAS_SPAWN_MAX_TARGETS; ++j) {
+            uint32_t f = ~0u;
+            if (j < T) {
+                const float2 o = occ[(A + j) * 64 + lane];
+                const f32x2 o2{o.x, o.y};
+                f = 0u;
+#pragma unroll
+                for (int r = 0; r < R; ++r) f |= near_pk(o2, c[r], d2_min) ? 0u : (1u << r);
+            }
+            far[j] = f;
+        }
+        // target i's occupied set: every target after it, the targets before it that do not move
+        // (not covered), never itself -- prefix / suffix products of the clear-of bits
+        uint32_t suf[VMAS_SPAWN_MAX_TARGETS + 1];
+        suf[VMAS_SPAWN_MAX_TARGETS] = ~0u;
+#pragma unroll
+        for (int j = VMAS_SPAWN_MAX_TARGETS - 1; j >= 0; --j) suf[j] = suf[j + 1] & far[j];
+        const uint32_t rmask = (1u << R) - 1u;
+        const int s = p0, w0 = s >> 5, sh = s & 31;
+        uint32_t pre = ~0u;
+#pragma unroll
+        for (int i = 0; i < VMAS_SPAWN_MAX_TARGETS; ++i) {
+            const uint32_t ok = ~hit & rmask & pre & suf[i + 1];
+            pre &= ((covm >> i) & 1u) ? ~0u : far[i];
+            if (i < T && ok) {
+                atomicOr(&okw[(i * 64 + lane) * 4 + w0], ok << sh);
+                if (sh + R > 32) atomicOr(&okw[(i * 64 + lane) * 4 + w0 + 1], ok >> (32 - sh));
+            }
+        }
+    }
+    __syncthreads();
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[30] = __builtin_amdgcn_s_memrealtime();
+    uint32_t mk0 = 0u, mk1 = 0u, mk2 = 0u, mk3 = 0u;  // (wave i < T) the lane's mask of target i
+    if (wave < T) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&okw[(wave * 64 + lane) * 4]);
+        mk0 = v.x;
+        mk1 = v.y;
+        mk2 = v.z;
+        mk3 = v.w;
+    }
+    if (wave == 0 && valid && covm) {  // an env with a covered target: listed for the chain
+        const int d = atomicAdd(&io.max_accepted[kWinListWord], 1);
+        if (d < wa.cap) {
+            uint32_t* e = wa.list + (long)d * (2 + 4 * T);
+            e[0] = (uint32_t)b;
+            e[1] = covm;
+            for (int i = 0; i < T; ++i)
+                *reinterpret_cast<uint4*>(e + 2 + 4 * i) = *reinterpret_cast<const uint4*>(&okw[(i * 64 + lane) * 4]);
+        }
+    }
+    __syncthreads();  // (the masks are in registers: the space becomes the table)
+    uint32_t* ktab = reinterpret_cast<uint32_t*>(win_lds);  // [64][cols + 1]: byte P & 3 of word (i, P >> 2)
+    if (wave < T) {
+        // k(P) = the first accepted pair at or after P, minus P, for P = 127 .. 0 (255: none in the
+        // window); 0 for an env that is not in target i's table (dirty for i, or past the batch)
+        const int i = wave;
+        const bool in_table = valid && (covm & ((1u << i) - 1u)) == 0u;
+        uint32_t k = 255u, packed = 0u;
+#pragma unroll
+        for (int P = kWinMaxPairs - 1; P >= 0; --P) {
+            const uint32_t word = P < 32 ? mk0 : P < 64 ? mk1 : P < 96 ? mk2 : mk3;
+            const bool ok = (word >> (P & 31)) & 1u;  // (pairs past the window never set)
+            k = ok ? 0u : (k + 1u > 255u ? 255u : k + 1u);
+            packed |= (in_table ? k : 0u) << (8 * (P & 3));
+            if ((P & 3) == 0) {
+                ktab[lane * (cols + 1) + i * 32 + (P >> 2)] = packed;
+                packed = 0u;
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = (int)threadIdx.x; c < cols; c += kWinThreads) {  // the group's table: max over its 64 envs
+        uint32_t acc = 0u;
+#pragma unroll 8
+        for (int l = 0; l < 64; ++l) acc = bytes_max(acc, ktab[l * (cols + 1) + c]);
+        st_agent(wa.part + (long)blockIdx.x * cols + c, acc);
+    }
+    // The last group of each cluster of kWinCluster reduces the cluster's tables into one row (the
+    // chain then reads G / kWinCluster rows, not G: one workgroup pulls ~10 B per cycle from HBM).
+    // The rows go out as agent-scope stores and come back as agent-scope loads (another XCD's L2
+    // may hold the lines), landed before the cluster's count.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    __shared__ int last_s;
+    const int cl = (int)blockIdx.x / kWinCluster, first = cl * kWinCluster;
+    const int members = min(kWinCluster, (int)gridDim.x - first);
+    if (threadIdx.x == 0) last_s = atomicAdd(&io.max_accepted[win_cluster_word(T) + cl], 1) == members - 1;
+    __syncthreads();
+    if (last_s) {
+        const int per = kWinThreads / cols, c = (int)threadIdx.x % cols, r0 = (int)threadIdx.x / cols;
+        uint32_t acc = 0u;
+        if (r0 < per) {
+            uint32_t v[kWinCluster];
+#pragma unroll
+            for (int u = 0; u < kWinCluster; ++u) {
+                const int r = r0 + u * per;
+                v[u] = r < members ? ld_agent(wa.part + (long)(first + r) * cols + c) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kWinCluster; ++u) acc = bytes_max(acc, v[u]);
+        }
+        uint32_t* red = ktab;  // (the table space is free again)
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        if ((int)threadIdx.x < cols) {
+            for (int r = 1; r < per; ++r) acc = bytes_max(acc, red[r * cols + threadIdx.x]);
+            wa.crow[(long)cl * cols + threadIdx.x] = acc;
+        }
+    }
+    if (prof && threadIdx.x == 0) prof[32 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---- one workgroup: the tables over every group, then the chain of targets ------------------------
+// Chain of the targets.  (a) The clean chain: P_i from the reduced tables alone.  (b) Every listed
+// env's candidates at the first two accepted pairs (against the targets that do not move) at or
+// after P_i, one thread per (env, target).  (c) The first of them clear of the env's moved targets
+// (more, drawn in place, if both land on one): one thread per (env, target) for an env with one
+// covered target (its moved target's position is its first candidate there), one thread per env,
+// in target order, for an env with several.  (d) Where no listed env needs more tries than a
+// target's clean maximum, the clean chain is the chain; else it is rebuilt from the first such
+// target with the listed envs' maxima, one target at a time (P_j for the targets before it are
+// right: their maxima held).
+template <bool Q0>
+__global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
+                                                             WinArgs wa, int n_rows, unsigned long long* prof,
+                                                             ChanArgs ch) {
+    extern __shared__ __align__(16) unsigned char win_lds[];
+    __shared__ unsigned long long rng_s[3];
+    __shared__ int red_s[2][kWinWaves];  // (double-buffered: one barrier per step)
+    __shared__ int ps_s[VMAS_SPAWN_MAX_TARGETS + 1], mc_s[VMAS_SPAWN_MAX_TARGETS], lmax_s[VMAS_SPAWN_MAX_TARGETS];
+    __shared__ int bad_s, i0_s;
+    __shared__ unsigned long long stamp_s[8];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int T = io.n_targets, c4 = T * 8;  // (uint4 columns of a table row)
+    int32_t* const W = io.max_accepted;
+    const int MT = io.max_tries > 0 ? io.max_tries : VMAS_SPAWN_MAX_TRIES;
+    const int WP = wa.pairs;
+    const int cap = win_list_cap(T);
+    uint32_t* lmask = reinterpret_cast<uint32_t*>(win_lds);             // [cap][T][4]
+    float2* newpos = reinterpret_cast<float2*>(lmask + cap * T * 4);      // [cap][T]
+    float2* cand1 = newpos + cap * T;                                     // [cap][T]
+    float2* cand2 = cand1 + cap * T;                                      // [cap][T]
+    uint32_t* pp = reinterpret_cast<uint32_t*>(cand2 + cap * T);          // [cap][T] p1 | p2 << 16
+    uint32_t* linfo = pp + cap * T;                                       // [cap][2]
+    uint8_t* mclean = reinterpret_cast<uint8_t*>(linfo + cap * 2);        // [T][128]
+    const bool stamp = prof && threadIdx.x == 0;
+    if (stamp) stamp_s[0] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);
+    const int n_listed = W[kWinListWord];
+    const int n_list = n_listed < cap ? n_listed : cap;
+    if ((int)threadIdx.x < c4) {  // column c of the tables: max over every cluster's row, 16 loads in flight
+        const uint4* src = reinterpret_cast<const uint4*>(wa.crow) + threadIdx.x;
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        for (int r0 = 0; r0 < n_rows; r0 += 16) {
+            uint4 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = r0 + u < n_rows ? src[(long)(r0 + u) * c4] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                acc.x = bytes_max(acc.x, v[u].x);
+                acc.y = bytes_max(acc.y, v[u].y);
+                acc.z = bytes_max(acc.z, v[u].z);
+                acc.w = bytes_max(acc.w, v[u].w);
+            }
+        }
+        reinterpret_cast<uint4*>(mclean)[threadIdx.x] = acc;  // byte P of row i = max over groups of k(i, P)
+    }
+    {
+        // the listed envs: entry d = [env, covered, T masks], 4 loads in flight per thread
+        const int E = 2 + 4 * T;
+        for (int q0i = 0; q0i < n_list * E; q0i += 4 * kWinThreads) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0i + u * kWinThreads + (int)threadIdx.x;
+                v[u] = q < n_list * E ? wa.list[q] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0i + u * kWinThreads + (int)threadIdx.x;
+                if (q < n_list * E) {
+                    const int d = q / E, f = q - d * E;
+                    if (f < 2) linfo[d * 2 + f] = v[u];
+                    else lmask[d * T * 4 + (f - 2)] = v[u];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // (a) the clean chain
+        if (stamp) stamp_s[1] = __builtin_amdgcn_s_memrealtime();
+        int P = 0, bad = T;
+        for (int i = 0; i < T; ++i) {
+            const int M = P < kWinMaxPairs ? (int)mclean[i * kWinMaxPairs + P] : 255;
+            ps_s[i] = P;
+            mc_s[i] = M;
+            lmax_s[i] = 0;
+            if (M >= 255 || M >= MT) {
+                bad = i;
+                break;
+            }
+            P += M == 0 ? 1 : M + 2;
+        }
+        bad_s = bad;
+    }
+    __syncthreads();
+    const int bad = bad_s;
+    const unsigned long long seed = rng_s[0], off0 = rng_s[1];
+    // (b) the candidates of every (listed env, target after its first covered one or covered)
+    for (int it = (int)threadIdx.x; it < n_list * T; it += kWinThreads) {
+        const int d = it / T, i = it - d * T;
+        const uint32_t cov = linfo[d * 2 + 1];
+        const int j0 = __builtin_ctz(cov);
+        if (i >= bad || !(i > j0 || ((cov >> i) & 1u))) continue;
+        const uint4 m = *reinterpret_cast<const uint4*>(&lmask[(d * T + i) * 4]);
+        const int p1 = next_bit128(m.x, m.y, m.z, m.w, ps_s[i]);
+        const int p2 = i > j0 ? next_bit128(m.x, m.y, m.z, m.w, p1 + 1) : kWinMaxPairs;
+        const int db = (int)linfo[d * 2];
+        const float2 c1 = spawn_pair(io, g, Q0, seed, off0, p1 < WP ? p1 : 0, db);  // (both drawn: in flight together)
+        const float2 c2 = spawn_pair(io, g, Q0, seed, off0, p2 < WP ? p2 : 0, db);
+        cand1[d * T + i] = c1;
+        cand2[d * T + i] = c2;
+        pp[d * T + i] = (uint32_t)p1 | ((uint32_t)p2 << 16);
+        if (i == j0) newpos[d * T + i] = c1;  // (its first covered target: the first accepted try)
+    }
+    __syncthreads();
+    if (stamp) stamp_s[2] = __builtin_amdgcn_s_memrealtime();
+    // target i's first accepted try of listed env d at start pair P (255: none within the window or
+    // max_tries); covered: its new position.  pre: the precomputed candidates at P (else drawn).
+    auto walk = [&](int d, int i, int P, bool pre) -> int {
+        const uint4 m = *reinterpret_cast<const uint4*>(&lmask[(d * T + i) * 4]);
+        const uint32_t dcov = linfo[d * 2 + 1];
+        const uint32_t moved = dcov & ((1u << i) - 1u);
+        const bool cov_i = (dcov >> i) & 1u;
+        const uint32_t pw = pp[d * T + i];
+        int p = pre ? (int)(pw & 0xFFFFu) : next_bit128(m.x, m.y, m.z, m.w, P);
+        for (int n = 0; p < WP && p - P < MT; ++n) {
+            const float2 cnd = pre && n == 0   ? cand1[d * T + i]
+                               : pre && n == 1 ? cand2[d * T + i]
+                                               : spawn_pair_call<Q0>(io.x_lo, io.x_hi, io.y_lo, io.y_hi, io.mode,
+                                                                     g.step, g.inc, seed, off0, p, (int)linfo[d * 2]);
+            bool hit = false;
+            for (uint32_t mv = moved; mv; mv &= mv - 1u) {
+                const float2 q = newpos[d * T + __builtin_ctz(mv)];
+                hit = hit || near(q.x, q.y, cnd.x, cnd.y, d2_min);
+            }
+            if (!hit) {
+                if (cov_i) newpos[d * T + i] = cnd;
+                return p - P;
+            }
+            p = pre && n == 0 ? (int)(pw >> 16) : next_bit128(m.x, m.y, m.z, m.w, p + 1);
+        }
+        return 255;
+    };
+    // (c) one covered target: per (env, target after it), in parallel; several: per env, in order
+    for (int it = (int)threadIdx.x; it < n_list * T; it += kWinThreads) {
+        const int d = it / T, i = it - d * T;
+        const uint32_t cov = linfo[d * 2 + 1];
+        const int j0 = __builtin_ctz(cov);
+        if ((cov & (cov - 1u)) == 0u) {
+            if (i > j0 && i < bad) atomicMax(&lmax_s[i], walk(d, i, ps_s[i], true));
+        } else if (i == j0) {
+            for (int t = j0 + 1; t < bad; ++t) atomicMax(&lmax_s[t], walk(d, t, ps_s[t], true));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // (d) the first target whose maximum a listed env raises
+        int i0 = T;
+        for (int i = 0; i < bad; ++i)
+            if (lmax_s[i] > mc_s[i]) {
+                i0 = i;
+                break;
+            }
+        i0_s = i0;
+        if (stamp) stamp_s[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    const int i0 = i0_s;
+    const int d = (int)threadIdx.x;
+    const bool has = d < n_list;
+    const uint32_t dcov = has ? linfo[d * 2 + 1] : 0u;
+    const int j0 = has ? __builtin_ctz(dcov) : 32;  // the first covered target
+    bool unresolved = n_listed > cap || (i0 == T && bad < T);
+    if (!unresolved && i0 < T) {
+        // rebuild from target i0: its maximum with the listed envs' (computed at the right P), then
+        // one target at a time
+        int P = ps_s[i0];
+        int M = max(mc_s[i0], lmax_s[i0]);
+        if (M >= 255 || M >= MT) unresolved = true;
+        __syncthreads();  // (every thread has read mc_s[i0])
+        if (threadIdx.x == 0) mc_s[i0] = M;
+        for (int i = i0 + 1; i < T && !unresolved; ++i) {
+            P += M == 0 ? 1 : M + 2;
+            int kd = 0;
+            if (has && (i > j0 || ((dcov >> i) & 1u))) {
+                const int k = walk(d, i, P, false);
+                if (i > j0) kd = k;
+            }
+            const int wm = wave_max_nonneg(kd);
+            if (lane == 0) red_s[i & 1][wave] = wm;
+            __syncthreads();
+            M = P < kWinMaxPairs ? (int)mclean[i * kWinMaxPairs + P] : 255;
+#pragma unroll
+            for (int w = 0; w < kWinWaves; ++w) M = max(M, red_s[i & 1][w]);
+            if (M >= 255 || M >= MT) unresolved = true;
+            else if (threadIdx.x == 0) mc_s[i] = M;
+        }
+    }
+    if (!unresolved && has) {  // every covered target of a listed env to its new position
+        const int db = (int)linfo[d * 2];
+        for (int i = 0; i < T; ++i)
+            if ((dcov >> i) & 1u) {
+                float* p = io.pos[i] + (long)db * io.pos_s0[i];
+                p[0] = newpos[d * T + i].x;
+                p[io.pos_s1[i]] = newpos[d * T + i].y;
+            }
+    }
+    if (threadIdx.x == 0) {
+        if (!unresolved)
+            for (int i = 0; i < T; ++i) W[i] = mc_s[i];
+        W[T] = unresolved ? 1 : 0;
+    }
+    if (stamp) {
+        stamp_s[4] = __builtin_amdgcn_s_memrealtime();
+        stamp_s[5] = (unsigned long long)i0;
+        for (int k = 0; k < 6; ++k) prof[1 + k] = stamp_s[k];
+    }
+    if (ch.out) {  // (publish_channel reads the words with agent-scope loads: stored above by this group)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (wave == 0) publish_channel(ch, W, T, rng_s[2]);
+    }
+}
+
+size_t win_cands_lds_bytes(int A, int T) {
+    const size_t p1a = (size_t)(A + T) * 64 * 8 + (size_t)T * 64 * 16 + 64 * 4 + 3 * 8;
+    const size_t p1b = (size_t)64 * (T * 32 + 1) * 4;
+    return std::max(p1a, p1b);
+}
+
+size_t win_chain_lds_bytes(int T) {
+    const size_t cap = (size_t)win_list_cap(T);
+    return cap * (44 * T + 8) + (size_t)T * kWinMaxPairs;
+}
+
 // The smallest float x >= 0 with sqrtf(x) >= min_dist (binary search over the ordered bit patterns
 // of non-negative floats; sqrtf is correctly rounded on the host as on the device).
 float spawn_d2_min(float min_dist) {
@@ -747,6 +1284,13 @@ int32_t vmas_spawn_profile(uint64_t* out, int64_t n) {
     return (int32_t)k;
 }
 
+int64_t vmas_spawn_scratch_words(int32_t batch, int32_t n_targets) {
+    if (batch <= 0 || n_targets < 1 || n_targets > VMAS_SPAWN_MAX_TARGETS) return -1;
+    const int64_t groups = (batch + 63) / 64;
+    const int64_t clusters = (groups + kWinCluster - 1) / kWinCluster;
+    return (groups + clusters) * n_targets * 32 + (int64_t)win_list_cap(n_targets) * (2 + 4 * n_targets);
+}
+
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream) {
     if (!io || !increment || device < 0 || device >= 64 || io->batch <= 0 || io->n_agents < 0 || io->n_agents > 32 ||
         io->n_targets < 1 || io->n_targets > VMAS_SPAWN_MAX_TARGETS || !io->covered || !io->max_accepted ||
@@ -779,14 +1323,16 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     const float d2_min = spawn_d2_min(io->min_dist);
     hipStream_t st = (hipStream_t)stream;
     const int T = io->n_targets, n_groups = (int)((B + 63) / 64);
-    const bool group_resident = n_groups <= resident_static[device] && !getenv("VMAS_SPAWN_CLAIMED");
+    const char* kn = getenv("VMAS_SPAWN_KERNEL");
+    const bool group_resident = n_groups <= resident_static[device] && !getenv("VMAS_SPAWN_CLAIMED") &&
+                                !(kn && strcmp(kn, "claimed") == 0);
     const long long grid = std::min<long long>(n_groups, resident[device]);
     // VMAS_SPAWN_PROFILE=1 (a probe's knob): per item s_memrealtime stamps [claimed, wait over,
     // occupied loaded, tries done, completion added, workgroup] into g_spawn_prof (vmas_spawn_profile)
     unsigned long long* prof = nullptr;
     static const bool want_prof = getenv("VMAS_SPAWN_PROFILE") && getenv("VMAS_SPAWN_PROFILE")[0] == '1';
     if (want_prof) {
-        const size_t need = (size_t)T * n_groups * 6;
+        const size_t need = std::max<size_t>((size_t)T * n_groups * 6, 32 + (size_t)n_groups);  // (window: [0] cands start, [1, 9 + T) the chain's stamps, [30] group 0's pairs drawn, [32 + g] group g done)
         if (g_spawn_prof_n < need) {
             if (g_spawn_prof) (void)hipFree(g_spawn_prof);
             VMAS_AUX_HIP(hipMalloc((void**)&g_spawn_prof, need * sizeof(unsigned long long)));
@@ -799,6 +1345,57 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
         if (io->channel->device != device) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_targets: channel of another device");
         ch.in = io->channel->d_in;
         ch.out = io->channel->d_out;
+    }
+    // the kernel: the windowed one when the caller gave it its scratch (VMAS_SPAWN_KERNEL=resident /
+    // claimed selects the per-target hand-off kernels, an A/B knob)
+    const bool per_target = kn && (strcmp(kn, "resident") == 0 || strcmp(kn, "claimed") == 0);
+    const int64_t need = vmas_spawn_scratch_words(io->batch, T);
+    if (!per_target && io->scratch && need > 0 && io->scratch_words >= need &&
+        (n_groups + kWinCluster - 1) / kWinCluster <= 32 * 32) {  // (the cluster counts: the replica words)
+        const char* wv = getenv("VMAS_SPAWN_WINDOW");
+        const int pairs = wv ? atoi(wv) : kWinMaxPairs;
+        if (pairs != 16 && pairs != 64 && pairs != 96 && pairs != 128)
+            return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_targets: VMAS_SPAWN_WINDOW=%d (16, 64, 96 or 128)", pairs);
+        const int cap = win_list_cap(T);
+        const size_t lds1 = win_cands_lds_bytes(io->n_agents, T), lds2 = win_chain_lds_bytes(T);
+        const bool q0 = g.step >= B;
+        using CandsFn = void (*)(VmasSpawnTargetsIO, DrawGrid, float, WinArgs, unsigned long long*, ChanArgs);
+        CandsFn cands = nullptr;
+        switch (pairs * 2 + (q0 ? 1 : 0)) {
+            case 16 * 2 + 1: cands = k_spawn_cands<1, true>; break;
+            case 16 * 2: cands = k_spawn_cands<1, false>; break;
+            case 64 * 2 + 1: cands = k_spawn_cands<4, true>; break;
+            case 64 * 2: cands = k_spawn_cands<4, false>; break;
+            case 96 * 2 + 1: cands = k_spawn_cands<6, true>; break;
+            case 96 * 2: cands = k_spawn_cands<6, false>; break;
+            case 128 * 2 + 1: cands = k_spawn_cands<8, true>; break;
+            default: cands = k_spawn_cands<8, false>; break;
+        }
+        static bool attr[64] = {false};
+        if (!attr[device]) {  // (as k_step: > 64 KiB of dynamic LDS; HIP on gfx950 may refuse the attribute and
+                              // launch anyway -- the launch's own error check below is the one that counts)
+            (void)hipFuncSetAttribute((const void*)k_spawn_chain<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds2);
+            (void)hipFuncSetAttribute((const void*)k_spawn_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds2);
+            (void)hipGetLastError();
+            attr[device] = true;
+        }
+        const int n_clusters = (n_groups + kWinCluster - 1) / kWinCluster;
+        uint32_t* sw = reinterpret_cast<uint32_t*>(io->scratch);
+        WinArgs wa{sw, sw + (size_t)n_groups * T * 32, sw + (size_t)(n_groups + n_clusters) * T * 32, cap, pairs,
+                   q0 ? 1 : 0};
+        hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T), ch.in);
+        hipLaunchKernelGGL(cands, dim3((unsigned)n_groups), dim3(kWinThreads), lds1, st, *io, g, d2_min, wa, prof, ch);
+        if (q0)
+            hipLaunchKernelGGL(k_spawn_chain<true>, dim3(1), dim3(kWinThreads), lds2, st, *io, g, d2_min, wa, n_clusters,
+                               prof, ch);
+        else
+            hipLaunchKernelGGL(k_spawn_chain<false>, dim3(1), dim3(kWinThreads), lds2, st, *io, g, d2_min, wa,
+                               n_clusters, prof, ch);
+        VMAS_AUX_HIP(hipGetLastError());
+        *increment = g.inc;
+        return VMAS_OK;
     }
     hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T), ch.in);
     if (group_resident)

@@ -475,8 +475,16 @@ def spawn_max_tries() -> int:
     return int(os.environ.get("VMAS_SPAWN_TEST_MAX_TRIES", "0") or 0)
 
 
+def spawn_scratch(batch: int, n_targets: int, device) -> Tensor:
+    """Device words of the windowed spawn kernel (vmas_spawn_scratch_words)."""
+    n = int(N.load_library().vmas_spawn_scratch_words(batch, n_targets))
+    if n <= 0:
+        raise ValueError(f"vmas_spawn_scratch_words({batch}, {n_targets})")
+    return torch.empty(n, dtype=torch.int32, device=device)
+
+
 def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
-                  target_pos, mx: Tensor, channel=None, backup: Tensor = None):
+                  target_pos, mx: Tensor, channel=None, backup: Tensor = None, scratch: Tensor = None):
     """One vmas_spawn_targets launch on the current stream; returns (io, philox increment)."""
     import numpy as np
 
@@ -506,6 +514,8 @@ def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidi
     io.channel = channel
     io.max_tries = spawn_max_tries()
     io.backup = backup.data_ptr() if backup is not None else None
+    if scratch is not None:
+        io.scratch, io.scratch_words = scratch.data_ptr(), scratch.numel()
     inc = ctypes.c_uint64(0)
     N.check_aux(N.load_library().vmas_spawn_targets(idx, ctypes.byref(io), ctypes.byref(inc),
                                                       ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
@@ -562,6 +572,7 @@ class SpawnChannel:
         # capture's private pool was found overwritten after a later replay)
         self.mx = torch.zeros(N.spawn_words(n_targets), dtype=torch.int32, device=dev)
         self.backup = torch.empty((n_targets, batch, 2), dtype=torch.float32, device=dev)  # (see _respawn_redo)
+        self.scratch = spawn_scratch(batch, n_targets, dev)
         ch = ctypes.c_void_p()
         N.check_aux(N.load_library().vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
         self.ptr = ch
@@ -601,7 +612,7 @@ class DeferredRespawn:
         a = self.args
         self.mx = self.chan.mx
         _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch,
-                                    backup=self.chan.backup)
+                                    backup=self.chan.backup, scratch=self.chan.scratch)
 
     def arm(self):
         if self.chan.busy is not None:  # (an earlier replay never finished: drain it first)
@@ -658,7 +669,9 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     T = len(target_pos)
     mx = out if out is not None else torch.empty(N.spawn_words(T), dtype=torch.int32, device=dev)
     backup = torch.empty((T, agents_pos.shape[0], 2), dtype=torch.float32, device=dev)
-    io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx, backup=backup)
+    scratch = spawn_scratch(agents_pos.shape[0], T, dev)
+    io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx, backup=backup,
+                            scratch=scratch)
     h = mx[:N.VMAS_SPAWN_ERR_WORD + 1].tolist()  # the step's one host wait (maxima, unresolved, error)
     gen = torch.cuda.default_generators[idx]
     if h[N.VMAS_SPAWN_ERR_WORD] or h[T]:
