@@ -42,7 +42,8 @@ extern "C" {
 /* v3: VmasDiscoveryIO gained covered_count / all_time / done; increment spans (src NULL) in
  * vmas_copy_spans; VMAS_COPY_MAX_SPANS 160
  * v4: VmasSpawnTargetsIO max_tries / backup; vmas_uniform_columns_snap
- * v5: VmasSpawnTargetsIO scratch / scratch_words (the windowed respawn), vmas_spawn_scratch_words */
+ * v5: VmasSpawnTargetsIO scratch / scratch_words (the windowed respawn), vmas_spawn_scratch_words;
+ *     the fused programs' out_delta (direct outputs) and VMAS_COPY_STORE64 spans */
 #define VMAS_ABI_VERSION 5
 
 /* error codes */
@@ -501,6 +502,9 @@ typedef struct VmasBalanceIO {
     uint8_t* done;                       /* [B] torch.bool (DONE) */
     float* pos_rew_prev; /* [B] the previous pos_rew, zeroed in place (REWARD; the reference's
                             `pos_rew[:] = 0` before re-binding it); may be NULL */
+    const int64_t* out_delta;            /* optional (v5; graph mode's direct outputs): three device words,
+                                             the byte offsets added to the obs / rewards / done pointers
+                                             (simulator/environment/_graph.py DirectOutputs); NULL: none */
 } VmasBalanceIO;
 int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream);
 
@@ -539,6 +543,9 @@ typedef struct VmasFlockingIO {
     float* rewards[VMAS_FLOCK_MAX_AGENTS];       /* [B] fresh */
     float* obs[VMAS_FLOCK_MAX_AGENTS];           /* [B, 6 + n_rays] fresh (OBS) */
     float* lidar[VMAS_FLOCK_MAX_AGENTS];         /* [B, n_rays] fresh (OBS): Lidar._last_measurement */
+    const int64_t* out_delta;            /* optional (v5; graph mode's direct outputs): three device words,
+                                             the byte offsets added to the obs / rewards / done pointers
+                                             (simulator/environment/_graph.py DirectOutputs); NULL: none */
 } VmasFlockingIO;
 int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* stream);
 /* flocking's scripted target (flocking.py:81-87 action_script): u[b] = (cos(t[b] / period),
@@ -572,6 +579,9 @@ typedef struct VmasTransportIO {
     float* rew;                                               /* [B] fresh (REWARD) */
     float* obs[VMAS_TRANSPORT_MAX_AGENTS];                    /* [B, 4 + 7 n_packages] (OBS) */
     uint8_t* done;                                            /* [B] torch.bool (DONE) */
+    const int64_t* out_delta;            /* optional (v5; graph mode's direct outputs): three device words,
+                                             the byte offsets added to the obs / rewards / done pointers
+                                             (simulator/environment/_graph.py DirectOutputs); NULL: none */
 } VmasTransportIO;
 int32_t vmas_transport_outputs(int32_t device, const VmasTransportIO* io, void* stream);
 
@@ -626,6 +636,9 @@ typedef struct VmasDiscoveryIO {
     int64_t* covered_count;                       /* [B] fresh */
     const uint8_t* all_time;                      /* [B, T] torch.bool, contiguous */
     uint8_t* done;                                /* [B] torch.bool fresh */
+    const int64_t* out_delta;            /* optional (v5; graph mode's direct outputs): three device words,
+                                             the byte offsets added to the obs / rewards / done pointers
+                                             (simulator/environment/_graph.py DirectOutputs); NULL: none */
 } VmasDiscoveryIO;
 int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream);
 
@@ -635,7 +648,10 @@ int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* 
  * overlap one another's destinations; more than VMAS_COPY_MAX_SPANS spans take several launches.
  * A span with src == NULL is an increment, not a copy: 1.0f is added to each of the nbytes / 4
  * floats at dst (4-byte aligned) -- graph mode's `Environment.steps += 1` (ref environment.py:397),
- * folded into the post-replay launch instead of a kernel node of its own. */
+ * folded into the post-replay launch instead of a kernel node of its own.  A span with nbytes ==
+ * VMAS_COPY_STORE64 stores the 8-byte value (uint64_t)src at dst (8-byte aligned): graph mode's
+ * direct-output offsets for the next replay (the fused programs' out_delta words). */
+#define VMAS_COPY_STORE64 (-8)
 #define VMAS_COPY_MAX_SPANS 160 /* (spans travel as kernel arguments: 160 x 24 B < 4 KiB) */
 typedef struct VmasCopySpan {
     const void* src;

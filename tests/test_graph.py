@@ -65,6 +65,10 @@ CASES = [
 ]
 
 
+# fused scenarios whose outputs the replays write directly: categories (obs, rewards, done)
+DIRECT = {"balance": 3, "transport": 3, "flocking": 2, "discovery": 3}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps,expect", CASES, ids=[c[0] for c in CASES])
 def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, substeps, expect):
@@ -108,10 +112,13 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
         _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
         assert torch.equal(eager.steps, graph.steps), (name, t)  # (folded into the post-replay launch)
         if t == 4:
-            held = _flat(out_g, [])[0].clone(), _flat(out_g, [])[0]
-    # returned tensors are fresh copies: a later replay does not overwrite them
-    assert torch.equal(held[0], held[1])
+            held = [(x.clone(), x) for x in _flat(out_g, [])]
+    # returned tensors are fresh: a later replay does not overwrite them (copies, or -- the fused
+    # scenarios' obs / rewards / done -- tensors the replay wrote directly, DirectOutputs)
+    assert all(torch.equal(v, x) for v, x in held)
     assert graph.graph_status == expect, graph.graph_reason
+    if name in DIRECT and not hole:  # (every category of the fused launch written directly)
+        assert len(graph._graph._direct.enabled) == DIRECT[name], [r["dtype"] for r in graph._graph._direct.enabled]
     if expect == "graph":
         assert graph._graph.replays >= 5
         assert graph._graph._steps_folded  # no max_steps: steps += 1 left the graph

@@ -274,6 +274,7 @@ class VmasSpawnTargetsIO(ctypes.Structure):
 
 
 COPY_SPAN_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("nbytes", np.int64)])  # VmasCopySpan
+VMAS_COPY_STORE64 = -8  # (a span storing the 8-byte value src at dst)
 
 
 def stream_ptr(index: int) -> int:
@@ -342,6 +343,7 @@ class VmasBalanceIO(ctypes.Structure):
         ("on_the_ground", _vp),
         ("rewards", _vp * VMAS_SCN_MAX_AGENTS), ("obs", _vp * VMAS_SCN_MAX_AGENTS),
         ("done", _vp), ("pos_rew_prev", _vp),
+        ("out_delta", _vp),  # (graph mode's direct outputs: [obs, rewards, done] byte offsets)
     ]
 
 
@@ -369,6 +371,7 @@ class VmasFlockingIO(ctypes.Structure):
         ("t", _vp),
         ("shaping_in", _vp * _FA), ("shaping_out", _vp * _FA), ("dist_rew", _vp * _FA),
         ("collision_rew", _vp * _FA), ("rewards", _vp * _FA), ("obs", _vp * _FA), ("lidar", _vp * _FA),
+        ("out_delta", _vp),  # (graph mode's direct outputs: [obs, rewards, done] byte offsets)
     ]
 
 
@@ -386,6 +389,7 @@ class VmasTransportIO(ctypes.Structure):
         ("global_shaping", _vp * _TP), ("gs_s0", _i32 * _TP), ("global_shaping_out", _vp * _TP),
         ("dist_to_goal", _vp * _TP), ("on_goal", _vp * _TP), ("color", _vp * _TP), ("on_goal_in", _vp * _TP),
         ("rew", _vp), ("obs", _vp * _TA), ("done", _vp),
+        ("out_delta", _vp),  # (graph mode's direct outputs: [obs, rewards, done] byte offsets)
     ]
 
 
@@ -408,6 +412,7 @@ class VmasDiscoveryIO(ctypes.Structure):
         ("time_rew", _vp), ("shared", _vp), ("covering", _vp * _DA), ("collision", _vp * _DA),
         ("rewards", _vp * _DA),
         ("covered_count", _vp), ("all_time", _vp), ("done", _vp),
+        ("out_delta", _vp),  # (graph mode's direct outputs: [obs, rewards, done] byte offsets)
     ]
 
 

@@ -46,6 +46,10 @@ __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restr
 }
 
 __device__ __forceinline__ void copy_span(const VmasCopySpan& s, bool nt = false) {
+    if (s.nbytes == VMAS_COPY_STORE64) {  // a store span: the 8-byte value src at dst
+        if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint64_t*>(s.dst) = (uint64_t)(uintptr_t)s.src;
+        return;
+    }
     if (!s.src) {  // an increment span: dst[i] += 1.0f
         float* d = reinterpret_cast<float*>(s.dst);
         const int64_t n = s.nbytes / 4;
@@ -106,6 +110,12 @@ hipError_t vmas_aux::fill_u32_async(void* dst, uint32_t value, size_t n_words, h
     return hipGetLastError();
 }
 
+// a span the launch can run: a copy, an increment (src NULL: whole floats) or a store (STORE64)
+static bool span_ok(const VmasCopySpan& s) {
+    if (s.nbytes == VMAS_COPY_STORE64) return s.dst && ((uintptr_t)s.dst & 7) == 0;
+    return s.nbytes >= 0 && (s.nbytes == 0 || s.dst) && (s.src || (s.nbytes % 4 == 0 && ((uintptr_t)s.dst & 3) == 0));
+}
+
 extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, void* stream) {
     if (n < 0 || (n > 0 && !spans) || device < 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad arguments");
     VMAS_AUX_HIP(hipSetDevice(device));
@@ -117,12 +127,10 @@ extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, in
         int64_t most = 0;  // units of the largest span (16-byte units: sets the grid)
         for (int i = first; i < std::min(n, first + VMAS_COPY_MAX_SPANS); ++i) {
             const VmasCopySpan& s = spans[i];
-            if (s.nbytes < 0 || (s.nbytes > 0 && !s.dst) ||
-                (!s.src && (s.nbytes % 4 != 0 || ((uintptr_t)s.dst & 3) != 0)))
-                return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad span %d", i);
-            if (s.nbytes == 0 || s.src == s.dst) continue;
+            if (!span_ok(s)) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans: bad span %d", i);
+            if (s.nbytes == 0 || (s.nbytes > 0 && s.src == s.dst)) continue;
             a.s[a.n++] = s;
-            most = std::max<int64_t>(most, (s.nbytes + 15) / 16);
+            most = std::max<int64_t>(most, s.nbytes > 0 ? (s.nbytes + 15) / 16 : 1);
         }
         if (a.n == 0) continue;
         const int64_t per_block = (int64_t)kCopyThreads * kCopyUnroll;
@@ -156,11 +164,10 @@ extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* span
     int n = 0;
     for (int i = 0; i < n_spans; ++i) {
         const VmasCopySpan& sp = spans[i];
-        if (sp.nbytes < 0 || (sp.nbytes > 0 && !sp.dst) || (!sp.src && (sp.nbytes % 4 != 0 || ((uintptr_t)sp.dst & 3) != 0)))
-            return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: bad span %d", i);
-        if (sp.nbytes == 0 || sp.src == sp.dst) continue;
+        if (!span_ok(sp)) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: bad span %d", i);
+        if (sp.nbytes == 0 || (sp.nbytes > 0 && sp.src == sp.dst)) continue;
         a.s[n++] = sp;
-        most = std::max<int64_t>(most, (sp.nbytes + 15) / 16);
+        most = std::max<int64_t>(most, sp.nbytes > 0 ? (sp.nbytes + 15) / 16 : 1);
     }
     for (int i = 0; i < n_cols; ++i) {
         if (!cols[i].out) return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: null column %d", i);

@@ -7,6 +7,10 @@
 //     split into its n tensors, the address of every member written into the post-replay copy
 //     table (VmasCopySpan rows, simulator/environment/_graph.py _post_table), then ONE
 //     vmas_copy_spans launch for the outputs, the carried state and the backups.
+//     Direct outputs (simulator/environment/_graph.py DirectOutputs): categories a fused program
+//     wrote straight into this step's fresh buffer are handed out as views of it, and the next
+//     step's buffer is allocated here, its offset from the captured buffer going out in the same
+//     launch (a VMAS_COPY_STORE64 row).
 //   * UniformDraw: Environment.get_random_actions for continuous actions on a GPU (environment.py:
 //     524-606): one [A, B, n] allocation split per agent, the column table's output addresses, one
 //     vmas_uniform_columns launch at the device generator's (seed, offset) and the offset advanced
@@ -55,14 +59,47 @@ struct Group {
     int64_t member_bytes = 0;
 };
 
+// One directly written category: the captured buffer's address, the buffer the next replay writes
+// (box[0], a Python list shared with the graph: a rebuilt table's OutputAlloc takes over where this
+// one left off) and the one after it (pending, allocated by alloc(), current after the launch:
+// commit()), its members as (sizes, strides, element offset) of the category's dtype, its row.
+struct Region {
+    at::ScalarType dtype;
+    int64_t nbytes = 0, row = 0;
+    uintptr_t base = 0;
+    std::vector<std::vector<int64_t>> sizes, strides;
+    std::vector<int64_t> offsets;
+    py::list box;
+    at::Tensor pending;
+};
+
 class OutputAlloc {
 public:
     // groups: [(sample tensor of the group's dtype, shape tuple, n, r0, [member index per row])]
     // table: the copy table (numpy, VmasCopySpan rows), kept alive here
+    // regions: [(captured buffer, [buffer the next replay writes], sample tensor of the dtype, row,
+    //            [(sizes, strides, element offset) per member])]
     OutputAlloc(int device, py::list groups, py::object table, int64_t table_addr, int64_t copy_fn,
-                int64_t last_error_fn)
+                int64_t last_error_fn, py::list regions)
         : device_(device), table_(std::move(table)), tbl_((VmasCopySpan*)table_addr),
           copy_((CopySpansFn)copy_fn), last_error_((LastErrorFn)last_error_fn) {
+        for (py::handle h : regions) {
+            py::tuple t = h.cast<py::tuple>();
+            Region r;
+            at::Tensor buf = t[0].cast<at::Tensor>();
+            r.base = (uintptr_t)buf.data_ptr();
+            r.nbytes = buf.numel();
+            r.box = t[1].cast<py::list>();
+            r.dtype = t[2].cast<at::Tensor>().scalar_type();
+            r.row = t[3].cast<int64_t>();
+            for (py::handle m : t[4].cast<py::list>()) {
+                py::tuple mt = m.cast<py::tuple>();
+                r.sizes.push_back(mt[0].cast<std::vector<int64_t>>());
+                r.strides.push_back(mt[1].cast<std::vector<int64_t>>());
+                r.offsets.push_back(mt[2].cast<int64_t>());
+            }
+            regions_.push_back(std::move(r));
+        }
         for (py::handle g : groups) {
             py::tuple t = g.cast<py::tuple>();
             Group gr;
@@ -82,7 +119,8 @@ public:
     }
 
     // Fresh tensors of every group (in group order, members in order), their addresses written
-    // into the table's output rows.
+    // into the table's output rows; then the direct categories' members (views of the buffer the
+    // replay wrote), the next buffers allocated and their offsets written into the store rows.
     std::vector<at::Tensor> alloc() {
         std::vector<at::Tensor> out;
         out.reserve(count());
@@ -93,7 +131,23 @@ public:
                 tbl_[g.r0 + (int64_t)r].dst = (void*)(base + (uintptr_t)(g.row_members[r] * g.member_bytes));
             for (int64_t k = 0; k < g.n; ++k) out.push_back(buf.select(0, k));
         }
+        for (Region& r : regions_) {
+            at::Tensor typed = r.box[0].cast<at::Tensor>().view(r.dtype);
+            for (size_t m = 0; m < r.offsets.size(); ++m)
+                out.push_back(typed.as_strided(r.sizes[m], r.strides[m], r.offsets[m]));
+            r.pending = at::empty({r.nbytes}, opts_.dtype(at::kByte));
+            tbl_[r.row].src = (const void*)((uintptr_t)r.pending.data_ptr() - r.base);
+        }
         return out;
+    }
+
+    // after the launch that stored the pending buffers' offsets: they are what the next replay writes
+    void commit() {
+        for (Region& r : regions_)
+            if (r.pending.defined()) {
+                r.box[0] = py::cast(r.pending);
+                r.pending = at::Tensor();
+            }
     }
 
     // One vmas_copy_spans launch of table rows [lo, hi) on the current stream.
@@ -113,12 +167,14 @@ public:
         } else {
             launch(0, hi);
         }
+        commit();
         return out;
     }
 
     int64_t count() const {
         int64_t n = 0;
         for (const Group& g : groups_) n += g.n;
+        for (const Region& r : regions_) n += (int64_t)r.offsets.size();
         return n;
     }
 
@@ -132,6 +188,7 @@ private:
     CopySpansFn copy_;
     LastErrorFn last_error_;
     std::vector<Group> groups_;
+    std::vector<Region> regions_;
     at::TensorOptions opts_;
 };
 
@@ -240,6 +297,7 @@ py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, in
                                                        d.cols(), (int32_t)d.n_cols(), seed, off, d.mode(), delta, &inc,
                                                        current_stream(d.device()));
     if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
+    oa.commit();
     return py::make_tuple(outs, acts, snap, seed, off, inc);
 }
 
@@ -256,8 +314,9 @@ PYBIND11_MODULE(_vmas_host, m) {
     m.doc() = "Host path of a graph-mode step in C++ (csrc/vmas_host.cpp)";
     m.attr("ABI_VERSION") = VMAS_ABI_VERSION;
     py::class_<OutputAlloc>(m, "OutputAlloc")
-        .def(py::init<int, py::list, py::object, int64_t, int64_t, int64_t>())
+        .def(py::init<int, py::list, py::object, int64_t, int64_t, int64_t, py::list>())
         .def("alloc", &OutputAlloc::alloc)
+        .def("commit", &OutputAlloc::commit)
         .def("launch", &OutputAlloc::launch)
         .def("post", &OutputAlloc::post)
         .def("count", &OutputAlloc::count);

@@ -38,6 +38,27 @@ __device__ __forceinline__ float torch_remainder(float a, float b) {
     return mod;
 }
 
+// Graph mode's direct outputs (simulator/environment/_graph.py DirectOutputs): the byte offsets from
+// the captured step's obs / rewards / done buffers to this replay's fresh output tensors, written by
+// the previous post-replay launch; out_delta NULL (every eager launch): in place.
+struct OutDelta {
+    long long obs, rew, done;
+};
+template <class IO>
+__device__ __forceinline__ OutDelta load_out_delta(IO& io) {
+    OutDelta o{0, 0, 0};
+    if (io.out_delta) {
+        o.obs = io.out_delta[0];
+        o.rew = io.out_delta[1];
+        o.done = io.out_delta[2];
+    }
+    return o;
+}
+template <class T>
+__device__ __forceinline__ T* moved(T* p, long long d) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + d);
+}
+
 // balance.py:205-262 (restated in scenarios/balance.py): reward of the first agent (on-the-ground
 // test, package-goal distance, ground / position rewards and the global shaping update), every
 // agent's reward (ground_rew + pos_rew), every agent's 16-entry observation, and done
@@ -54,11 +75,12 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
     const int b = blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
+    const OutDelta od = load_out_delta(io);
     if (blockIdx.y == 0) {
         if (!(io.what & VMAS_SCN_REWARD)) {
             if (wave != 0 || !valid || !(io.what & VMAS_SCN_DONE)) return;
             const bool og = io.on_the_ground[b] != 0;
-            io.done[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
+            moved(io.done, od.done)[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
             return;
         }
         {  // side `wave` of closest_line_box(floor, line) (get_distance's box-line branch)
@@ -100,9 +122,9 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
         if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
         io.pos_rew[b] = pos_rew;
         const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
-        for (int i = 0; i < io.n_agents; ++i) io.rewards[i][b] = r;
+        for (int i = 0; i < io.n_agents; ++i) moved(io.rewards[i], od.rew)[b] = r;
         if (io.what & VMAS_SCN_DONE)  // done = on_the_ground + is_overlapping(package, goal)
-            io.done[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
+            moved(io.done, od.done)[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
         return;
     }
     // agent i's observation
@@ -115,7 +137,7 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
     const V2 pg = pkg - goal;
     const V2 p = ld_vec2(io.agent_pos[i], b), v = ld_vec2(io.agent_vel[i], b);
     const V2 dp = p - pkg, dl = p - lpos;
-    float4* dst = reinterpret_cast<float4*>(io.obs[i] + (long)b * 16);
+    float4* dst = reinterpret_cast<float4*>(moved(io.obs[i], od.obs) + (long)b * 16);
     dst[0] = make_float4(p.x, p.y, v.x, v.y);
     dst[1] = make_float4(dp.x, dp.y, dl.x, dl.y);
     dst[2] = make_float4(pg.x, pg.y, pv.x, pv.y);
@@ -141,7 +163,7 @@ struct FlockHead {
 // IO: the argument block by value, or (k_flocking_fast) read in place through the kernel
 // argument segment pointer -- structs copied out before use, see k_flocking_fast.
 template <class IO>
-__device__ __forceinline__ FlockHead flock_part0(IO& io, int b, int p, bool ret = false) {
+__device__ __forceinline__ FlockHead flock_part0(IO& io, int b, int p, const OutDelta& od, bool ret = false) {
     FlockHead h{};
     constexpr int MA = VMAS_FLOCK_MAX_AGENTS;
     const int k = io.policy[p], na = io.n_all;
@@ -201,7 +223,7 @@ __device__ __forceinline__ FlockHead flock_part0(IO& io, int b, int p, bool ret 
         const float dr = io.shaping_in[p][b] - shaping;
         io.shaping_out[p][b] = shaping;
         io.dist_rew[p][b] = dr;
-        io.rewards[p][b] = cr + dr;
+        moved(io.rewards[p], od.rew)[b] = cr + dr;
     }
     if (io.what & VMAS_SCN_OBS) {
         const VmasVec vp = io.vel[p];
@@ -212,7 +234,7 @@ __device__ __forceinline__ FlockHead flock_part0(IO& io, int b, int p, bool ret 
             if (j == io.target) tp = P[j];
         h = FlockHead{{pk.x, pk.y, v.x, v.y, pk.x - tp.x, pk.y - tp.y}};
         if (!ret) {
-            float* o = io.obs[p] + (long)b * W;
+            float* o = moved(io.obs[p], od.obs) + (long)b * W;
 #pragma unroll
             for (int i = 0; i < 6; ++i) o[i] = h.v[i];
         }
@@ -232,8 +254,9 @@ __global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
     if (b >= io.batch) return;
     const int parts = (io.what & VMAS_SCN_OBS) ? 1 + io.n_rays : 1;
     const int p = blockIdx.y / parts, part = blockIdx.y - p * parts, k = io.policy[p];
+    const OutDelta od = load_out_delta(io);
     if (part == 0) {
-        flock_part0(io, b, p);
+        flock_part0(io, b, p, od);
         return;
     }
     // LIDAR ray r: Lidar.measure = World.cast_rays(angles + agent rot) (cast_one)
@@ -253,7 +276,7 @@ __global__ void __launch_bounds__(64) k_flocking(VmasFlockingIO io) {
     for (int t = 0; t < MT; ++t)  // (sphere targets: checked by the host entry point)
         if (t < nt) best = tmin(best, ray_sphere(pk, dc, ds, T[t], io.ray_targets[t].radius, io.max_range));
     io.lidar[p][(long)b * io.n_rays + r] = best;
-    io.obs[p][(long)b * W + 6 + r] = best;
+    moved(io.obs[p], od.obs)[(long)b * W + 6 + r] = best;
 }
 
 // The same program with the fast LIDAR (io.fast_lidar, the default): the ray-sphere distance in
@@ -297,6 +320,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
     const int nr = NR > 0 ? NR : io.n_rays, nt = NT > 0 ? NT : io.n_ray_targets, W = 6 + nr;
     const int bb = valid ? b : io.batch - 1;
     const int row = lane * W;
+    const OutDelta od = load_out_delta(io);
     if (io.what & VMAS_SCN_OBS) {
         // loads first (independent): angles, rotation, position, targets
         const float* ang = io.angles[p] + (long)bb * io.ang_s0[p];
@@ -319,7 +343,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
             R2[t] = t < nt ? rad * rad : 0.f;
         }
         if (valid) {
-            const FlockHead h = flock_part0(io, b, p, true);
+            const FlockHead h = flock_part0(io, b, p, od, true);
 #pragma unroll
             for (int i = 0; i < 6; ++i) S[w][row + i] = h.v[i];
         }
@@ -374,7 +398,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
         }
         // the wave's rows out as contiguous blocks: obs [64 x W], the LIDAR [64 x nr]
         const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
-        float* obs = io.obs[p] + (long)g0 * W;
+        float* obs = moved(io.obs[p], od.obs) + (long)g0 * W;
         for (int i = lane; i < nv * W; i += 64) obs[i] = S[w][i];
         float* lid = io.lidar[p] + (long)g0 * nr;
         for (int i = lane; i < nv * nr; i += 64) {
@@ -382,7 +406,7 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
             lid[i] = S[w][e * W + 6 + (i - e * nr)];
         }
     } else if (valid) {
-        flock_part0(io, b, p);
+        flock_part0(io, b, p, od);
     }
 }
 
@@ -404,6 +428,7 @@ __global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= io.batch) return;
     const int part = blockIdx.y, np = io.n_packages;
+    const OutDelta od = load_out_delta(io);
     if (part == 0) {
         bool all_on = true;
         if (io.what & VMAS_SCN_REWARD) {
@@ -424,18 +449,18 @@ __global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
                 io.global_shaping_out[i][b] = shaping;
                 all_on = all_on && on;
             }
-            io.rew[b] = rew;
+            moved(io.rew, od.rew)[b] = rew;
         } else if (io.what & VMAS_SCN_DONE) {
 #pragma unroll
             for (int i = 0; i < MP; ++i)
                 if (i < np) all_on = all_on && io.on_goal_in[i][b] != 0;
         }
-        if (io.what & VMAS_SCN_DONE) io.done[b] = all_on ? 1 : 0;  // all(stack(on_goal), -1)
+        if (io.what & VMAS_SCN_DONE) moved(io.done, od.done)[b] = all_on ? 1 : 0;  // all(stack(on_goal), -1)
         return;
     }
     const int a = part - 1;
     const V2 p = ld_vec2(io.agent_pos[a], b), v = ld_vec2(io.agent_vel[a], b);
-    float* o = io.obs[a] + (long)b * (4 + 7 * np);
+    float* o = moved(io.obs[a], od.obs) + (long)b * (4 + 7 * np);
     o[0] = p.x;
     o[1] = p.y;
     o[2] = v.x;
@@ -465,7 +490,7 @@ __device__ __forceinline__ void disc_reductions(IO& io, int b, int T, int n_cov)
     if (io.done) {
         bool all = true;
         for (int j = 0; j < T; ++j) all = all && io.all_time[(long)b * T + j] != 0;
-        io.done[b] = all ? 1 : 0;
+        moved(io.done, load_out_delta(io).done)[b] = all ? 1 : 0;
     }
 }
 
@@ -543,7 +568,7 @@ __global__ void __launch_bounds__(64) k_discovery_reward(VmasDiscoveryIO io) {
         if (i >= A) continue;
         io.collision[i][b] = 0.f;  // collision_rew[:] = 0 (penalty 0: nothing added)
         const float cv = io.shared_reward ? shared : covr[i];
-        io.rewards[i][b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
+        moved(io.rewards[i], load_out_delta(io).rew)[b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
     }
 }
 
@@ -557,7 +582,7 @@ __global__ void __launch_bounds__(64) k_discovery_obs(VmasDiscoveryIO io) {
     const int parts = 1 + rays, a = blockIdx.y / parts, part = blockIdx.y - a * parts;
     const int self = io.agent_entity[a], W = 4 + rays;
     const V2 p = ld_vec2(io.pos[self], b);
-    float* o = io.obs[a] + (long)b * W;
+    float* o = moved(io.obs[a], load_out_delta(io).obs) + (long)b * W;
     if (part == 0) {
         const V2 v = ld_vec2(io.vel[a], b);
         o[0] = p.x;
@@ -666,7 +691,7 @@ __global__ void __launch_bounds__(1024) k_discovery_reward_fast(VmasDiscoveryIO 
     __syncthreads();
     if (valid) {
         const float cv = io.shared_reward ? SH[lane] : covr;
-        io.rewards[i][b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
+        moved(io.rewards[i], load_out_delta(io).rew)[b] = (0.f + cv) + io.time_penalty;  // collision_rew + covering_rew + time_rew
     }
     // the stacks and the distances as contiguous blocks of the workgroup's envs
     const int tid = (int)threadIdx.x, nth = (int)blockDim.x;
@@ -783,7 +808,7 @@ __global__ void __launch_bounds__(256) k_discovery_obs_fast(VmasDiscoveryIO io_a
         }
         col += nr;
     }
-    float* obs = io.obs[a] + (long)g0 * W;
+    float* obs = moved(io.obs[a], load_out_delta(io).obs) + (long)g0 * W;
     for (int k = lane; k < nv * W; k += 64) obs[k] = S[w][k];
 }
 

@@ -184,6 +184,11 @@ class Scenario(BaseScenario):
         io.line = _fused.ref(w, self.line, keep, 0)
         io.floor = _fused.ref(w, self.floor, keep, 0)
         out = {}
+        # (graph-mode capture: obs / rewards / done written straight into each replay's fresh tensors)
+        io.out_delta, direct = _fused.direct_outputs(w, (
+            (torch.float32, (B, 16), A) if what & N.VMAS_SCN_OBS else None,
+            (torch.float32, (B,), A) if what & N.VMAS_SCN_REWARD else None,
+            (torch.bool, (B,), 1) if what & N.VMAS_SCN_DONE else None))
         if what & N.VMAS_SCN_REWARD:
             gs = _fused.f32(self.global_shaping, dev)
             keep.append(gs)
@@ -198,7 +203,7 @@ class Scenario(BaseScenario):
             io.ground_rew = self.ground_rew.data_ptr()
             prev = self.pos_rew
             io.pos_rew_prev = prev.data_ptr() if prev.numel() else None
-            out["rewards"] = [torch.empty(B, device=dev, dtype=torch.float32) for _ in range(A)]
+            out["rewards"] = direct[1] or [torch.empty(B, device=dev, dtype=torch.float32) for _ in range(A)]
             for i, r in enumerate(out["rewards"]):
                 io.rewards[i] = r.data_ptr()
         if what & N.VMAS_SCN_OBS:
@@ -208,7 +213,7 @@ class Scenario(BaseScenario):
             for i, a in enumerate(w.agents):
                 io.agent_pos[i] = _fused.vec(_fused.f32(a.state.pos, dev), keep)
                 io.agent_vel[i] = _fused.vec(_fused.f32(a.state.vel, dev), keep)
-            out["obs"] = [torch.empty(B, 16, device=dev, dtype=torch.float32) for _ in range(A)]
+            out["obs"] = direct[0] or [torch.empty(B, 16, device=dev, dtype=torch.float32) for _ in range(A)]
             for i, o in enumerate(out["obs"]):
                 io.obs[i] = o.data_ptr()
         if what & N.VMAS_SCN_DONE:
@@ -217,7 +222,7 @@ class Scenario(BaseScenario):
                 og = og.to(device=dev, dtype=torch.bool).contiguous()
             keep.append(og)
             io.on_the_ground = og.data_ptr()
-            out["done"] = torch.empty(B, device=dev, dtype=torch.bool)
+            out["done"] = direct[2][0] if direct[2] else torch.empty(B, device=dev, dtype=torch.bool)
             io.done = out["done"].data_ptr()
         _fused.check(_fused.lib().vmas_balance_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
                      "vmas_balance_outputs")

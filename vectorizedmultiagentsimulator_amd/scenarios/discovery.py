@@ -284,12 +284,17 @@ class Scenario(BaseScenario):
             io, dev = self._fused_io(N.VMAS_SCN_REWARD, keep)
             B, A, T = w.batch_dim, len(w.agents), len(self._targets)
             int_time = bool(io.time_int)
+            at = self.all_time_covered_targets
+            fuse_done = (at.dtype is torch.bool and at.is_contiguous() and at.shape == (B, T) and at.device == dev)
+            # (graph-mode capture: rewards / done written straight into each replay's fresh tensors)
+            io.out_delta, direct = _fused.direct_outputs(w, (
+                None, (torch.float32, (B,), A), (torch.bool, (B,), 1) if fuse_done else None))
             out = {
                 "agents_pos": torch.empty(B, A, 2, device=dev), "targets_pos": torch.empty(B, T, 2, device=dev),
                 "dists": torch.empty(B, A, T, device=dev), "per_target": torch.empty(B, T, device=dev, dtype=torch.int64),
                 "covered": torch.empty(B, T, device=dev, dtype=torch.bool),
                 "time_rew": torch.empty(B, device=dev, dtype=torch.int64 if int_time else torch.float32),
-                "rewards": [torch.empty(B, device=dev) for _ in w.agents],
+                "rewards": direct[1] or [torch.empty(B, device=dev) for _ in w.agents],
             }
             for k in ("agents_pos", "targets_pos", "dists", "per_target", "covered", "time_rew"):
                 setattr(io, k, out[k].data_ptr())
@@ -298,10 +303,8 @@ class Scenario(BaseScenario):
             # inputs are the same tensors at the same versions)
             out["count"] = torch.empty(B, device=dev, dtype=torch.int64)
             io.covered_count = out["count"].data_ptr()
-            at = self.all_time_covered_targets
-            fuse_done = (at.dtype is torch.bool and at.is_contiguous() and at.shape == (B, T) and at.device == dev)
             if fuse_done:
-                out["done"] = torch.empty(B, device=dev, dtype=torch.bool)
+                out["done"] = direct[2][0] if direct[2] else torch.empty(B, device=dev, dtype=torch.bool)
                 io.all_time, io.done = at.data_ptr(), out["done"].data_ptr()
             inplace = [self.shared_covering_rew] + [a.covering_reward for a in w.agents] + [a.collision_rew for a in w.agents]
             if any(t.dtype is not torch.float32 or not t.is_contiguous() or t.shape != (B,) or t.device != dev
@@ -362,7 +365,8 @@ class Scenario(BaseScenario):
             plan = self._fused_plan()
             B = w.batch_dim
             W = 4 + sum(plan["n_rays"])
-            obs = [torch.empty(B, W, device=dev) for _ in w.agents]
+            io.out_delta, direct = _fused.direct_outputs(w, ((torch.float32, (B, W), len(w.agents)), None, None))
+            obs = direct[0] or [torch.empty(B, W, device=dev) for _ in w.agents]
             lid = [[torch.empty(B, R, device=dev) for _ in w.agents] for R in plan["n_rays"]]
             for s, (m, R) in enumerate(zip(plan["masks"], plan["n_rays"])):
                 io.n_rays[s], io.mask[s] = R, m

@@ -225,6 +225,10 @@ class Scenario(BaseScenario):
         for i, e in enumerate(plan["targets"]):
             io.ray_targets[i] = _fused.ray_target(w, e, keep, dev)
         out = {}
+        # (graph-mode capture: obs / rewards written straight into each replay's fresh tensors)
+        io.out_delta, direct = _fused.direct_outputs(w, (
+            (torch.float32, (B, 6 + plan["R"]), len(pol)) if what & N.VMAS_SCN_OBS else None,
+            (torch.float32, (B,), len(pol)) if what & N.VMAS_SCN_REWARD else None, None))
         if what & N.VMAS_SCN_REWARD:
             t = self.t
             if t.dtype is not torch.float32 or not t.is_contiguous() or t.device != dev:
@@ -232,9 +236,11 @@ class Scenario(BaseScenario):
             io.t = t.data_ptr()
             for k in ("shaping", "dist_rew", "rewards"):
                 out[k] = [torch.empty(B, device=dev, dtype=torch.float32) for _ in pol]
+            if direct[1]:
+                out["rewards"] = direct[1]
         if what & N.VMAS_SCN_OBS:
             R = plan["R"]
-            out["obs"] = [torch.empty(B, 6 + R, device=dev, dtype=torch.float32) for _ in pol]
+            out["obs"] = direct[0] or [torch.empty(B, 6 + R, device=dev, dtype=torch.float32) for _ in pol]
             out["lidar"] = [torch.empty(B, R, device=dev, dtype=torch.float32) for _ in pol]
         for p, a in enumerate(pol):
             io.policy[p] = plan["policy"][p]

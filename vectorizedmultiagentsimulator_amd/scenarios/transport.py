@@ -141,6 +141,11 @@ class Scenario(BaseScenario):
         for k in range(3):
             io.red[k], io.green[k] = Color.RED.value[k], Color.GREEN.value[k]
         out = {"dist": [], "on_goal": [], "color": [], "gs": []}
+        # (graph-mode capture: obs / rew / done written straight into each replay's fresh tensors)
+        io.out_delta, direct = _fused.direct_outputs(w, (
+            (torch.float32, (B, 4 + 7 * len(self.packages)), len(w.agents)) if what & N.VMAS_SCN_OBS else None,
+            (torch.float32, (B,), 1) if what & N.VMAS_SCN_REWARD else None,
+            (torch.bool, (B,), 1) if what & N.VMAS_SCN_DONE else None))
         for i, p in enumerate(self.packages):
             io.package[i] = _fused.ref(w, p, keep, 0)
             io.goal[i] = _fused.ref(w, p.goal, keep, 0)
@@ -163,17 +168,17 @@ class Scenario(BaseScenario):
                 keep.append(og)
                 io.on_goal_in[i] = og.data_ptr()
         if what & N.VMAS_SCN_REWARD:
-            out["rew"] = torch.empty(B, device=dev, dtype=torch.float32)
+            out["rew"] = direct[1][0] if direct[1] else torch.empty(B, device=dev, dtype=torch.float32)
             io.rew = out["rew"].data_ptr()
         if what & N.VMAS_SCN_OBS:
             W = 4 + 7 * len(self.packages)
-            out["obs"] = [torch.empty(B, W, device=dev, dtype=torch.float32) for _ in w.agents]
+            out["obs"] = direct[0] or [torch.empty(B, W, device=dev, dtype=torch.float32) for _ in w.agents]
             for i, a in enumerate(w.agents):
                 io.agent_pos[i] = _fused.vec(_fused.f32(a.state.pos, dev), keep)
                 io.agent_vel[i] = _fused.vec(_fused.f32(a.state.vel, dev), keep)
                 io.obs[i] = out["obs"][i].data_ptr()
         if what & N.VMAS_SCN_DONE:
-            out["done"] = torch.empty(B, device=dev, dtype=torch.bool)
+            out["done"] = direct[2][0] if direct[2] else torch.empty(B, device=dev, dtype=torch.bool)
             io.done = out["done"].data_ptr()
         _fused.check(_fused.lib().vmas_transport_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
                      "vmas_transport_outputs")

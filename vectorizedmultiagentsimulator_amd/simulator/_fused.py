@@ -153,6 +153,18 @@ def ray_target(world, e, keep: list, dev) -> "N.VmasRayTarget":
     return r
 
 
+def direct_outputs(world, specs):
+    """The step outputs of one fused launch during a graph-mode capture (StepGraph's
+    DirectOutputs): ``specs`` per category (obs, rewards, done) None or (dtype, member shape, n
+    members).  Returns (the launch's out_delta address, per category its n member tensors -- views
+    of one buffer whose replays the graph relocates to fresh tensors -- or None).  Outside a
+    capture (None, [None, None, None]): the scenario allocates its outputs as before."""
+    d = getattr(world, "_direct_out", None)
+    if d is None:
+        return None, [None, None, None]
+    return d.launch(specs)
+
+
 def check(rc: int, what: str) -> None:
     N.check_aux(rc, what)
 

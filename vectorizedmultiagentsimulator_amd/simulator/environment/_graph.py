@@ -352,6 +352,79 @@ class _Segments:
 _STATE_KEYS = ("_pos", "_vel", "_rot", "_ang_vel", "_force", "_torque")
 
 
+class DirectOutputs:
+    """Fused programs writing a replay's outputs straight into fresh tensors: no
+    copy of the step's observations / rewards / done after the replay.
+
+    During the capture a fused scenario launch asks for its outputs here (_fused.direct_outputs):
+    per category (obs, rewards, done) one buffer in the graph's pool, split into the members it
+    returns, and three device words its kernel adds to those pointers (out_delta).  After the
+    capture a category is relocated only when the step returns each of its members as is and
+    nothing modified them in place (version counters) -- an op of the captured step that reads a
+    member to build another output would read the captured buffer, which no replay writes any
+    more -- and the scenario is one of this package's own classes (whose steps read their
+    outputs nowhere else).  Each replay then writes into a fresh buffer allocated one step ahead
+    (its offset from the captured buffer stored into the category's word by the previous
+    post-replay launch, a VMAS_COPY_STORE64 span); the step hands out views of it, and the
+    caching allocator recycles it once the caller drops them, as the reference's fresh tensors.
+    Categories left out keep their words at 0: the kernel writes the captured buffer, and the
+    post-replay launch copies it out as before."""
+
+    MAX_LAUNCHES = 16
+
+    def __init__(self, dev):
+        self.dev = torch.device(dev)
+        # (allocated outside the capture: the post-replay launches write them)
+        self.words = torch.zeros(3 * self.MAX_LAUNCHES, dtype=torch.int64, device=self.dev)
+        self.regions: List[dict] = []
+        self.launches = 0
+        self.enabled: List[dict] = []
+
+    def launch(self, specs):
+        k = self.launches
+        if k >= self.MAX_LAUNCHES:
+            return None, [None, None, None]
+        self.launches += 1
+        out = []
+        for c, spec in enumerate(specs):
+            if spec is None:
+                out.append(None)
+                continue
+            dt, shape, n = spec
+            numel = n * int(np.prod(shape, dtype=np.int64))
+            buf = torch.empty(numel * torch.empty((), dtype=dt).element_size(), dtype=torch.uint8, device=self.dev)
+            members = list(buf.view(dt).view(n, *shape).unbind(0))
+            self.regions.append({"buf": buf, "dtype": dt, "members": members,
+                                 "word": self.words.data_ptr() + 8 * (3 * k + c)})
+            out.append(members)
+        return self.words.data_ptr() + 24 * k, out
+
+    def finalize(self, out_tensors, scenario) -> None:
+        """Which categories the replays relocate (see the class notes)."""
+        # (make_env loads scenario modules afresh, without a package name: by source file)
+        scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                               "scenarios") + os.sep
+        cls = type(scenario)
+        own = (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
+               and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir))
+        ids = {id(t) for t in out_tensors}
+        self.enabled = [r for r in self.regions
+                        if own and r["buf"]._version == 0 and all(id(m) in ids for m in r["members"])]
+
+    def arm(self, stream) -> None:
+        """Before the first replay: each relocated category's first fresh buffer and its word."""
+        if not self.enabled:
+            return
+        tbl = np.zeros(len(self.enabled), dtype=N.COPY_SPAN_DTYPE)
+        for i, r in enumerate(self.enabled):
+            cur = torch.empty_like(r["buf"])
+            r["box"] = [cur]  # (the buffer the next replay writes: OutputAlloc moves it on)
+            tbl[i] = ((cur.data_ptr() - r["buf"].data_ptr()) % (1 << 64), r["word"], N.VMAS_COPY_STORE64)
+        dev = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        N.copy_table_at(dev, tbl.ctypes.data, 0, len(tbl), stream)
+        self._arm_tbl = tbl  # (the launch reads its arguments at enqueue time; kept for clarity)
+
+
 class _FreshState:
     """Fresh entity-state tensors after every replay, made on first use.
 
@@ -482,6 +555,7 @@ class StepGraph:
         self._executed = None  # outputs of a capture step that already ran (segmented capture)
         self._carry_ys: List[Tensor] = []  # the Y tensors as bound (version counters)
         self._post: Optional[dict] = None  # what the last post-replay launch covered (_post_replay)
+        self._direct: Optional[DirectOutputs] = None  # (the capture's directly written outputs)
         # launches captured with their host side deferred (world._deferred_sink: discovery's
         # DeferredRespawn): armed before every replay, finished after its host work is queued
         self._deferred: List[Any] = []
@@ -738,6 +812,7 @@ class StepGraph:
         # before the hole for real, so a failure after that has state to restore
         contents = [(t, t.clone()) for t, _ in versions.values()]
         segs = _Segments(side)
+        self._direct = DirectOutputs(dev) if self._DIRECT else None
         deferred: List[Any] = []
 
         def deferred_sink(d):  # captured here; armed / finished around each replay
@@ -750,6 +825,7 @@ class StepGraph:
             env.world._hole_sink = segs.hole
             # (the deferred form only when the step draws no other device random numbers)
             env.world._deferred_sink = None if getattr(self, "_device_rng_outside_holes", True) else deferred_sink
+            env.world._direct_out = self._direct
             torch.cuda.synchronize(dev)
             self._folding = self._fold_steps_ok()
             with torch.cuda.stream(side), consts:
@@ -763,14 +839,16 @@ class StepGraph:
             self._consts = consts
             self._asserts = asserts
             self._sig = eng.graph_token()
+            if self._direct is not None and not segs.holes:  # (a segmented step keeps its copies)
+                self._direct.finalize(_tensors(out, []), env.scenario)
             self._plan(objs, snap, out)
+            if self._direct is not None:
+                self._direct.arm(N.stream_ptr(self._dev_index()))
             self._inplace = [t for t, v in versions.values() if t._version != v]
             self._bk_src: List[Tensor] = []
             self._bk_dst: List[Tensor] = []
             self._bk_u = None
         except Exception as ex:  # noqa: BLE001 -- any capture failure means "stay eager"
-            from ... import _native as N
-
             # a capture invalidated by a forbidden call may be left open: end it, so that the
             # eager step that follows can launch
             N.load_library().vmas_stream_abort_capture(ctypes.c_void_p(side.cuda_stream))
@@ -790,6 +868,7 @@ class StepGraph:
             self.status = "eager"
             self.why = f"{type(ex).__name__}: {str(ex).splitlines()[0] if str(ex) else ''}"[:300]
             self.graph = None
+            self._direct = None
             self._folding = False
             return False
         finally:
@@ -800,6 +879,7 @@ class StepGraph:
             env.world._assert_range_sink = None
             env.world._hole_sink = None
             env.world._deferred_sink = None
+            env.world._direct_out = None
         del contents
         self._steps_folded, self._folding = self._folding, False
         self._steps_t = env.steps
@@ -937,6 +1017,8 @@ class StepGraph:
             self._raw_exec = ctypes.c_void_p(self.graph.raw_cuda_graph_exec())
 
     _RAW_LAUNCH = os.environ.get("VMAS_GRAPH_RAW_LAUNCH", "1") != "0"  # (A/B knob)
+    # fused programs write the step's outputs into fresh tensors (DirectOutputs); 0: copied out
+    _DIRECT = os.environ.get("VMAS_GRAPH_DIRECT_OUTPUTS", "1") != "0"
     # fresh entity-state tensors on first use after each replay (_FreshState); 0: the states stay
     # views of the graph's buffers (an alias kept across a step then sees later steps' values)
     _FRESH_STATES = os.environ.get("VMAS_GRAPH_FRESH_STATES", "1") != "0"
@@ -1125,6 +1207,7 @@ class StepGraph:
         tbl, n_out, n_all = t["addr"], t["n_out"], t["n_all"]
         if t["plain"]:  # non-contiguous carries / backups: the old order
             N.copy_table_at(dev, tbl, 0, n_out, st)
+            t["host"].commit()
             self._clone_finish(rest)
             self._post = None
         else:
@@ -1133,6 +1216,7 @@ class StepGraph:
                 N.copy_table_at(dev, tbl, n_out, n_all, st)
             else:
                 N.copy_table_at(dev, tbl, 0, n_all, st)
+            t["host"].commit()
             self._clone_finish(rest)
             self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),
                           "bk_ver": tuple(map(_VERSION, self._inplace)), "bk_n": t["n_bk"]}
@@ -1152,6 +1236,11 @@ class StepGraph:
             return c[4]
         out_rows = [(x.data_ptr(), 0, x.numel() * x.element_size()) for _, _, srcs in self._clone_group_srcs
                     for x in srcs if x.is_contiguous()]
+        direct = self._direct.enabled if self._direct is not None else []
+        direct_rows = []
+        for r in direct:  # (the next replay's buffer offset: written by OutputAlloc.alloc)
+            direct_rows.append(len(out_rows))
+            out_rows.append((0, r["word"], N.VMAS_COPY_STORE64))
         steps_row = None
         if self._steps_folded:  # (last output row: the launch of the outputs always covers it)
             st = self.env.steps
@@ -1163,10 +1252,11 @@ class StepGraph:
         tbl = np.zeros(len(out_rows) + len(extra), dtype=N.COPY_SPAN_DTYPE)
         for i, row in enumerate(out_rows + extra):
             tbl[i] = row
-        clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows for _, x, cn in carry)
+        clash = any(lo < x + cn and x < lo + nb for lo, _, nb in out_rows if nb > 0 for _, x, cn in carry)
         t = {"tbl": tbl, "addr": tbl.ctypes.data, "n_out": len(out_rows), "n_all": len(out_rows) + len(extra),
              "plain": plain,
              "clash": clash, "n_bk": n_bk, "steps_row": steps_row, "steps": self.env.steps if self._steps_folded else None,
+             "direct_rows": direct_rows,
              "contig": [[x.is_contiguous() for x in srcs] for _, _, srcs in self._clone_group_srcs]}
         self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
         return t
@@ -1189,8 +1279,12 @@ class StepGraph:
             loose += [(start + k, srcs[k]) for k, c in enumerate(contig) if not c]
             row += len(ks)
             start += n
+        direct = self._direct.enabled if self._direct is not None else []
+        regions = [(r["buf"], r["box"], r["members"][0], row,
+                    [(list(m.shape), list(m.stride()), m.storage_offset()) for m in r["members"]])
+                   for r, row in zip(direct, t["direct_rows"])]
         host = N.load_host().OutputAlloc(self._dev_index(), groups, t["tbl"], t["addr"], N.fn_addr("vmas_copy_spans"),
-                                         N.fn_addr("vmas_aux_last_error"))
+                                         N.fn_addr("vmas_aux_last_error"), regions)
         t["host"], t["loose"] = host, loose
         return host
 
@@ -1233,13 +1327,25 @@ class StepGraph:
         function generated for its structure.  Built once per capture (the replay's output tensors
         are fixed), so a step makes a handful of host calls instead of several per output."""
         ts = self._out_tensors
+        direct = self._direct.enabled if self._direct is not None else []
+        dmember = {id(m): (ri, mi) for ri, r in enumerate(direct) for mi, m in enumerate(r["members"])}
         groups: Dict[Tuple[torch.dtype, Tuple[int, ...]], List[int]] = {}
         for i, t in enumerate(ts):
-            groups.setdefault((t.dtype, tuple(t.shape)), []).append(i)
+            if id(t) not in dmember:  # (directly written: views of the replay's fresh buffer)
+                groups.setdefault((t.dtype, tuple(t.shape)), []).append(i)
         plan = sorted(groups.items(), key=lambda kv: str(kv[0][0]))  # same dtypes adjacent
         self._clone_groups = [(dt, shape, len(idx)) for (dt, shape), idx in plan]
         order = [i for _, idx in plan for i in idx]  # position in the concatenated views -> output
         pos = {i: p for p, i in enumerate(order)}
+        # the direct categories' members follow the groups' views (OutputAlloc.alloc's order)
+        base, at = [], len(order)
+        for r in direct:
+            base.append(at)
+            at += len(r["members"])
+        for i, t in enumerate(ts):
+            if id(t) in dmember:
+                ri, mi = dmember[id(t)]
+                pos[i] = base[ri] + mi
         # per (dtype, shape) group, in view order: its sources
         self._clone_group_srcs, start = [], 0
         for _, idx in plan:
@@ -1281,6 +1387,7 @@ class StepGraph:
             self._steps_current(t)
         views, rest = self._clone_alloc(t)
         N.copy_table_at(self._dev_index(), t["addr"], 0, t["n_out"], self._stream())
+        t["host"].commit()
         self._clone_finish(rest)
         fn, consts = self._clone_build
         return fn(views, consts)
