@@ -325,6 +325,8 @@ def main():
     sync()
     barrier()
     sync()
+    handovers = type(env.scenario).make_world.__globals__.get("HANDOVERS", [0])  # (discovery's respawn)
+    h0 = handovers[0]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         env.step(env.get_random_actions())
@@ -456,6 +458,8 @@ def main():
         "roofline": roofline,
         "roofline_program": program,
     }
+    if args.scenario == "discovery":  # (respawns the one-launch sampler handed over to the reference loop)
+        out["config"]["respawn_handovers"] = {"timed": handovers[0] - h0, "total": handovers[0]}
     if rank == 0 and world_size == 1 and args.cpu_steps > 0:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

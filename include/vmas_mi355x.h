@@ -440,6 +440,9 @@ typedef struct VmasSpawnTargetsIO {
 } VmasSpawnTargetsIO;
 #define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets) + 32 * 32)
 #define VMAS_SPAWN_ERR_WORD 64
+/* (u64 at int32 index 36 of the words) the generator offset after a call through a channel: the
+ * call's offset plus the tries the reference loop consumes (valid when the call resolved) */
+#define VMAS_SPAWN_OFF_END_WORD 36
 /* scratch words of the windowed kernel for (batch, n_targets); -1 for bad arguments */
 int64_t vmas_spawn_scratch_words(int32_t batch, int32_t n_targets);
 int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_t* increment, void* stream);
@@ -662,10 +665,14 @@ int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, int32_t n, vo
 /* The copies of vmas_copy_spans (at most 96 spans) and the draw of vmas_uniform_columns_snap (at
  * most 16 columns) in ONE launch: graph mode's post-replay copies together with the next step's
  * random actions drawn ahead (simulator/environment/_graph.py); the numbers and the generator
- * increment are those of vmas_uniform_columns (no reference counterpart beyond those two). */
+ * increment are those of vmas_uniform_columns (no reference counterpart beyond those two).
+ * offset_dev (optional, v5): a device word holding the generator offset to draw at, read when the
+ * launch runs (`offset` is then added to it): the offset a spawn launch earlier on the stream leaves
+ * (max_accepted words at VMAS_SPAWN_OFF_END_WORD), unknown to the host when it queues the draw. */
 int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* spans, int32_t n_spans, int64_t numel,
                              const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed, uint64_t offset,
-                             int32_t mode, int64_t u_snap_delta, uint64_t* increment, void* stream);
+                             const uint64_t* offset_dev, int32_t mode, int64_t u_snap_delta, uint64_t* increment,
+                             void* stream);
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);

@@ -362,13 +362,20 @@ def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps", [("balance", dict(n_agents=4), 10), ("flocking", dict(n_agents=4), None),
-                                               ("discovery", dict(n_agents=4), None)],
-                         ids=["balance", "flocking", "discovery"])
-def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substeps):
+                                               ("discovery", dict(n_agents=4), None),
+                                               ("discovery-redo", dict(n_agents=4), None)],
+                         ids=["balance", "flocking", "discovery", "discovery-redo"])
+def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name, kw, substeps):
     """env.step(env.get_random_actions()) in graph mode: the draw kernel also writes the applied
     actions into the graph's action buffer, and the step launches no action kernel.  Bit-identical
     to the eager step on the same draws; an in-place edit of the drawn tensors, or other tensors,
-    take the normal action path."""
+    take the normal action path.  Discovery: the next draw is made ahead at the generator offset
+    the in-graph respawn leaves on the device; "discovery-redo" hands every respawn over to the
+    reference loop (VMAS_SPAWN_TEST_MAX_TRIES=1), so every such draw is dropped and made anew."""
+    redo = name == "discovery-redo"
+    if redo:
+        monkeypatch.setenv("VMAS_SPAWN_TEST_MAX_TRIES", "1")
+        name = "discovery"
     eager, graph = _twin_envs(gpu_device, name, **kw)
     for env in (eager, graph):
         if substeps:
@@ -404,9 +411,11 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, name, kw, substep
         _assert_same([a.action.u for a in eager.agents], [a.action.u for a in graph.agents], f"u step {t}")
         assert torch.equal(eager.steps, graph.steps), (name, t)
     assert graph.graph_status == "graph", graph.graph_reason
-    assert graph.preapplied_steps >= 5
-    if name == "balance":  # (no device asserts, no deferred launch: draws were made ahead and handed out)
+    assert graph.preapplied_steps >= (0 if redo else 5)  # (a redone respawn edits state between steps)
+    if name in ("balance", "discovery") and not redo:  # (no device asserts: draws made ahead, handed out)
         assert graph._SPEC_DRAW and getattr(graph, "drawn_ahead", 0) >= 3
+    if redo:
+        assert getattr(graph, "drawn_ahead", 0) == 0
 
 
 @pytest.mark.gpu

@@ -70,6 +70,7 @@ def launch(self):
 
 _graph.StepGraph._launch = launch
 wrap(_graph.StepGraph, "_post_replay", "clone0", "clone1")
+wrap(_graph.StepGraph, "_finish_deferred", "deferred0", "deferred1")
 
 N = 100
 torch.cuda.synchronize()
@@ -85,6 +86,8 @@ wall = (time.perf_counter() - t0) / N * 1e6
 
 
 def mean_us(a, b):
+    if a not in stamps or b not in stamps:
+        return float("nan")  # (the path did not run: e.g. pre-applied actions skip the action launch)
     return sum(y - x for x, y in zip(stamps[a], stamps[b])) / len(stamps[a]) * 1e6
 
 
@@ -97,6 +100,7 @@ out = {
         "apply_actions_incl_wait": round(mean_us("apply0", "apply1"), 1),
         "graph_replay_launch": round(mean_us("replay0", "replay1"), 1),
         "post_replay_copies": round(mean_us("clone0", "clone1"), 1),
+        "deferred_finish_incl_wait": round(mean_us("deferred0", "deferred1"), 1),
         "whole_step_call": round(mean_us("draw1", "step1"), 1),
     },
     "gpu_us": {"graph_replay": round(gpu_graph, 1)},

@@ -254,6 +254,7 @@ VMAS_SPAWN_MAX_TRIES = 65536
 
 
 VMAS_SPAWN_ERR_WORD = 64
+VMAS_SPAWN_OFF_END_WORD = 36  # (u64: the generator offset after a call through a channel)
 
 
 def spawn_words(n_targets: int) -> int:  # VMAS_SPAWN_WORDS
@@ -559,7 +560,7 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_copy_spans.argtypes = [_i32, _vp, _i32, _vp]
     lib.vmas_copy_spans_draw.restype = _i32
     lib.vmas_copy_spans_draw.argtypes = [_i32, _vp, _i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64, ctypes.c_uint64,
-                                         _i32, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64), _vp]
+                                         _vp, _i32, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint64), _vp]
     lib.vmas_stream_abort_capture.restype = _i32
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_graph_launch.restype = _i32

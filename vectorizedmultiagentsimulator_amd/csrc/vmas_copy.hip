@@ -79,6 +79,7 @@ struct CopyDrawArgs {
     VmasUniformColumn c[kMergedCols];
     unsigned long long seed;
     long long numel, snap;
+    const unsigned long long* off_dev;  // (non-null: the columns' offsets are relative to *off_dev)
     int n_spans, gx_draw, mode, pad;
 };
 static_assert(sizeof(CopyDrawArgs) <= 4096, "kernel argument block");
@@ -90,7 +91,9 @@ __global__ void __launch_bounds__(kCopyThreads) k_copy_draw(CopyDrawArgs a) {
         return;
     }
     if ((int)blockIdx.x >= a.gx_draw) return;
-    vmas_uniform::draw_column(a.c[y - a.n_spans], a.seed, a.numel, a.snap, a.mode, a.gx_draw, (int)blockIdx.x);
+    VmasUniformColumn col = a.c[y - a.n_spans];
+    if (a.off_dev) col.offset += *a.off_dev;  // (the generator offset a device launch left: see the ABI)
+    vmas_uniform::draw_column(col, a.seed, a.numel, a.snap, a.mode, a.gx_draw, (int)blockIdx.x);
 }
 
 constexpr int kFillThreads = 256;
@@ -143,7 +146,8 @@ extern "C" int32_t vmas_copy_spans(int32_t device, const VmasCopySpan* spans, in
 
 extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* spans, int32_t n_spans, int64_t numel,
                                         const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed, uint64_t offset,
-                                        int32_t mode, int64_t u_snap_delta, uint64_t* increment, void* stream) {
+                                        const uint64_t* offset_dev, int32_t mode, int64_t u_snap_delta,
+                                        uint64_t* increment, void* stream) {
     if (device < 0 || n_spans < 0 || n_spans > kMergedSpans || (n_spans > 0 && !spans) || n_cols <= 0 ||
         n_cols > kMergedCols || !cols || numel <= 0 || !increment || mode < 0 || mode > 3)
         return vmas_aux::fail(VMAS_E_INVALID, "vmas_copy_spans_draw: bad arguments");
@@ -177,6 +181,7 @@ extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* span
     a.seed = seed;
     a.numel = numel;
     a.snap = u_snap_delta;
+    a.off_dev = reinterpret_cast<const unsigned long long*>(offset_dev);
     a.n_spans = n;
     a.gx_draw = gx_draw;
     a.mode = mode;

@@ -41,7 +41,7 @@ using CopySpansFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, void*);
 using UniformColumnsSnapFn = int32_t (*)(int32_t, int64_t, const VmasUniformColumn*, int32_t, uint64_t, uint64_t,
                                          int32_t, int64_t, uint64_t*, void*);
 using CopySpansDrawFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, int64_t, const VmasUniformColumn*, int32_t,
-                                    uint64_t, uint64_t, int32_t, int64_t, uint64_t*, void*);
+                                    uint64_t, uint64_t, const uint64_t*, int32_t, int64_t, uint64_t*, void*);
 using LastErrorFn = const char* (*)(void);
 
 void* current_stream(int device) {
@@ -278,9 +278,11 @@ private:
 // OutputAlloc.post with the next step's random actions drawn in the same launch (speculatively:
 // the generator is NOT advanced here; the host hands the draw out and advances it by `increment`
 // only if get_random_actions is called next at the same generator state).  Returns (outputs,
-// drawn per-agent tensors, snapshot, seed, offset, increment).
+// drawn per-agent tensors, snapshot, seed, offset, increment).  off_dev (a device address, 0:
+// none): the draw's generator offset is read there when the launch runs (a spawn launch earlier on
+// the stream leaves it); the returned offset is then None.
 py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, int64_t snap_base, int64_t snap_numel,
-                    int64_t copy_draw_fn) {
+                    int64_t copy_draw_fn, int64_t off_dev) {
     std::vector<at::Tensor> outs = oa.alloc();
     auto [acts, snap, delta] = d.prepare(snap_base, snap_numel);
     if (mid > 0) oa.launch(0, mid);
@@ -291,14 +293,15 @@ py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, in
         std::lock_guard<std::mutex> lock(gen.mutex());
         auto* impl = gen.get<at::CUDAGeneratorImpl>();
         seed = impl->current_seed();
-        off = impl->get_offset();
+        off = off_dev ? 0 : impl->get_offset();
     }
     const int32_t rc = ((CopySpansDrawFn)copy_draw_fn)(d.device(), oa.table() + lo, (int32_t)(hi - lo), d.batch(),
-                                                       d.cols(), (int32_t)d.n_cols(), seed, off, d.mode(), delta, &inc,
+                                                       d.cols(), (int32_t)d.n_cols(), seed, off,
+                                                       (const uint64_t*)off_dev, d.mode(), delta, &inc,
                                                        current_stream(d.device()));
     if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
     oa.commit();
-    return py::make_tuple(outs, acts, snap, seed, off, inc);
+    return py::make_tuple(outs, acts, snap, seed, off_dev ? py::object(py::none()) : py::object(py::int_(off)), inc);
 }
 
 // (tensor._version of each, as a tuple: the version snapshots of the post-replay bookkeeping)

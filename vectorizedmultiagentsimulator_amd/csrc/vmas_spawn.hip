@@ -276,9 +276,23 @@ __device__ __forceinline__ void launch_rng(const VmasSpawnTargetsIO& io, const C
 }
 
 // (the last workgroup done with the last target, one wave) the launch's words to the channel: every
-// maximum and unresolved count has landed (each workgroup's before its completion)
-__device__ __forceinline__ void publish_channel(const ChanArgs& ch, const int32_t* W, int T, unsigned long long seq) {
+// maximum and unresolved count has landed (each workgroup's before its completion).  Also the
+// generator offset after the call (the launch's offset + the tries the reference loop consumes) into
+// the launch's words at kOffEndWord, for a draw made ahead on the device (vmas_copy_spans_draw's
+// offset_dev; meaningless when the call is unresolved -- the host then draws anew).
+constexpr int kOffEndWord = VMAS_SPAWN_OFF_END_WORD;  // (int32 index; a u64, 8-byte aligned)
+__device__ __forceinline__ void publish_channel(const ChanArgs& ch, int32_t* W, int T, unsigned long long seq,
+                                                unsigned long long off0, unsigned long long per_try) {
     const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        unsigned long long tries = 0;
+        for (int j = 0; j < T; ++j) {
+            const int m = ld_agent(W + j);
+            tries += m == 0 ? 1ull : (unsigned long long)m + 2ull;
+        }
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(W + kOffEndWord), off0 + tries * per_try,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int32_t* o = reinterpret_cast<int32_t*>(ch.out);
     if (lane < T) __hip_atomic_store(o + lane, ld_agent(W + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane == 16) __hip_atomic_store(o + 16, ld_agent(W + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -423,7 +437,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets(VmasSpawnTar
                 last = atomicAdd(&done[32 * i], 1) == n_groups - 1;
                 if (prof) prof[(long)it * 6 + 4] = __builtin_amdgcn_s_memrealtime();
             }
-            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2]);
+            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2], rng_s[1], per_try);
         }
         // (item_s is rewritten only after every wave has passed the barrier above)
     }
@@ -563,7 +577,7 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
             // the last group done: every maximum has landed (each group's before its completion);
             // it publishes the tries consumed so far to the replicas the others poll (kSpawnReplicas
             // lines: one line polled by every workgroup took ~6 us to see the count complete)
-            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2]);
+            if (ch.out && i == T - 1 && __shfl(last, 0)) publish_channel(ch, W, T, rng_s[2], rng_s[1], per_try);
             if (__shfl(last, 0) && i + 1 < T) {
                 int mv[VMAS_SPAWN_MAX_TARGETS];
 #pragma unroll
@@ -588,8 +602,10 @@ __global__ void __launch_bounds__(64 * kSpawnWaves) k_spawn_targets_resident(Vma
 // round 1 saw memset nodes in front of k_world's persistent launch that had not completed when the
 // kernel ran.  A kernel node is ordered like every other node of the graph.
 // (With a channel it also stages the channel's generator state at kRngWord, see launch_rng.)
+constexpr int kWinNextWord = 38;  // (the windowed kernels' window for the next call: kept by the clear)
 __global__ void __launch_bounds__(256) k_spawn_clear(int32_t* w, int n, const uint64_t* chan_in) {
-    for (int i = (int)threadIdx.x; i < n; i += 256) w[i] = 0;
+    for (int i = (int)threadIdx.x; i < n; i += 256)
+        if (i != kWinNextWord) w[i] = 0;
     __syncthreads();
     if (chan_in && threadIdx.x < 3)
         reinterpret_cast<unsigned long long*>(w + kRngWord)[threadIdx.x] =
@@ -637,6 +653,14 @@ struct WinArgs {
     int cap, pairs, q0;
 };
 constexpr int kWinCluster = 16;  // groups per cluster (the first reduction of the tables)
+// The window of a call: the previous call's consumption + kWinMargin tries, rounded up to 16 (its
+// chain kernel leaves it in the words at kWinNextWord; 0, or anything else, means the full window).
+// C4 consumes ~74-84 tries over 7 targets (std ~3): 96 or 112 instead of 128 draws per env.
+constexpr int kWinMargin = 24;
+__device__ __forceinline__ int win_pairs(const int32_t* W, int full) {
+    const int w = W[kWinNextWord];
+    return (w >= 32 && w < full && (w & 15) == 0) ? w : full;  // (a multiple of 16: whole pairs per wave)
+}
 // (max_accepted words) cluster c's count: the per-target kernels' replica words, free here
 __host__ __device__ inline int win_cluster_word(int T) { return 96 + 32 * T; }
 
@@ -736,6 +760,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
     if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+    const int WP = win_pairs(io.max_accepted, wa.pairs);  // (the tries this call evaluates)
     float2* occ = reinterpret_cast<float2*>(win_lds);                // [n_occ][64]
     uint32_t* okw = reinterpret_cast<uint32_t*>(occ + n_occ * 64);   // [T][64][4] the masks
     uint32_t* covs = okw + T * 64 * 4;                               // [64] covered bits
@@ -772,11 +797,14 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
     {
         // this wave's R pairs, all drawn first (independent philox chains in flight), then tested
         // against each occupied position once
-        const int p0 = __builtin_amdgcn_readfirstlane(wave) * R;
+        // (this call's window spread over every wave: Rw <= R pairs each, so that no SIMD keeps
+        // the full window's share when the window shrinks)
+        const int Rw = (WP + kWinWaves - 1) / kWinWaves;
+        const int p0 = __builtin_amdgcn_readfirstlane(wave) * Rw;
         f32x2 c[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const float2 v = spawn_pair(io, g, Q0, seed, off0, p0 + r, bb);
+            const float2 v = r < Rw ? spawn_pair(io, g, Q0, seed, off0, p0 + r, bb) : make_float2(0.f, 0.f);
             c[r] = f32x2{v.x, v.y};
         }
         uint32_t hit = 0u;  // bit r: pair r lands near an agent
@@ -805,7 +833,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
         suf[VMAS_SPAWN_MAX_TARGETS] = ~0u;
 #pragma unroll
         for (int j = VMAS_SPAWN_MAX_TARGETS - 1; j >= 0; --j) suf[j] = suf[j + 1] & far[j];
-        const uint32_t rmask = (1u << R) - 1u;
+        const uint32_t rmask = (1u << Rw) - 1u;
         const int s = p0, w0 = s >> 5, sh = s & 31;
         uint32_t pre = ~0u;
 #pragma unroll
@@ -814,7 +842,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
             pre &= ((covm >> i) & 1u) ? ~0u : far[i];
             if (i < T && ok) {
                 atomicOr(&okw[(i * 64 + lane) * 4 + w0], ok << sh);
-                if (sh + R > 32) atomicOr(&okw[(i * 64 + lane) * 4 + w0 + 1], ok >> (32 - sh));
+                if (sh + Rw > 32) atomicOr(&okw[(i * 64 + lane) * 4 + w0 + 1], ok >> (32 - sh));
             }
         }
     }
@@ -924,7 +952,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO 
     const int T = io.n_targets, c4 = T * 8;  // (uint4 columns of a table row)
     int32_t* const W = io.max_accepted;
     const int MT = io.max_tries > 0 ? io.max_tries : VMAS_SPAWN_MAX_TRIES;
-    const int WP = wa.pairs;
+    const int WP = win_pairs(W, wa.pairs);  // (as the candidates kernel evaluated them)
     const int cap = win_list_cap(T);
     uint32_t* lmask = reinterpret_cast<uint32_t*>(win_lds);             // [cap][T][4]
     float2* newpos = reinterpret_cast<float2*>(lmask + cap * T * 4);      // [cap][T]
@@ -1106,9 +1134,15 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO 
             }
     }
     if (threadIdx.x == 0) {
+        int used = 0;  // (the tries the reference loop consumes: the next call's window from it)
         if (!unresolved)
-            for (int i = 0; i < T; ++i) W[i] = mc_s[i];
+            for (int i = 0; i < T; ++i) {
+                W[i] = mc_s[i];
+                used += mc_s[i] == 0 ? 1 : mc_s[i] + 2;
+            }
         W[T] = unresolved ? 1 : 0;
+        const int next = (used + kWinMargin + 15) & ~15;
+        W[kWinNextWord] = unresolved || next >= wa.pairs ? 0 : max(next, 32);
     }
     if (stamp) {
         stamp_s[4] = __builtin_amdgcn_s_memrealtime();
@@ -1118,7 +1152,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO 
     if (ch.out) {  // (publish_channel reads the words with agent-scope loads: stored above by this group)
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-        if (wave == 0) publish_channel(ch, W, T, rng_s[2]);
+        if (wave == 0) publish_channel(ch, W, T, rng_s[2], rng_s[1], 2ull * g.inc);
     }
 }
 

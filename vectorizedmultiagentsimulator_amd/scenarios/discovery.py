@@ -548,11 +548,15 @@ def respawn_reference_loop(agents_pos: Tensor, covered: Tensor, min_dist: float,
         tp.copy_(torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), tp))
 
 
+HANDOVERS = [0]  # (respawns redone by the reference loop in this process: bench.py reports it)
+
+
 def _respawn_redo(args, backup: Tensor, offset: int, gen) -> None:
     """Undo a one-launch respawn that left an env unresolved after max_tries tries, or whose
     bounded wait timed out (a workgroup never ran: the co-residency the resident kernel assumes did
     not hold), and redo it with the reference's loop: the targets back from the launch's backup,
     the generator back to the launch's offset."""
+    HANDOVERS[0] += 1
     targets = args[5:]
     for i, tp in enumerate(targets):
         tp.copy_(backup[i])
@@ -671,7 +675,7 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     dev = agents_pos.device
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     T = len(target_pos)
-    mx = out if out is not None else torch.empty(N.spawn_words(T), dtype=torch.int32, device=dev)
+    mx = out if out is not None else torch.zeros(N.spawn_words(T), dtype=torch.int32, device=dev)  # (zeros: see k_spawn_clear)
     backup = torch.empty((T, agents_pos.shape[0], 2), dtype=torch.float32, device=dev)
     scratch = spawn_scratch(agents_pos.shape[0], T, dev)
     io, inc = _spawn_launch(agents_pos, covered, min_dist, x_semidim, y_semidim, target_pos, mx, backup=backup,

@@ -726,16 +726,39 @@ class StepGraph:
                         + ", ".join(f"{names.get(i, '?')}.{k}" for i, k in changed[:4]))[:300]
         return out
 
+    _AHEAD_DEFERRED = os.environ.get("VMAS_GRAPH_DRAW_AHEAD_DEFERRED", "1") != "0"  # (A/B knob)
+
+    def _ahead_offset_word(self):
+        """Where a draw made ahead in the post-replay launch reads its generator offset: 0 (the
+        host passes it) without deferred launches; with one spawn channel (discovery's respawn,
+        whose host side advances the generator only after this launch is queued) the device word
+        the respawn launch leaves it in (VMAS_SPAWN_OFF_END_WORD); None: no draw ahead."""
+        if not self._deferred:
+            return 0
+        if len(self._deferred) != 1 or not self._AHEAD_DEFERRED:
+            return None
+        mx = getattr(getattr(self._deferred[0], "chan", None), "mx", None)
+        return None if mx is None else mx.data_ptr() + 4 * N.VMAS_SPAWN_OFF_END_WORD
+
     def _finish_deferred(self, apply: bool = True, out=None):
         """The host side of the captured deferred launches (discovery's respawn).  One that had to
         be redone on the host (DeferredRespawn.finish) changed state the graph's observations had
-        already read: the step's observations in ``out`` are recomputed eagerly."""
+        already read: the step's observations in ``out`` are recomputed eagerly.  A draw made ahead
+        at the device offset the respawn left gets that offset now -- the generator's, once the
+        respawn's tries are accounted -- or is dropped when the respawn was redone (its offset
+        word is then not what the host loop leaves)."""
         err, redone = None, False
         for d in self._deferred:
             try:
                 redone |= bool(d.finish(apply))
             except Exception as ex:  # noqa: BLE001 -- drain every channel, then raise the first
                 err = err or ex
+        sp = getattr(self.env, "_spec", None)
+        if sp is not None and sp[3] is None:
+            if err is not None or redone or not apply:
+                self.env._spec = None
+            else:
+                self.env._spec = sp[:3] + (sp[0][5].get_offset(),) + sp[4:]
         if err is not None:
             raise err
         if redone and out is not None:
@@ -1187,12 +1210,15 @@ class StepGraph:
                 self._steps_current(t)
             host = t.get("host") or self._host_alloc(t)
             mid, hi = (t["n_out"] if t["clash"] else 0), t["n_all"]
-            # (not with deferred launches: their host side advances the generator after this)
-            ahead = self.env._draw_ahead_plan() if (hi - mid <= 96 and not t["n_bk"] and not self._deferred) else None
+            # (with a deferred launch -- discovery's respawn, whose host side advances the generator
+            # after this -- the draw reads its offset where the respawn launch leaves it)
+            off_dev = self._ahead_offset_word()
+            ahead = (self.env._draw_ahead_plan() if (hi - mid <= 96 and not t["n_bk"] and off_dev is not None)
+                     else None)
             if ahead is not None:  # (+ the next step's random actions in the same launch)
                 st, drawer, P = ahead
                 views, acts, snap, seed, off, inc = N.load_host().post_draw(
-                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"))
+                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"), off_dev)
                 self.env._drew_ahead(st, acts, snap, seed, off, inc)
             else:
                 views = host.post(mid, hi)
