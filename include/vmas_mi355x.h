@@ -437,7 +437,14 @@ typedef struct VmasSpawnTargetsIO {
                                              (128 tries of the call's shared stream, VMAS_SPAWN_WINDOW) counts
                                              as unresolved, as past max_tries */
     int64_t scratch_words;
+    int32_t prestaged;                    /* (v5, with a channel and the windowed kernels) the launch's words
+                                             were cleaned by the previous call through them and the channel's
+                                             words staged by an earlier launch on the stream (the discovery
+                                             REWARD launch's stage_out): no clear kernel */
+    int32_t pad2;
 } VmasSpawnTargetsIO;
+/* (int32 index of the words) where a channel's (seed, offset, seq) are staged for the launch */
+#define VMAS_SPAWN_RNG_WORD 40
 #define VMAS_SPAWN_WORDS(n_targets) (96 + 32 * (n_targets) + 32 * 32)
 #define VMAS_SPAWN_ERR_WORD 64
 /* (u64 at int32 index 36 of the words) the generator offset after a call through a channel: the
@@ -456,6 +463,9 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
 typedef struct VmasSpawnChannel VmasSpawnChannel;
 int32_t vmas_spawn_channel_create(int32_t device, VmasSpawnChannel** out);
 int32_t vmas_spawn_channel_destroy(VmasSpawnChannel* ch);
+/* (v5) the device address of the channel's armed words (seed, offset, seq): what an earlier launch of
+ * the step copies into the respawn's words (VmasDiscoveryIO.stage_in) */
+int32_t vmas_spawn_channel_in(VmasSpawnChannel* ch, const uint64_t** d_in);
 /* the generator state the next launch through the channel reads; seq != 0, new per launch */
 int32_t vmas_spawn_channel_arm(VmasSpawnChannel* ch, uint64_t seed, uint64_t offset, uint32_t seq);
 /* waits (host spin, checking `stream` for errors) for the launch armed with seq; words[0, T) the
@@ -642,6 +652,11 @@ typedef struct VmasDiscoveryIO {
     const int64_t* out_delta;            /* optional (v5; graph mode's direct outputs): three device words,
                                              the byte offsets added to the obs / rewards / done pointers
                                              (simulator/environment/_graph.py DirectOutputs); NULL: none */
+    const uint64_t* stage_in;            /* optional (v5): a spawn channel's armed words (seed, offset,
+                                             seq), copied by the REWARD launch into stage_out -- the step's
+                                             respawn launch then needs no clear kernel of its own
+                                             (VmasSpawnTargetsIO.prestaged) */
+    uint64_t* stage_out;
 } VmasDiscoveryIO;
 int32_t vmas_discovery_outputs(int32_t device, const VmasDiscoveryIO* io, void* stream);
 

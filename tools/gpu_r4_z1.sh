@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 4, closing evidence 1/2: smoke, the whole GPU suite, C2 bench lines (graph, eager) and the
+# rocprofv3 kernel stats of the C2 bench.
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r4z
+mkdir -p $O
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $O/smoke.log; exit 1; }
+echo "smoke ok"; tail -2 $O/smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+echo "suite rc=$rc"; grep -E "FAILED|ERROR" $O/pytest_gpu.log | head; tail -1 $O/pytest_gpu.log
+case $rc in 0|1) ;; *) exit $rc;; esac
+for i in 1 2; do
+  timeout -k 10 300 python bench.py > $O/bench_c2_$i.log 2>&1 || exit $?
+  echo "C2 run $i: $(tail -1 $O/bench_c2_$i.log | cut -c90-150)"
+done
+timeout -k 10 300 python bench.py --graph off --cpu-steps 0 > $O/bench_c2_eager.log 2>&1 || exit $?
+echo "C2 eager: $(tail -1 $O/bench_c2_eager.log | cut -c90-150)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o c2 --output-format csv -- python bench.py --steps 50 --cpu-steps 0 > $O/prof_c2.log 2>&1 || exit $?
+echo done

@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "vmas_spawn_channel_create",
     "vmas_spawn_channel_destroy",
     "vmas_spawn_channel_arm",
+    "vmas_spawn_channel_in",
     "vmas_spawn_channel_wait",
     "vmas_spawn_profile",
     "vmas_world_step_vjp",
@@ -255,6 +256,7 @@ VMAS_SPAWN_MAX_TRIES = 65536
 
 VMAS_SPAWN_ERR_WORD = 64
 VMAS_SPAWN_OFF_END_WORD = 36  # (u64: the generator offset after a call through a channel)
+VMAS_SPAWN_RNG_WORD = 40  # (where a channel's seed / offset / seq are staged)
 
 
 def spawn_words(n_targets: int) -> int:  # VMAS_SPAWN_WORDS
@@ -270,7 +272,7 @@ class VmasSpawnTargetsIO(ctypes.Structure):
         ("covered", _vp), ("cov_s0", _i32), ("cov_s1", _i32),
         ("min_dist", _f32), ("x_lo", _f32), ("x_hi", _f32), ("y_lo", _f32), ("y_hi", _f32), ("pad1", _f32),
         ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64), ("max_accepted", _vp), ("channel", _vp),
-        ("backup", _vp), ("scratch", _vp), ("scratch_words", ctypes.c_int64),
+        ("backup", _vp), ("scratch", _vp), ("scratch_words", ctypes.c_int64), ("prestaged", _i32), ("pad2", _i32),
     ]
 
 
@@ -414,6 +416,7 @@ class VmasDiscoveryIO(ctypes.Structure):
         ("rewards", _vp * _DA),
         ("covered_count", _vp), ("all_time", _vp), ("done", _vp),
         ("out_delta", _vp),  # (graph mode's direct outputs: [obs, rewards, done] byte offsets)
+        ("stage_in", _vp), ("stage_out", _vp),  # (a spawn channel's words staged for the step's respawn)
     ]
 
 
@@ -550,6 +553,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_spawn_channel_create.argtypes = [_i32, ctypes.POINTER(_vp)]
     lib.vmas_spawn_channel_destroy.restype = _i32
     lib.vmas_spawn_channel_destroy.argtypes = [_vp]
+    lib.vmas_spawn_channel_in.restype = _i32
+    lib.vmas_spawn_channel_in.argtypes = [_vp, ctypes.POINTER(_vp)]
     lib.vmas_spawn_channel_arm.restype = _i32
     lib.vmas_spawn_channel_arm.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
     lib.vmas_spawn_channel_wait.restype = _i32

@@ -482,6 +482,16 @@ __global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
     }
 }
 
+// (the REWARD launch, workgroup 0) a spawn channel's armed words into the step's respawn words
+// (VmasDiscoveryIO.stage_in / stage_out): one PCIe read while the reward runs, instead of a clear
+// kernel of the respawn's own on the step's critical path
+template <class IO>
+__device__ __forceinline__ void disc_stage(IO& io) {
+    if (io.stage_in && blockIdx.x == 0 && threadIdx.x < 3)
+        io.stage_out[threadIdx.x] = __hip_atomic_load(io.stage_in + threadIdx.x, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The optional reductions over the targets (VmasDiscoveryIO.covered_count / done): the count of
 // covered targets (an integer sum: exact) and all() of the all-time covered flags.
 template <class IO>
@@ -497,6 +507,7 @@ __device__ __forceinline__ void disc_reductions(IO& io, int b, int T, int n_cov)
 // discovery.py:146-246 (restated in scenarios/discovery.py), REWARD part: one thread per env.
 __global__ void __launch_bounds__(64) k_discovery_reward(VmasDiscoveryIO io) {
     constexpr int MA = VMAS_DISC_MAX_AGENTS, MT = VMAS_DISC_MAX_TARGETS;
+    disc_stage(io);
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= io.batch) return;
     const int A = io.n_agents, T = io.n_targets;
@@ -624,6 +635,7 @@ typedef const VmasDiscoveryIO KDiscoveryIO;
 constexpr int kDiscFastAgents = 16, kDiscFastTargets = 16;
 __global__ void __launch_bounds__(1024) k_discovery_reward_fast(VmasDiscoveryIO io_arg) {
     VMAS_KARG(KDiscoveryIO, io_arg);
+    disc_stage(io);
     constexpr int MT = kDiscFastTargets;
     __shared__ float D[64 * kDiscFastAgents * kDiscFastTargets];  // dists rows of the 64 envs (64 KiB)
     __shared__ uint32_t IN[kDiscFastAgents][64];                  // agent i's in-range target bits

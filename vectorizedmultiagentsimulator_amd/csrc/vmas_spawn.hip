@@ -258,7 +258,7 @@ struct ChanArgs {
 // int32 index (free words of the claim counter's line) and the spawn kernel's workgroups read them
 // there: 256 workgroups each reading the mapped host words over PCIe took up to 54 us to all start
 // (the reads serialise), one copy by one thread takes one round trip.
-constexpr int kRngWord = 40;
+constexpr int kRngWord = VMAS_SPAWN_RNG_WORD;
 
 // Generator state of a launch: the channel's (staged by k_spawn_clear) or the arguments'.
 __device__ __forceinline__ void launch_rng(const VmasSpawnTargetsIO& io, const ChanArgs& ch, unsigned long long* seed,
@@ -1133,6 +1133,10 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO 
                 p[io.pos_s1[i]] = newpos[d * T + i].y;
             }
     }
+    // the words the next call's candidates count on, back to zero (a prestaged call has no clear
+    // kernel): the listed envs and every cluster's count (read above; the candidates are done)
+    if (threadIdx.x == 0) W[kWinListWord] = 0;
+    for (int c = (int)threadIdx.x; c < n_rows; c += kWinThreads) W[win_cluster_word(T) + c] = 0;
     if (threadIdx.x == 0) {
         int used = 0;  // (the tries the reference loop consumes: the next call's window from it)
         if (!unresolved)
@@ -1289,6 +1293,12 @@ int32_t vmas_spawn_channel_destroy(VmasSpawnChannel* ch) {
     return VMAS_OK;
 }
 
+int32_t vmas_spawn_channel_in(VmasSpawnChannel* ch, const uint64_t** d_in) {
+    if (!ch || !d_in) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_channel_in: bad arguments");
+    *d_in = ch->d_in;
+    return VMAS_OK;
+}
+
 int32_t vmas_spawn_channel_arm(VmasSpawnChannel* ch, uint64_t seed, uint64_t offset, uint32_t seq) {
     if (!ch || seq == 0u) return vmas_aux::fail(VMAS_E_INVALID, "vmas_spawn_channel_arm: bad arguments");
     __atomic_store_n(&ch->h_in[0], seed, __ATOMIC_RELAXED);
@@ -1419,7 +1429,9 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
         uint32_t* sw = reinterpret_cast<uint32_t*>(io->scratch);
         WinArgs wa{sw, sw + (size_t)n_groups * T * 32, sw + (size_t)(n_groups + n_clusters) * T * 32, cap, pairs,
                    q0 ? 1 : 0};
-        hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T), ch.in);
+        if (!(io->prestaged && ch.in))  // (prestaged: cleaned by the previous call, staged by the step)
+            hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T),
+                               ch.in);
         hipLaunchKernelGGL(cands, dim3((unsigned)n_groups), dim3(kWinThreads), lds1, st, *io, g, d2_min, wa, prof, ch);
         if (q0)
             hipLaunchKernelGGL(k_spawn_chain<true>, dim3(1), dim3(kWinThreads), lds2, st, *io, g, d2_min, wa, n_clusters,

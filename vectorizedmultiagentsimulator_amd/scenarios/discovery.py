@@ -298,6 +298,14 @@ class Scenario(BaseScenario):
             }
             for k in ("agents_pos", "targets_pos", "dists", "per_target", "covered", "time_rew"):
                 setattr(io, k, out[k].data_ptr())
+            # (a graph capture whose respawn goes through the spawn channel: this launch stages the
+            # channel's armed words for it -- the respawn launch then runs no clear kernel)
+            ch = getattr(self, "_spawn_channel", None)
+            if (ch is not None and self.targets_respawn and deferred_respawn()
+                    and getattr(w, "_deferred_sink", None) is not None
+                    and ch.backup.shape[0] == T and ch.backup.shape[1] == B):
+                io.stage_in, io.stage_out = ch.d_in, ch.mx.data_ptr() + 4 * N.VMAS_SPAWN_RNG_WORD
+                ch.prestaged = True
             # the step's other reductions over the targets, in the same launch: info's count of
             # covered targets and done() (handed out by _targets_covered_count / done while their
             # inputs are the same tensors at the same versions)
@@ -488,7 +496,8 @@ def spawn_scratch(batch: int, n_targets: int, device) -> Tensor:
 
 
 def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidim: float, y_semidim: float,
-                  target_pos, mx: Tensor, channel=None, backup: Tensor = None, scratch: Tensor = None):
+                  target_pos, mx: Tensor, channel=None, backup: Tensor = None, scratch: Tensor = None,
+                  prestaged: bool = False):
     """One vmas_spawn_targets launch on the current stream; returns (io, philox increment)."""
     import numpy as np
 
@@ -520,6 +529,7 @@ def _spawn_launch(agents_pos: Tensor, covered: Tensor, min_dist: float, x_semidi
     io.backup = backup.data_ptr() if backup is not None else None
     if scratch is not None:
         io.scratch, io.scratch_words = scratch.data_ptr(), scratch.numel()
+    io.prestaged = 1 if prestaged else 0
     inc = ctypes.c_uint64(0)
     N.check_aux(N.load_library().vmas_spawn_targets(idx, ctypes.byref(io), ctypes.byref(inc),
                                                       ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)),
@@ -584,6 +594,10 @@ class SpawnChannel:
         ch = ctypes.c_void_p()
         N.check_aux(N.load_library().vmas_spawn_channel_create(self.idx, ctypes.byref(ch)), "vmas_spawn_channel_create")
         self.ptr = ch
+        d_in = ctypes.c_void_p()
+        N.check_aux(N.load_library().vmas_spawn_channel_in(ch, ctypes.byref(d_in)), "vmas_spawn_channel_in")
+        self.d_in = d_in.value
+        self.prestaged = False  # (the step's reward launch staged the armed words: see Scenario._fused_reward)
         self.seq = 0
         self.busy = None  # the DeferredRespawn with a launch in flight
 
@@ -620,7 +634,8 @@ class DeferredRespawn:
         a = self.args
         self.mx = self.chan.mx
         _, self.inc = _spawn_launch(a[0], a[1], a[2], a[3], a[4], a[5:], self.mx, channel=self.ch,
-                                    backup=self.chan.backup, scratch=self.chan.scratch)
+                                    backup=self.chan.backup, scratch=self.chan.scratch, prestaged=self.chan.prestaged)
+        self.chan.prestaged = False
 
     def arm(self):
         if self.chan.busy is not None:  # (an earlier replay never finished: drain it first)
