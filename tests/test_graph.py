@@ -35,6 +35,19 @@ def _state(env):
     return out
 
 
+def _write_only_attrs(env):
+    """The attributes the package's classes declare write-only within a step (not carried between
+    replays: environment/_graph.py _write_only), as bound now."""
+    objs = [env.scenario] + [s for a in env.agents for s in (a.sensors or ())]
+    out = []
+    for o in objs:
+        for k in sorted(type(o).__dict__.get("_vmas_graph_write_only", ())):
+            v = o.__dict__.get(k)
+            if isinstance(v, torch.Tensor):
+                out.append(v)
+    return out
+
+
 def _rng_save():
     return ([x.clone() if isinstance(x, torch.Tensor) else x for x in Environment.vmas_random_state],
             torch.cuda.get_rng_state())
@@ -110,6 +123,8 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
         out_g = graph.step([a.clone() for a in actions])
         _assert_same(out_e, out_g, f"{name} outputs step {t}")
         _assert_same(_state(eager), _state(graph), f"{name} state step {t}")
+        # (re-bound each step, not carried between replays: the step's values all the same)
+        _assert_same(_write_only_attrs(eager), _write_only_attrs(graph), f"{name} write-only attributes step {t}")
         assert torch.equal(eager.steps, graph.steps), (name, t)  # (folded into the post-replay launch)
         if t == 4:
             held = [(x.clone(), x) for x in _flat(out_g, [])]
@@ -121,6 +136,9 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
         assert len(graph._graph._direct.enabled) == DIRECT[name], [r["dtype"] for r in graph._graph._direct.enabled]
     if expect == "graph":
         assert graph._graph.replays >= 5
+        if name in DIRECT:  # (each declares write-only attributes: none of them carried)
+            wo = {id(t) for t in graph._graph._write_only_ys}
+            assert wo and not wo & {id(y) for y in graph._graph._carry_ys}
         assert graph._graph._steps_folded  # no max_steps: steps += 1 left the graph
     if name == "discovery":  # the targets' respawn is one native call: inside the one graph with
         # its host side after the replay (a spawn channel), or one host hole between two graphs
@@ -224,6 +242,8 @@ def test_failed_action_check_leaves_world_as_eager_gpu(gpu_device, monkeypatch, 
     actions[2][5, 1] = float("nan") if bad == "nan" else 3.0
     _step_both(eager, graph, actions, "^$" if bad == "nan" else "out of its range")
     _assert_same(_state(eager), _state(graph), "state after the failed step")
+    # (a rolled-back replay restores the write-only attributes from its backups)
+    _assert_same(_write_only_attrs(eager), _write_only_attrs(graph), "write-only attributes after the failed step")
     for i, (ae, ag) in enumerate(zip(eager.agents, graph.agents)):
         if i < 2 or speculative:  # (documented: without speculation the failing agent and those
             # after it hold the rejected actions in their persistent u, until the next step)

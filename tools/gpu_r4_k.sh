@@ -18,4 +18,15 @@ for i in 1 2; do
 done
 TAG=c4 ARGS="--scenario discovery" bash tools/step_trace.sh > $O/step_trace_c4.txt 2>&1 || exit $?
 tail -10 $O/step_trace_c4.txt
+for pk in 0 1 0 1; do
+  VMAS_COPY_PACKED=$pk timeout -k 10 200 python bench.py --cpu-steps 0 > $O/ab_packed_c2_$pk.log 2>&1 || exit $?
+  echo "C2 packed=$pk $(tail -1 $O/ab_packed_c2_$pk.log | cut -c1-120)"
+  VMAS_COPY_PACKED=$pk timeout -k 10 200 python bench.py --scenario discovery --cpu-steps 0 --steps 200 > $O/ab_packed_c4_$pk.log 2>&1 || exit $?
+  echo "C4 packed=$pk $(tail -1 $O/ab_packed_c4_$pk.log | cut -c1-120)"
+done
+for sc in discovery balance; do
+  VMAS_COPY_TRACE=1 timeout -k 10 150 python bench.py --scenario $sc --cpu-steps 0 --steps 20 > $O/copytrace_$sc.out 2> $O/copytrace_$sc.log || exit $?
+done
+grep -c span $O/copytrace_discovery.log $O/copytrace_balance.log
+timeout -k 10 200 python tools/host_profile.py discovery 16384 300 > $O/host_profile_c4.log 2>&1 || exit $?
 echo done

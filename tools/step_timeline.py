@@ -20,6 +20,8 @@ from vectorizedmultiagentsimulator_amd.simulator.environment.environment import 
 scenario = sys.argv[1] if len(sys.argv) > 1 else "balance"
 n_envs = int(sys.argv[2]) if len(sys.argv) > 2 else 32768
 kw = {"n_agents": 8 if scenario in ("discovery", "flocking") else 4}
+if scenario == "discovery":  # (bench.py's C4)
+    kw["use_agent_lidar"] = True
 env = make_env(scenario, num_envs=n_envs, device="cuda:0", seed=0, graph_step=True, **kw)
 if scenario == "balance":
     env.world._substeps = 10

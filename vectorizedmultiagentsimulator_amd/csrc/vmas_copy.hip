@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "vmas_aux.hpp"
@@ -28,10 +29,11 @@ struct CopyArgs {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 static_assert(sizeof(CopyArgs) <= 4096, "kernel argument block");
 
+// blk / nblk: this workgroup's index among the span's nblk workgroups (grid-stride over them)
 template <typename T, bool NT = false>
-__device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restrict__ dst, int64_t n) {
-    const int64_t step = (int64_t)gridDim.x * kCopyThreads;
-    int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x;
+__device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restrict__ dst, int64_t n, int blk, int nblk) {
+    const int64_t step = (int64_t)nblk * kCopyThreads;
+    int64_t i = (int64_t)blk * kCopyThreads + threadIdx.x;
     for (; i + (kCopyUnroll - 1) * step < n; i += kCopyUnroll * step) {
         T v[kCopyUnroll];
 #pragma unroll
@@ -45,34 +47,40 @@ __device__ __forceinline__ void copy_units(const T* __restrict__ src, T* __restr
     for (; i < n; i += step) dst[i] = src[i];
 }
 
-__device__ __forceinline__ void copy_span(const VmasCopySpan& s, bool nt = false) {
+__device__ __forceinline__ void copy_span(const VmasCopySpan& s, bool nt, int blk, int nblk) {
     if (s.nbytes == VMAS_COPY_STORE64) {  // a store span: the 8-byte value src at dst
-        if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint64_t*>(s.dst) = (uint64_t)(uintptr_t)s.src;
+        if (blk == 0 && threadIdx.x == 0) *reinterpret_cast<uint64_t*>(s.dst) = (uint64_t)(uintptr_t)s.src;
         return;
     }
     if (!s.src) {  // an increment span: dst[i] += 1.0f
         float* d = reinterpret_cast<float*>(s.dst);
         const int64_t n = s.nbytes / 4;
-        for (int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kCopyThreads)
+        for (int64_t i = (int64_t)blk * kCopyThreads + threadIdx.x; i < n; i += (int64_t)nblk * kCopyThreads)
             d[i] = d[i] + 1.0f;
         return;
     }
     const uintptr_t al = (uintptr_t)s.src | (uintptr_t)s.dst | (uintptr_t)s.nbytes;
     if ((al & 15) == 0 && nt)
-        copy_units<u32x4, true>(reinterpret_cast<const u32x4*>(s.src), reinterpret_cast<u32x4*>(s.dst), s.nbytes / 16);
+        copy_units<u32x4, true>(reinterpret_cast<const u32x4*>(s.src), reinterpret_cast<u32x4*>(s.dst), s.nbytes / 16,
+                                blk, nblk);
     else if ((al & 15) == 0)
-        copy_units(reinterpret_cast<const uint4*>(s.src), reinterpret_cast<uint4*>(s.dst), s.nbytes / 16);
+        copy_units(reinterpret_cast<const uint4*>(s.src), reinterpret_cast<uint4*>(s.dst), s.nbytes / 16, blk, nblk);
     else if ((al & 3) == 0)
-        copy_units(reinterpret_cast<const uint32_t*>(s.src), reinterpret_cast<uint32_t*>(s.dst), s.nbytes / 4);
+        copy_units(reinterpret_cast<const uint32_t*>(s.src), reinterpret_cast<uint32_t*>(s.dst), s.nbytes / 4, blk, nblk);
     else
-        copy_units(reinterpret_cast<const uint8_t*>(s.src), reinterpret_cast<uint8_t*>(s.dst), s.nbytes);
+        copy_units(reinterpret_cast<const uint8_t*>(s.src), reinterpret_cast<uint8_t*>(s.dst), s.nbytes, blk, nblk);
 }
 
-__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) { copy_span(a.s[blockIdx.y], a.nt != 0); }
+__global__ void __launch_bounds__(kCopyThreads) k_copy_spans(CopyArgs a) {
+    copy_span(a.s[blockIdx.y], a.nt != 0, (int)blockIdx.x, (int)gridDim.x);
+}
 
-// The post-replay copies and the next step's random-action draw in ONE launch (vmas_copy_spans_draw):
-// blockIdx.y < n_spans copies span y (grid-stride over gridDim.x), the rest draw column
-// y - n_spans with torch's grid of gx_draw blocks (blocks beyond it leave).
+// The post-replay copies and the next step's random-action draw in ONE launch (vmas_copy_spans_draw).
+// Packed grid (default): item y (span y < n_spans, else draw column y - n_spans) owns the 1-D
+// workgroups [first[y], first[y + 1]) -- a copy span as many as its bytes need (<= 1024), a column
+// exactly torch's gx_draw -- so no workgroup is launched only to leave (the 2-D grid of
+// max(copy, draw) x items launched ~10 000 of them per step for ~1 000 that work).  VMAS_COPY_PACKED=0:
+// the 2-D grid (blockIdx.y = item, blocks beyond the item's share leave; an A/B knob).
 constexpr int kMergedSpans = 96, kMergedCols = 16;
 struct CopyDrawArgs {
     VmasCopySpan s[kMergedSpans];
@@ -80,20 +88,36 @@ struct CopyDrawArgs {
     unsigned long long seed;
     long long numel, snap;
     const unsigned long long* off_dev;  // (non-null: the columns' offsets are relative to *off_dev)
-    int n_spans, gx_draw, mode, pad;
+    int n_spans, gx_draw, mode, n_items;
+    int first[kMergedSpans + kMergedCols + 1];  // packed grid: the items' first workgroups (n_items + 1)
+    int gx_copy, packed;
 };
 static_assert(sizeof(CopyDrawArgs) <= 4096, "kernel argument block");
 
 __global__ void __launch_bounds__(kCopyThreads) k_copy_draw(CopyDrawArgs a) {
-    const int y = (int)blockIdx.y;
+    int y, blk;
+    if (a.packed) {  // the item owning this workgroup: the last y with first[y] <= blockIdx.x
+        const int bx = (int)blockIdx.x;
+        int lo = 0, hi = a.n_items - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.first[mid] <= bx) lo = mid;
+            else hi = mid - 1;
+        }
+        y = lo;
+        blk = bx - a.first[y];
+    } else {
+        y = (int)blockIdx.y;
+        blk = (int)blockIdx.x;
+        if (y < a.n_spans ? blk >= a.gx_copy : blk >= a.gx_draw) return;
+    }
     if (y < a.n_spans) {
-        copy_span(a.s[y]);
+        copy_span(a.s[y], false, blk, a.packed ? a.first[y + 1] - a.first[y] : a.gx_copy);
         return;
     }
-    if ((int)blockIdx.x >= a.gx_draw) return;
     VmasUniformColumn col = a.c[y - a.n_spans];
     if (a.off_dev) col.offset += *a.off_dev;  // (the generator offset a device launch left: see the ABI)
-    vmas_uniform::draw_column(col, a.seed, a.numel, a.snap, a.mode, a.gx_draw, (int)blockIdx.x);
+    vmas_uniform::draw_column(col, a.seed, a.numel, a.snap, a.mode, a.gx_draw, blk);
 }
 
 constexpr int kFillThreads = 256;
@@ -187,8 +211,38 @@ extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* span
     a.mode = mode;
     const int64_t per_block = (int64_t)kCopyThreads * kCopyUnroll;
     const int gx_copy = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (most + per_block - 1) / per_block));
-    hipLaunchKernelGGL(k_copy_draw, dim3((unsigned)std::max(gx_copy, gx_draw), n + n_cols), dim3(kCopyThreads), 0,
-                       (hipStream_t)stream, a);
+    static const int packed = !(getenv("VMAS_COPY_PACKED") && getenv("VMAS_COPY_PACKED")[0] == '0');
+    a.gx_copy = gx_copy;
+    a.packed = packed;
+    a.n_items = n + n_cols;
+    int total = 0;
+    for (int y = 0; y < n + n_cols; ++y) {
+        a.first[y] = total;
+        if (y < n) {  // a span's own share: its 16-byte units over 256 threads x 4, at least one
+            const VmasCopySpan& sp = a.s[y];
+            const int64_t units = sp.nbytes > 0 ? (sp.nbytes + 15) / 16 : 1;
+            total += (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (units + per_block - 1) / per_block));
+        } else {
+            total += gx_draw;
+        }
+    }
+    a.first[n + n_cols] = total;
+    static int trace = getenv("VMAS_COPY_TRACE") ? atoi(getenv("VMAS_COPY_TRACE")) : 0;
+    if (trace > 0) {  // (a diagnostic: the first calls' span list, to stderr)
+        --trace;
+        int64_t bytes = 0;
+        for (int i = 0; i < n; ++i) bytes += a.s[i].nbytes > 0 ? a.s[i].nbytes : 0;
+        fprintf(stderr, "[vmas_copy_spans_draw] spans %d cols %d numel %lld bytes %lld grid %d x %d (copy %d draw %d) packed %d\n",
+                n, n_cols, (long long)numel, (long long)bytes, std::max(gx_copy, gx_draw), n + n_cols, gx_copy, gx_draw,
+                total);
+        for (int i = 0; i < n; ++i)
+            fprintf(stderr, "  span %d: %lld bytes%s\n", i, (long long)a.s[i].nbytes, a.s[i].src ? "" : " (increment)");
+    }
+    if (packed)
+        hipLaunchKernelGGL(k_copy_draw, dim3((unsigned)total), dim3(kCopyThreads), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(k_copy_draw, dim3((unsigned)std::max(gx_copy, gx_draw), n + n_cols), dim3(kCopyThreads), 0,
+                           (hipStream_t)stream, a);
     VMAS_AUX_HIP(hipGetLastError());
     *increment = inc * (unsigned long long)n_cols;
     return VMAS_OK;

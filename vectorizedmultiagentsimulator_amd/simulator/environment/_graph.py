@@ -90,6 +90,25 @@ def _tracked_objects(env) -> List[Any]:
     return out
 
 
+def _own_scenario(scenario) -> bool:
+    """The scenario is one of this package's own classes, unmodified (its make_world defined in
+    the class itself, in a file of the package's scenarios directory): only then does the step's
+    code hold the contracts DirectOutputs and the write-only attributes rely on.  (make_env loads
+    scenario modules afresh, without a package name: by source file.)"""
+    scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                           "scenarios") + os.sep
+    cls = type(scenario)
+    return (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
+            and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir))
+
+
+def _write_only(o, k: str) -> bool:
+    """Attribute k of o is declared write-only within a step by o's own class (not inherited: a
+    subclass may read it): `_vmas_graph_write_only`, a set of attribute names each step re-binds
+    before anything in the step reads it.  The replays then need no carry of its previous value."""
+    return k in type(o).__dict__.get("_vmas_graph_write_only", ())
+
+
 def _host_rng_states():
     return torch.random.get_rng_state(), np.random.get_state(), random.getstate()
 
@@ -401,12 +420,7 @@ class DirectOutputs:
 
     def finalize(self, out_tensors, scenario) -> None:
         """Which categories the replays relocate (see the class notes)."""
-        # (make_env loads scenario modules afresh, without a package name: by source file)
-        scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-                               "scenarios") + os.sep
-        cls = type(scenario)
-        own = (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
-               and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir))
+        own = _own_scenario(scenario)
         ids = {id(t) for t in out_tensors}
         self.enabled = [r for r in self.regions
                         if own and r["buf"]._version == 0 and all(id(m) in ids for m in r["members"])]
@@ -546,6 +560,7 @@ class StepGraph:
         self._first_replay = True
         self._asserts: Optional[_DeviceAsserts] = None
         self._inplace: List[Tensor] = []
+        self._write_only_ys: List[Tensor] = []  # (re-bound, not carried: _write_only)
         self._bk_src: List[Tensor] = []
         self._bk_dst: List[Tensor] = []
         self._bk_u: Optional[Tensor] = None
@@ -868,6 +883,8 @@ class StepGraph:
             if self._direct is not None:
                 self._direct.arm(N.stream_ptr(self._dev_index()))
             self._inplace = [t for t, v in versions.values() if t._version != v]
+            ids = {id(t) for t in self._inplace}
+            self._inplace += [y for y in self._write_only_ys if id(y) not in ids]
             self._bk_src: List[Tensor] = []
             self._bk_dst: List[Tensor] = []
             self._bk_u = None
@@ -935,6 +952,10 @@ class StepGraph:
         carry: List[Tuple[Tensor, Tensor]] = []
         names: List[str] = []
         fresh = []  # carried entity-state attributes: re-bound to fresh tensors on first use (_FreshState)
+        # re-bound attributes no step reads before re-binding them (the package's own scenarios and
+        # sensors declare them): not carried; a rollback restores them from the backups (_inplace)
+        own = self._WRITE_ONLY and _own_scenario(self.env.scenario)
+        self._write_only_ys = []
         for o, before in snap:
             after = o.__dict__
             for k, v0 in before.items():
@@ -949,6 +970,9 @@ class StepGraph:
                 if (_storage_key(v1) == _storage_key(v0) and v1.storage_offset() == v0.storage_offset()
                         and v1.stride() == v0.stride()):
                     continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
+                if own and _write_only(o, k):  # (no step reads X: Y needs no carry, see _write_only)
+                    self._write_only_ys.append(v1)
+                    continue
                 carry.append((v0, v1))
                 names.append(f"{type(o).__name__}.{k}")
                 if k in _STATE_KEYS and hasattr(type(o), "_fresh"):  # (an EntityState / AgentState)
@@ -1045,6 +1069,8 @@ class StepGraph:
     # fresh entity-state tensors on first use after each replay (_FreshState); 0: the states stay
     # views of the graph's buffers (an alias kept across a step then sees later steps' values)
     _FRESH_STATES = os.environ.get("VMAS_GRAPH_FRESH_STATES", "1") != "0"
+    # declared write-only attributes (_write_only) are not carried between replays; 0: carried
+    _WRITE_ONLY = os.environ.get("VMAS_GRAPH_WRITE_ONLY", "1") != "0"
 
     def _replay(self):
         asserts = self._asserts is not None and bool(self._asserts.msgs)

@@ -41,6 +41,10 @@ class Sensor(ABC):
 
 
 class Lidar(Sensor):
+    # graph mode (environment/_graph.py _write_only): measure() re-binds the measurement and nothing
+    # of this class reads the previous one, so replays of a step do not carry it forward
+    _vmas_graph_write_only = frozenset({"_last_measurement"})
+
     def __init__(
         self,
         world: "World",
