@@ -212,6 +212,10 @@ extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* span
     const int64_t per_block = (int64_t)kCopyThreads * kCopyUnroll;
     const int gx_copy = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (most + per_block - 1) / per_block));
     static const int packed = !(getenv("VMAS_COPY_PACKED") && getenv("VMAS_COPY_PACKED")[0] == '0');
+    // packed grid: 16-byte units per thread a span's share is sized for (VMAS_COPY_UNITS, an A/B
+    // knob: 1 = four times the workgroups, each thread one load in flight)
+    static const int units_per_thread = getenv("VMAS_COPY_UNITS") ? std::max(1, std::min(kCopyUnroll, atoi(getenv("VMAS_COPY_UNITS")))) : kCopyUnroll;
+    const int64_t per_share = (int64_t)kCopyThreads * units_per_thread;
     a.gx_copy = gx_copy;
     a.packed = packed;
     a.n_items = n + n_cols;
@@ -221,7 +225,7 @@ extern "C" int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* span
         if (y < n) {  // a span's own share: its 16-byte units over 256 threads x 4, at least one
             const VmasCopySpan& sp = a.s[y];
             const int64_t units = sp.nbytes > 0 ? (sp.nbytes + 15) / 16 : 1;
-            total += (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (units + per_block - 1) / per_block));
+            total += (int)std::max<int64_t>(1, std::min<int64_t>(kMaxCopyBlocks, (units + per_share - 1) / per_share));
         } else {
             total += gx_draw;
         }
