@@ -41,3 +41,63 @@ def test_increment_span_needs_aligned_floats_gpu(gpu_device):
         N.copy_raw(0, [(0, t.data_ptr(), 6)], N.stream_ptr(0))  # not a whole number of floats
     with pytest.raises(N.NativeLibraryError):
         N.copy_raw(0, [(0, t.data_ptr() + 2, 8)], N.stream_ptr(0))  # not 4-byte aligned
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numel", [1000, 32768])
+def test_copy_spans_draw_matches_copies_and_the_standalone_draw_gpu(gpu_device, numel):
+    """vmas_copy_spans_draw (the post-replay launch with the next step's draw, on its packed 1-D
+    grid: each item's own share of workgroups): copies of every alignment class and size, an
+    increment span, a store span, and uniform columns equal to vmas_uniform_columns' draw at the
+    same generator state -- also at an offset read from the device (offset_dev)."""
+    import ctypes
+
+    import numpy as np
+
+    lib = N.load_library()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    srcs, dsts, spans = [], [], []
+    for i in range(60):
+        nbytes = int(torch.randint(1, 300000 if i % 7 == 0 else 5000, (1,), generator=g))
+        off = int(torch.randint(0, 4, (1,), generator=g)) if i % 3 == 0 else 0
+        src = torch.randint(0, 256, (nbytes + off,), dtype=torch.uint8, generator=g).to(gpu_device)
+        dst = torch.zeros(nbytes + off, dtype=torch.uint8, device=gpu_device)
+        srcs.append((src, off, nbytes))
+        dsts.append(dst)
+        spans.append((src.data_ptr() + off, dst.data_ptr() + off, nbytes))
+    steps = torch.arange(3000, dtype=torch.float32, device=gpu_device)
+    spans.append((0, steps.data_ptr(), steps.numel() * 4))  # increment span
+    word = torch.zeros(1, dtype=torch.int64, device=gpu_device)
+    spans.append((0x123456789A, word.data_ptr(), N.VMAS_COPY_STORE64))  # store span
+    tbl = np.zeros(len(spans), dtype=N.COPY_SPAN_DTYPE)
+    for k, s in enumerate(spans):
+        tbl[k] = s
+
+    def columns(n_cols, out):
+        cols = np.zeros(n_cols, dtype=N.UNIFORM_COLUMN_DTYPE)
+        for k in range(n_cols):
+            cols[k]["out"], cols[k]["stride"] = out[k].data_ptr(), 1
+            cols[k]["from_"], cols[k]["to"] = -1.0 - 0.25 * k, 1.0 + 0.5 * k
+        return cols
+
+    n_cols, seed, offset, mode = 6, 1234, 40, 0
+    got = torch.full((n_cols, numel), float("nan"), device=gpu_device)
+    want = torch.full((n_cols, numel), float("nan"), device=gpu_device)
+    inc, inc2 = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    cg, cw = columns(n_cols, got), columns(n_cols, want)
+    off_dev = torch.tensor([offset], dtype=torch.int64, device=gpu_device)
+    for dev_off in (False, True):
+        rc = lib.vmas_copy_spans_draw(0, tbl.ctypes.data, len(spans), numel, cg.ctypes.data, n_cols, seed,
+                                      0 if dev_off else offset, off_dev.data_ptr() if dev_off else None, mode, 0,
+                                      ctypes.byref(inc), N.stream_ptr(0))
+        assert rc == 0, lib.vmas_aux_last_error()
+        assert lib.vmas_uniform_columns(0, numel, cw.ctypes.data, n_cols, seed, offset, mode, ctypes.byref(inc2),
+                                        N.stream_ptr(0)) == 0
+        torch.cuda.synchronize()
+        assert inc.value == inc2.value
+        assert torch.equal(got, want), (dev_off, (got - want).abs().max().item())
+    for (src, off, nbytes), dst in zip(srcs, dsts):
+        assert torch.equal(dst[off:off + nbytes], src[off:off + nbytes])
+        assert not dst[:off].any()
+    assert torch.equal(steps, torch.arange(3000, dtype=torch.float32, device=gpu_device) + 2.0)  # (two launches)
+    assert int(word.item()) == 0x123456789A

@@ -26,6 +26,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -57,6 +58,10 @@ struct Group {
     int64_t r0 = 0;
     std::vector<int64_t> row_members;  // member index of each table row r0, r0 + 1, ...
     int64_t member_bytes = 0;
+    // one allocation per step (OutputAlloc::one_): this group's byte offset in it, a member's sizes
+    // and (contiguous) strides
+    int64_t off = 0;
+    std::vector<int64_t> msizes, mstrides;
 };
 
 // One directly written category: the captured buffer's address, the buffer the next replay writes
@@ -71,6 +76,7 @@ struct Region {
     std::vector<int64_t> offsets;
     py::list box;
     at::Tensor pending;
+    int64_t off = 0;  // (one allocation per step: the next buffer's byte offset in it)
 };
 
 class OutputAlloc {
@@ -113,9 +119,25 @@ public:
             gr.member_bytes = numel * (int64_t)c10::elementSize(gr.dtype);
             gr.shape.push_back(gr.n);
             gr.shape.insert(gr.shape.end(), shape.begin(), shape.end());
+            gr.msizes = shape;
+            gr.mstrides.assign(shape.size(), 1);
+            for (int64_t d = (int64_t)shape.size() - 2; d >= 0; --d) gr.mstrides[d] = gr.mstrides[d + 1] * shape[d + 1];
             groups_.push_back(std::move(gr));
         }
         opts_ = at::TensorOptions().device(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+        // the step's fresh outputs and the next direct buffers in ONE allocation (one caching-
+        // allocator call per step instead of one per group and region); VMAS_HOST_ONE_ALLOC=0: one each
+        static const bool one = !(getenv("VMAS_HOST_ONE_ALLOC") && getenv("VMAS_HOST_ONE_ALLOC")[0] == '0');
+        one_ = one;
+        constexpr int64_t kAlign = 256;
+        for (Group& g : groups_) {
+            g.off = total_;
+            total_ += (g.n * g.member_bytes + kAlign - 1) / kAlign * kAlign;
+        }
+        for (Region& r : regions_) {
+            r.off = total_;
+            total_ += (r.nbytes + kAlign - 1) / kAlign * kAlign;
+        }
     }
 
     // Fresh tensors of every group (in group order, members in order), their addresses written
@@ -124,6 +146,26 @@ public:
     std::vector<at::Tensor> alloc() {
         std::vector<at::Tensor> out;
         out.reserve(count());
+        if (one_ && total_ > 0) {
+            at::Tensor big = at::empty({total_}, opts_.dtype(at::kByte));
+            const uintptr_t b0 = (uintptr_t)big.data_ptr();
+            for (const Group& g : groups_) {
+                for (size_t r = 0; r < g.row_members.size(); ++r)
+                    tbl_[g.r0 + (int64_t)r].dst = (void*)(b0 + (uintptr_t)(g.off + g.row_members[r] * g.member_bytes));
+                const int64_t es = (int64_t)c10::elementSize(g.dtype), e0 = g.off / es, en = g.member_bytes / es;
+                at::Tensor typed = big.view(g.dtype);
+                for (int64_t k = 0; k < g.n; ++k) out.push_back(typed.as_strided(g.msizes, g.mstrides, e0 + k * en));
+            }
+            for (Region& r : regions_) {
+                at::Tensor typed = r.box[0].cast<at::Tensor>().view(r.dtype);
+                const int64_t so = typed.storage_offset();  // (as_strided's offset is the storage's)
+                for (size_t m = 0; m < r.offsets.size(); ++m)
+                    out.push_back(typed.as_strided(r.sizes[m], r.strides[m], so + r.offsets[m]));
+                r.pending = big.narrow(0, r.off, r.nbytes);
+                tbl_[r.row].src = (const void*)(b0 + (uintptr_t)r.off - r.base);
+            }
+            return out;
+        }
         for (const Group& g : groups_) {
             at::Tensor buf = at::empty(g.shape, opts_.dtype(g.dtype));
             const uintptr_t base = (uintptr_t)buf.data_ptr();
@@ -133,8 +175,9 @@ public:
         }
         for (Region& r : regions_) {
             at::Tensor typed = r.box[0].cast<at::Tensor>().view(r.dtype);
+            const int64_t so = typed.storage_offset();
             for (size_t m = 0; m < r.offsets.size(); ++m)
-                out.push_back(typed.as_strided(r.sizes[m], r.strides[m], r.offsets[m]));
+                out.push_back(typed.as_strided(r.sizes[m], r.strides[m], so + r.offsets[m]));
             r.pending = at::empty({r.nbytes}, opts_.dtype(at::kByte));
             tbl_[r.row].src = (const void*)((uintptr_t)r.pending.data_ptr() - r.base);
         }
@@ -190,6 +233,8 @@ private:
     std::vector<Group> groups_;
     std::vector<Region> regions_;
     at::TensorOptions opts_;
+    bool one_ = true;
+    int64_t total_ = 0;
 };
 
 class UniformDraw {
