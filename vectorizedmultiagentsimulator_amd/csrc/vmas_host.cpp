@@ -25,7 +25,9 @@
 #include <ATen/hip/HIPGeneratorImpl.h>
 #include <c10/hip/HIPStream.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <stdexcept>
@@ -326,10 +328,31 @@ private:
 // drawn per-agent tensors, snapshot, seed, offset, increment).  off_dev (a device address, 0:
 // none): the draw's generator offset is read there when the launch runs (a spawn launch earlier on
 // the stream leaves it); the returned offset is then None.
+// VMAS_HOST_TIMING=1 (a diagnostic): post_draw's phases timed on the host, means to stderr at exit
+struct HostTiming {
+    bool on = getenv("VMAS_HOST_TIMING") && getenv("VMAS_HOST_TIMING")[0] == '1';
+    double ns[5] = {0, 0, 0, 0, 0};
+    long calls = 0;
+    ~HostTiming() {
+        if (on && calls)
+            fprintf(stderr, "[post_draw] %ld calls, us per call: alloc %.2f prepare %.2f launch %.2f commit %.2f tuple %.2f\n",
+                    calls, ns[0] / calls / 1e3, ns[1] / calls / 1e3, ns[2] / calls / 1e3, ns[3] / calls / 1e3,
+                    ns[4] / calls / 1e3);
+    }
+};
+HostTiming g_timing;
+inline double now_ns() {
+    return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, int64_t snap_base, int64_t snap_numel,
                     int64_t copy_draw_fn, int64_t off_dev) {
+    const bool tm = g_timing.on;
+    double t0 = tm ? now_ns() : 0.0, t1 = 0.0;
     std::vector<at::Tensor> outs = oa.alloc();
+    if (tm) g_timing.ns[0] += (t1 = now_ns()) - t0;
     auto [acts, snap, delta] = d.prepare(snap_base, snap_numel);
+    if (tm) g_timing.ns[1] += (t0 = now_ns()) - t1;
     if (mid > 0) oa.launch(0, mid);
     const int64_t lo = mid > 0 ? mid : 0;
     at::Generator gen = at::cuda::detail::getDefaultCUDAGenerator((c10::DeviceIndex)d.device());
@@ -345,8 +368,15 @@ py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, in
                                                        (const uint64_t*)off_dev, d.mode(), delta, &inc,
                                                        current_stream(d.device()));
     if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
+    if (tm) g_timing.ns[2] += (t1 = now_ns()) - t0;
     oa.commit();
-    return py::make_tuple(outs, acts, snap, seed, off_dev ? py::object(py::none()) : py::object(py::int_(off)), inc);
+    if (tm) g_timing.ns[3] += (t0 = now_ns()) - t1;
+    py::tuple res = py::make_tuple(outs, acts, snap, seed, off_dev ? py::object(py::none()) : py::object(py::int_(off)), inc);
+    if (tm) {
+        g_timing.ns[4] += now_ns() - t0;
+        ++g_timing.calls;
+    }
+    return res;
 }
 
 // (tensor._version of each, as a tuple: the version snapshots of the post-replay bookkeeping)

@@ -125,6 +125,19 @@ class _ActionShadow:
         return v[1]
 
 
+def _plain_accessors(agent_cls, action_cls) -> bool:
+    """The agent / action classes read `action`, `silent`, `batch_dim` and `u_range` through the
+    core classes' own properties (which return `_action`, `_silent`, `_batch_dim`, `_u_range`) and
+    keep `action_size` a plain attribute."""
+    from ..core import Action
+
+    bd = getattr(agent_cls, "batch_dim", None)
+    return (getattr(agent_cls, "action", None) is Agent.action and getattr(agent_cls, "silent", None) is Agent.silent
+            and isinstance(bd, property) and bd.fget is TorchVectorizedObject.batch_dim.fget
+            and not hasattr(agent_cls, "action_size")
+            and getattr(action_cls, "u_range", None) is Action.u_range)
+
+
 class Environment(TorchVectorizedObject):
     metadata = {"render.modes": ["human", "rgb_array"], "runtime.vectorized": True}
     vmas_random_state = [torch.random.get_rng_state(), np.random.get_state(), random.getstate()]
@@ -750,13 +763,23 @@ class Environment(TorchVectorizedObject):
             if type(ur) not in (float, int):
                 return None
             sig.append((a, act, ur, a.silent, a.action_size, a.batch_dim))
+        # plain: every agent and action of the core classes' accessors (the properties only return
+        # the underscored fields), so _uniform_same may read the fields without a Python frame each
+        plain = all(_plain_accessors(type(a), type(a.action)) for a in self.agents)
         # the device the plan draws on (env.to(...) moves the world and its agents)
-        return (self.world.dim_c, sig, self.world.device, self.world.batch_dim)
+        return (self.world.dim_c, sig, self.world.device, self.world.batch_dim, plain)
 
     def _uniform_same(self, sig) -> bool:
         if (sig is None or sig[0] != self.world.dim_c or len(sig[1]) != len(self.agents)
                 or sig[2] != self.world.device or sig[3] != self.world.batch_dim):
             return False
+        if sig[4]:  # (every draw and every post-replay launch asks: the fields directly)
+            for a, (ag, act, ur, sil, asz, bd) in zip(self.agents, sig[1]):
+                d = a.__dict__
+                if (a is not ag or d.get("_action") is not act or act.__dict__.get("_u_range") is not ur
+                        or d.get("_silent") is not sil or d.get("action_size") != asz or d.get("_batch_dim") != bd):
+                    return False
+            return True
         for a, (ag, act, ur, sil, asz, bd) in zip(self.agents, sig[1]):
             if (a is not ag or a.action is not act or act.u_range is not ur or a.silent is not sil
                     or a.action_size != asz or a.batch_dim != bd):
