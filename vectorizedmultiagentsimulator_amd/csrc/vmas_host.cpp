@@ -51,6 +51,25 @@ void* current_stream(int device) {
     return (void*)c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
 }
 
+// A tensor over `base`'s storage with its own dtype, sizes, strides and (storage) offset: what
+// as_strided / select return, without a dispatcher round trip and autograd's view bookkeeping
+// (~0.4 us each, tens per step: post_draw's profile).  The step's outputs are fresh
+// non-differentiable tensors, as the reference's are, not views of anything a caller holds.
+// VMAS_HOST_RAW_VIEWS=0: as_strided / select (an A/B knob).
+bool raw_views() {
+    static const bool on = !(getenv("VMAS_HOST_RAW_VIEWS") && getenv("VMAS_HOST_RAW_VIEWS")[0] == '0');
+    return on;
+}
+
+at::Tensor storage_view(const at::Tensor& base, at::ScalarType dtype, at::IntArrayRef sizes, at::IntArrayRef strides,
+                        int64_t offset) {
+    if (!raw_views() || base.requires_grad()) return base.view(dtype).as_strided(sizes, strides, offset);
+    auto impl = c10::make_intrusive<c10::TensorImpl>(c10::Storage(base.storage()), base.key_set(),
+                                                     caffe2::TypeMeta::fromScalarType(dtype));
+    impl->set_sizes_and_strides(sizes, strides, offset);
+    return at::Tensor(std::move(impl));
+}
+
 // One (dtype, shape) group of a step's outputs: `n` tensors of `shape`, allocated as [n, *shape];
 // members `contig[k]` get table row r0 + (their rank among the contiguous members).
 struct Group {
@@ -155,14 +174,13 @@ public:
                 for (size_t r = 0; r < g.row_members.size(); ++r)
                     tbl_[g.r0 + (int64_t)r].dst = (void*)(b0 + (uintptr_t)(g.off + g.row_members[r] * g.member_bytes));
                 const int64_t es = (int64_t)c10::elementSize(g.dtype), e0 = g.off / es, en = g.member_bytes / es;
-                at::Tensor typed = big.view(g.dtype);
-                for (int64_t k = 0; k < g.n; ++k) out.push_back(typed.as_strided(g.msizes, g.mstrides, e0 + k * en));
+                for (int64_t k = 0; k < g.n; ++k) out.push_back(storage_view(big, g.dtype, g.msizes, g.mstrides, e0 + k * en));
             }
             for (Region& r : regions_) {
-                at::Tensor typed = r.box[0].cast<at::Tensor>().view(r.dtype);
-                const int64_t so = typed.storage_offset();  // (as_strided's offset is the storage's)
+                at::Tensor box = r.box[0].cast<at::Tensor>();  // (a byte tensor: its offset in bytes)
+                const int64_t es = (int64_t)c10::elementSize(r.dtype), so = box.storage_offset() / es;
                 for (size_t m = 0; m < r.offsets.size(); ++m)
-                    out.push_back(typed.as_strided(r.sizes[m], r.strides[m], so + r.offsets[m]));
+                    out.push_back(storage_view(box, r.dtype, r.sizes[m], r.strides[m], so + r.offsets[m]));
                 r.pending = big.narrow(0, r.off, r.nbytes);
                 tbl_[r.row].src = (const void*)(b0 + (uintptr_t)r.off - r.base);
             }
@@ -278,10 +296,7 @@ public:
                 throw std::runtime_error(std::string("vmas_uniform_columns failed: ") + last_error_());
             impl->set_offset(off + inc);
         }
-        std::vector<at::Tensor> out;
-        out.reserve(n_agents_);
-        for (int64_t a = 0; a < n_agents_; ++a) out.push_back(buf.select(0, a));
-        return {std::move(out), std::move(snap)};
+        return {agents(buf), std::move(snap)};
     }
 
     // The draw's buffers and column table without the launch (a speculative draw merged into the
@@ -297,10 +312,16 @@ public:
             snap = at::empty({snap_numel}, opts_);
             delta = (int64_t)((uintptr_t)snap->data_ptr() - (uintptr_t)snap_base);
         }
+        return {agents(buf), std::move(snap), delta};
+    }
+
+    // the [A, B, n] buffer's per-agent [B, n] tensors
+    std::vector<at::Tensor> agents(const at::Tensor& buf) const {
         std::vector<at::Tensor> out;
         out.reserve(n_agents_);
-        for (int64_t a = 0; a < n_agents_; ++a) out.push_back(buf.select(0, a));
-        return {std::move(out), std::move(snap), delta};
+        const std::vector<int64_t> sizes{batch_, width_}, strides{width_, 1};
+        for (int64_t a = 0; a < n_agents_; ++a) out.push_back(storage_view(buf, at::kFloat, sizes, strides, a * batch_ * width_));
+        return out;
     }
 
     int device() const { return device_; }
