@@ -180,7 +180,11 @@ __global__ void __launch_bounds__(256) k_assert_publish(const uint8_t* cond, int
 // kernels and a publish).  Workgroups OR their verdict into the slot's work line and arrive on
 // its counter; the last one publishes and clears the line for the next launch.  (One 1024-thread
 // workgroup over the 65 536 elements of flocking's target took 30 us.)
-constexpr int kRangeThreads = 256, kRangePerThread = 8;
+// (4 elements per thread, 32-bit index math where the element count fits: the grid-stride loop's
+// serial chain of 64-bit divisions, not the bytes, set this kernel's ~6 us at flocking's 65 536
+// elements with 8 per thread; more workgroups would add arrivals on the one counter line)
+constexpr int kRangeThreads = 256, kRangePerThread = 4;
+template <typename I>
 __global__ void __launch_bounds__(kRangeThreads) k_assert_range(const float* u, int64_t s0, int64_t s1, int batch, int n,
                                                                 const float* mult, const float* range, uint32_t* epoch,
                                                                 uint64_t* hsig, uint32_t* work) {
@@ -189,11 +193,11 @@ __global__ void __launch_bounds__(kRangeThreads) k_assert_range(const float* u, 
     if (threadIdx.x == 0) bad = 0u;
     __syncthreads();
     bool mine = false;
-    const int64_t total = (int64_t)batch * n, step = (int64_t)gridDim.x * kRangeThreads;
-    for (int64_t i = (int64_t)blockIdx.x * kRangeThreads + threadIdx.x; i < total; i += step) {
-        const int64_t b = i / n;
-        const int c = (int)(i - b * n);
-        const float x = u[b * s0 + (int64_t)c * s1];
+    const I total = (I)batch * (I)n, step = (I)gridDim.x * kRangeThreads;
+    for (I i = (I)blockIdx.x * kRangeThreads + (I)threadIdx.x; i < total; i += step) {
+        const I b = i / (I)n;
+        const int c = (int)(i - b * (I)n);
+        const float x = u[(int64_t)b * s0 + (int64_t)c * s1];
         mine |= !(fabsf(x / mult[c]) <= range[c]);  // (NaN fails, as torch's comparison)
     }
     const bool wave_bad = __any(mine);  // (every lane takes part in the vote)
@@ -425,8 +429,12 @@ int32_t vmas_assert_publish_range(VmasDeviceAssert* ch, int32_t slot, const floa
     const int64_t total = (int64_t)batch * n;
     const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (total + kRangeThreads * kRangePerThread - 1) /
                                                                           (kRangeThreads * kRangePerThread)));
-    hipLaunchKernelGGL(k_assert_range, dim3(gx), dim3(kRangeThreads), 0, (hipStream_t)stream, u, s0, s1, batch, n, mult,
-                       range, ch->epoch + slot, ch->dsig + slot, ch->work + 32 * slot);
+    if (total + (int64_t)gx * kRangeThreads < ((int64_t)1 << 31))
+        hipLaunchKernelGGL(k_assert_range<int32_t>, dim3(gx), dim3(kRangeThreads), 0, (hipStream_t)stream, u, s0, s1, batch,
+                           n, mult, range, ch->epoch + slot, ch->dsig + slot, ch->work + 32 * slot);
+    else
+        hipLaunchKernelGGL(k_assert_range<int64_t>, dim3(gx), dim3(kRangeThreads), 0, (hipStream_t)stream, u, s0, s1, batch,
+                           n, mult, range, ch->epoch + slot, ch->dsig + slot, ch->work + 32 * slot);
     VMAS_AUX_HIP(hipGetLastError());
     return VMAS_OK;
 }
