@@ -229,3 +229,30 @@ def test_uniform_signature_sees_every_field_it_keys_on():
     assert not sig2[4] and env._uniform_same(sig2)
     a.action.__dict__["_u_range"] = 0.25
     assert not env._uniform_same(sig2)
+
+
+def test_write_only_declarations_are_not_inherited():
+    """Graph mode leaves out of the post-replay carry only the attributes a class declares in its
+    own `_vmas_graph_write_only` (environment/_graph.py _write_only): a subclass, which may read
+    them, has to declare them again; and only the package's own scenario classes are trusted."""
+    from vectorizedmultiagentsimulator_amd import make_env
+    from vectorizedmultiagentsimulator_amd.simulator.environment._graph import _own_scenario, _write_only
+    from vectorizedmultiagentsimulator_amd.simulator.sensors import Lidar
+
+    env = make_env("discovery", num_envs=2, device="cpu", seed=0, n_agents=2)
+    lid = env.agents[0].sensors[0]
+    assert type(lid) is Lidar and _write_only(lid, "_last_measurement")
+    assert not _write_only(lid, "_angles")
+    sc = env.scenario
+    assert _own_scenario(sc) and _write_only(sc, "covered_targets") and not _write_only(sc, "all_time_covered_targets")
+
+    class MyLidar(Lidar):
+        pass
+
+    class Scenario(type(sc)):  # a user's subclass: same name, the package's make_world inherited
+        pass
+
+    lid.__class__ = MyLidar
+    assert not _write_only(lid, "_last_measurement")
+    sc.__class__ = Scenario
+    assert not _own_scenario(sc) and not _write_only(sc, "covered_targets")
