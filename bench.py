@@ -368,10 +368,19 @@ def main():
             "lidar_rays_per_env": lidar_rays(world),
             "timer": prog_timer,
         }
+    group = None
     if dist is not None:
+        # what the live process group saw (not the launcher's environment): its size, backend and
+        # every rank's own rate, gathered once after the timed region
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        ranks = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(ranks, t)
+        per_rank = [args.envs * args.steps / float(r.item()) for r in ranks]
+        elapsed = max(float(r.item()) for r in ranks)
+        group = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                 "per_rank_env_steps_per_s": [round(r, 1) for r in per_rank],
+                 "timing": "max over ranks of each rank's barrier-bracketed wall time"}
+        world_size = dist.get_world_size()
 
     total_envs = args.envs * world_size
     value = total_envs * args.steps / elapsed
@@ -431,8 +440,12 @@ def main():
                 peak_at_clock = 256 * 4 * 0.5 * clock_ghz * 1e9
                 roofline["valu_issue"]["clock_ghz"] = round(clock_ghz, 3)
                 roofline["valu_issue"]["frac_at_clock"] = round(rate / peak_at_clock, 4)
+    if args.scenario == "balance" and args.envs == 32768:
+        metric = "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU"  # BASELINE.json
+    else:
+        metric = f"env-steps/sec (num_envs x steps / wall-s), '{args.scenario}' @{args.envs} envs/GPU"
     out = {
-        "metric": "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world_size,
@@ -458,6 +471,8 @@ def main():
         "roofline": roofline,
         "roofline_program": program,
     }
+    if group is not None:
+        out["process_group"] = group
     if args.scenario == "discovery":  # (respawns the one-launch sampler handed over to the reference loop)
         out["config"]["respawn_handovers"] = {"timed": handovers[0] - h0, "total": handovers[0]}
     if rank == 0 and world_size == 1 and args.cpu_steps > 0:

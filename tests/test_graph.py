@@ -431,6 +431,40 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name
         _assert_same([a.action.u for a in eager.agents], [a.action.u for a in graph.agents], f"u step {t}")
         assert torch.equal(eager.steps, graph.steps), (name, t)
     assert graph.graph_status == "graph", graph.graph_reason
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("other", ["clone", "policy"])
+def test_draw_ahead_dropped_by_caller_actions_gpu(gpu_device, other):
+    """random -> step -> step(caller's own actions) -> random -> step.  The
+    post-replay launch of the second step drew the next actions ahead into the persistent action
+    buffer; the caller's step rewrote that buffer, so the following get_random_actions must not
+    hand out the draw made ahead as pre-applied (its applied values are gone).  Bit-identical to
+    the eager twin at every step."""
+    eager, graph = _twin_envs(gpu_device, "balance", n_agents=4)
+    for t in range(10):
+        s = _rng_save()
+        if t % 3 == 2:  # the caller's own actions: a heuristic-like policy with no device draw
+            if other == "clone":
+                acts = [(a.action.u.clone() / a.action.u_multiplier_tensor).clamp_(-1, 1) for a in eager.agents]
+            else:
+                acts = [torch.full((256, 2), 0.1 * (i + 1), device=gpu_device).clamp_(-1, 1)
+                        for i in range(len(eager.agents))]
+            a_e, a_g = acts, [a.clone() for a in acts]
+        else:
+            a_e = eager.get_random_actions()
+            _rng_load(s)
+            a_g = graph.get_random_actions()
+            _assert_same(a_e, a_g, f"draws step {t}")
+        s = _rng_save()
+        out_e = eager.step(a_e)
+        _rng_load(s)
+        out_g = graph.step(a_g)
+        _assert_same(out_e, out_g, f"{other} outputs step {t}")
+        _assert_same(_state(eager), _state(graph), f"{other} state step {t}")
+        _assert_same([a.action.u for a in eager.agents], [a.action.u for a in graph.agents], f"u step {t}")
+    assert graph.graph_status == "graph", graph.graph_reason
+    assert graph.preapplied_steps > 0
     assert graph.preapplied_steps >= (0 if redo else 5)  # (a redone respawn edits state between steps)
     if name in ("balance", "discovery") and not redo:  # (no device asserts: draws made ahead, handed out)
         assert graph._SPEC_DRAW and getattr(graph, "drawn_ahead", 0) >= 3

@@ -1,0 +1,139 @@
+"""The step's action path and the benchmark scenarios' per-step programs against the CPU oracle
+(oracle/vmas_scenario_oracle.py; VERDICT r4 "Next" #1).
+
+The oracle restates ``Environment._set_action`` / ``Holonomic.process_action`` and each scenario's
+reward / observation / done / info from the reference's files; tests/_scenario_parity.py feeds it
+the product's states and actions step by step and compares u, state.force and every output.
+
+* CPU worlds (no GPU): the product's host path (native host backend + the scenarios' torch
+  programs) against the oracle -- this is what pins the restatement itself;
+* GPU worlds (``-m gpu``): the fused action launch (vmas_apply_actions / the pre-applied draw) and
+  the fused scenario programs (k_balance, k_transport, k_discovery_*_fast, k_flocking_fast) at the
+  BASELINE configs' full sizes, in graph mode (the bench's path) and eagerly; one ``PARITY`` line
+  per config.
+"""
+import pytest
+import torch
+
+from oracle import vmas_scenario_oracle as SO
+from tests._scenario_parity import ScenarioParity
+from vectorizedmultiagentsimulator_amd import make_env
+
+CASES = [
+    ("balance", dict(n_agents=4), 10),
+    ("transport", dict(n_agents=4), None),
+    ("discovery", dict(n_agents=5, use_agent_lidar=True), None),
+    ("flocking", dict(n_agents=5), None),
+]
+
+
+def _make(name, kw, substeps, device, envs, seed=0, **ekw):
+    env = make_env(name, num_envs=envs, device=device, seed=seed, **kw, **ekw)
+    if substeps is not None:
+        env.world._substeps = substeps
+        env.world._sub_dt = env.world._dt / substeps
+    return env
+
+
+def _run(env, name, kw, steps, config, actions=None):
+    sp = ScenarioParity(env, name, kw)
+    for t in range(steps):
+        sp.step(None if actions is None else actions(env, t))
+    rec = sp.record(config)
+    assert sp.ok, (sp.failures[:6], rec)
+    return rec
+
+
+# ---- the oracle's action path on its own (reference semantics) ---------------------------------
+def test_set_action_oracle_semantics():
+    a = torch.tensor([[0.5, -1.0], [1.0, 0.25]])
+    u, c = SO.set_action(a, action_size=2, u_range=1.0, u_multiplier=0.7)
+    assert torch.equal(u, a * torch.tensor([0.7, 0.7])) and c is None
+    with pytest.raises(AssertionError):  # environment.py:653-655
+        SO.set_action(a * 2, action_size=2, u_range=1.0, u_multiplier=0.7)
+    u, _ = SO.set_action(a * 2, action_size=2, u_range=1.0, u_multiplier=0.7, clamp_action=True)
+    assert torch.equal(u, (a * 2).clamp(-1, 1) * 0.7)
+    with pytest.raises(AssertionError):  # 621-623
+        SO.set_action(torch.tensor([[float("nan"), 0.0]]), action_size=2, u_range=1.0, u_multiplier=1.0)
+    # comm actions: clamped into the action, but the range assert reads the unclamped view (643, 739-743)
+    a3 = torch.tensor([[0.5, 0.5, 0.3]])
+    u, c = SO.set_action(a3, action_size=2, u_range=1.0, u_multiplier=1.0, dim_c=1, silent=False)
+    assert torch.equal(c, a3[:, 2:])
+    with pytest.raises(AssertionError):
+        SO.set_action(torch.tensor([[0.5, 0.5, 1.5]]), action_size=2, u_range=1.0, u_multiplier=1.0, dim_c=1,
+                      silent=False, clamp_action=True)
+    assert torch.equal(SO.holonomic_process_action(torch.ones(3, 4)), torch.ones(3, 2))
+    assert torch.equal(SO.lidar_angles(1, 4), torch.linspace(0, 2 * torch.pi, 5)[:4].unsqueeze(0))
+
+
+# ---- CPU worlds: the product's host path vs the oracle -----------------------------------------
+@pytest.mark.parametrize("name,kw,substeps", CASES, ids=[c[0] for c in CASES])
+def test_scenario_programs_match_oracle_cpu(name, kw, substeps):
+    env = _make(name, kw, substeps, "cpu", 96, seed=1)
+    _run(env, name, kw, 6, f"{name} 96 envs cpu")
+
+
+@pytest.mark.parametrize("name,kw,substeps", CASES[:2], ids=[c[0] for c in CASES[:2]])
+def test_clamped_actions_match_oracle_cpu(name, kw, substeps):
+    """clamp_actions=True with actions up to 3x the range (environment.py:635-646)."""
+    env = _make(name, kw, substeps, "cpu", 64, seed=2, clamp_actions=True)
+    g = torch.Generator().manual_seed(0)
+    acts = lambda env, t: [torch.rand(64, 2, generator=g) * 6 - 3 for _ in env.agents]  # noqa: E731
+    _run(env, name, kw, 3, f"{name} 64 envs cpu clamp", actions=acts)
+
+
+@pytest.mark.parametrize("mutation", ["shaping", "u_multiplier", "covering_range"])
+def test_oracle_catches_a_misread_program_cpu(mutation):
+    """The checker is not vacuous: a product program that misreads one constant of the reference
+    (balance's shaping factor, an agent's u_multiplier, discovery's covering range) fails."""
+    name, kw, sub = {"shaping": CASES[0], "u_multiplier": CASES[1], "covering_range": CASES[2]}[mutation]
+    env = _make(name, kw, sub, "cpu", 96, seed=1)
+    sp = ScenarioParity(env, name, kw)
+    if mutation == "shaping":
+        env.scenario.shaping_factor = 99
+    elif mutation == "u_multiplier":
+        # (the product's per-column tensor, not the parameter the oracle reads)
+        env.agents[1].action._u_multiplier_tensor = torch.tensor([0.61, 0.6])
+    else:
+        env.scenario._covering_range = 0.3
+    for _ in range(4):
+        sp.step()
+    assert not sp.ok
+
+
+# ---- GPU worlds: fused actions + fused scenario programs vs the oracle ---------------------------
+FULL = [
+    ("balance", dict(n_agents=4), 10, 32768, "C2"),
+    ("transport", dict(n_agents=4), None, 32768, "C3"),
+    ("discovery", dict(n_agents=8, use_agent_lidar=True), None, 16384, "C4"),
+    ("flocking", dict(n_agents=8), None, 32768, "C5 shard"),
+    ("flocking", dict(n_agents=8), None, 262144, "C5 full"),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps,envs,cfg", FULL, ids=[c[4].replace(" ", "_") for c in FULL])
+def test_scenario_programs_match_oracle_full_size_gpu(gpu_device, name, kw, substeps, envs, cfg):
+    """The bench's path (graph mode: captured step, pre-applied random draws, fused programs with
+    direct outputs) at the BASELINE config's full size: 6 steps (2 eager, capture, replays)."""
+    env = _make(name, kw, substeps, gpu_device, envs, graph_step=True)
+    rec = _run(env, name, kw, 6, f"{cfg} {name} {envs} envs graph: actions + scenario program vs oracle")
+    assert env.graph_status == "graph", env.graph_reason
+    assert rec["lidar"]["uncertified_rows"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps", CASES, ids=[c[0] for c in CASES])
+def test_scenario_programs_match_oracle_eager_gpu(gpu_device, name, kw, substeps):
+    """The eager default (make_env without graph_step): the fused action launch and programs."""
+    env = _make(name, kw, substeps, gpu_device, 4096, seed=4)
+    _run(env, name, kw, 4, f"{name} 4096 envs eager: actions + scenario program vs oracle")
+
+
+@pytest.mark.gpu
+def test_clamped_actions_match_oracle_gpu(gpu_device):
+    env = _make("balance", dict(n_agents=4), 10, gpu_device, 32768, seed=2, clamp_actions=True, graph_step=True)
+    g = torch.Generator().manual_seed(0)
+    acts = lambda env, t: [(torch.rand(32768, 2, generator=g) * 6 - 3).to(gpu_device) for _ in env.agents]  # noqa: E731
+    _run(env, "balance", dict(n_agents=4), 5, "C2 balance 32768 envs graph clamp_actions: actions vs oracle",
+         actions=acts)

@@ -329,6 +329,10 @@ class Environment(TorchVectorizedObject):
         """
         self._ushadow.disarm()  # (the step sets the agents' actions: no snapshot is shown any more)
         self._spec_ok = False
+        # a draw made ahead is handed out only by the get_random_actions right after the step that
+        # made it: one still pending here was never taken, and this step rewrites the buffer it
+        # was applied into
+        self._spec = None
         g = self._graph
         if g is not None and g.graph is not None and self.continuous_actions:
             try:
@@ -950,7 +954,10 @@ class Environment(TorchVectorizedObject):
         (or False) and the caller checks the flags later with _finish_speculative_actions."""
         agents = self.agents
         n = len(agents)
-        self._drawn = None  # (the persistent buffer is rewritten: a draw's applied values are stale)
+        # the persistent buffer is rewritten: a draw's applied values are stale, and so is a draw
+        # made ahead into it (_take_spec would hand out actions whose applied values are gone)
+        self._drawn = None
+        self._spec = None
         self._ushadow.disarm()
         if n == 0:
             return False
