@@ -132,6 +132,17 @@ class ScenarioParity:
                 unc = (rb & ~cert).any(-1)
                 lr["uncertified_rows"] += int(unc.sum())
                 lidar_bad_rows |= unc
+                for b in unc.nonzero().flatten()[:4].tolist():  # what a reader needs to judge the row
+                    r = (rb & ~cert)[b].nonzero().flatten().tolist()
+                    wide = {}
+                    for d in (3e-6, 1e-5, 3e-5, 1e-4):
+                        ok = False
+                        for s in (-d, d):
+                            e3 = ow.cast_rays(ai, rays + s, spec.max_range, spec.entity_filter)[b]
+                            ok |= bool(((g[b] - e3).abs() <= LIDAR_ATOL + LIDAR_RTOL * e3.abs())[r].all())
+                        wide[d] = ok
+                    self.failures.append(("lidar row", self.rec["steps"], k, c0, b, r, g[b, r].tolist(),
+                                          e[b, r].tolist(), rays[b, r].tolist(), wide))
         # the rest of the observations
         assert len(obs) == len(exp["obs"]), (len(obs), len(exp["obs"]))
         for k, (g, e) in enumerate(zip(obs, exp["obs"])):

@@ -40,7 +40,7 @@ def _run(env, name, kw, steps, config, actions=None):
     for t in range(steps):
         sp.step(None if actions is None else actions(env, t))
     rec = sp.record(config)
-    assert sp.ok, (sp.failures[:6], rec)
+    assert sp.ok, f"{sp.failures[:6]!r} {rec!r}"
     return rec
 
 

@@ -22,7 +22,7 @@ rocm-smi --showproductname > "$OUT/gpu_info.log" 2>&1 || true
 lscpu > "$OUT/lscpu.log" 2>&1 || true
 for step in ${SESSION_STEPS:-tests bench prof}; do
   case $step in
-    tests) run pytest_gpu 1100 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+    tests) run pytest_gpu 1100 python -u -m pytest ${TESTS:-tests} -m gpu ${XFLAG--x} -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     bench) run bench 600 python bench.py --steps "$STEPS" --warmup 10 ;;
     benchdef) run bench_default 600 python bench.py ;;
@@ -32,7 +32,9 @@ for step in ${SESSION_STEPS:-tests bench prof}; do
     bench_c5full) run bench_c5full 600 python bench.py --scenario flocking --envs 262144 --steps 50 --warmup 10 --cpu-steps 0 ;;
     bench_eager) run bench_eager 600 python bench.py --graph off --steps "$STEPS" --warmup 10 --cpu-steps 0 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-steps 0 ;;
-    profdef) run rocprof_default 600 rocprofv3 --kernel-trace --stats -d "$OUT/profdef" -o run --output-format csv -- python bench.py --steps 20 --warmup 5 ;;
+    profdef) run rocprof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/profdef" -o run --output-format csv -- python bench.py ;;
+    bench20) run bench_20 600 python bench.py --steps 20 --warmup 5 --cpu-steps 0 ;;
+    hostprof_eager) run hostprof_eager 600 python tools/host_profile.py balance 32768 200 eager ;;
   esac
 done
 echo "session done"

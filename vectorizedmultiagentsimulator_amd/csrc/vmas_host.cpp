@@ -146,8 +146,10 @@ public:
             groups_.push_back(std::move(gr));
         }
         opts_ = at::TensorOptions().device(at::Device(at::kCUDA, (c10::DeviceIndex)device));
-        // the step's fresh outputs and the next direct buffers in ONE allocation (one caching-
-        // allocator call per step instead of one per group and region); VMAS_HOST_ONE_ALLOC=0: one each
+        // the step's fresh outputs in ONE allocation and the next direct buffers in another (two
+        // caching-allocator calls per step instead of one per group and region; kept apart so that
+        // a caller holding only the next step's observations does not keep this step's state and
+        // info outputs alive); VMAS_HOST_ONE_ALLOC=0: one allocation each
         static const bool one = !(getenv("VMAS_HOST_ONE_ALLOC") && getenv("VMAS_HOST_ONE_ALLOC")[0] == '0');
         one_ = one;
         constexpr int64_t kAlign = 256;
@@ -156,8 +158,8 @@ public:
             total_ += (g.n * g.member_bytes + kAlign - 1) / kAlign * kAlign;
         }
         for (Region& r : regions_) {
-            r.off = total_;
-            total_ += (r.nbytes + kAlign - 1) / kAlign * kAlign;
+            r.off = rtotal_;
+            rtotal_ += (r.nbytes + kAlign - 1) / kAlign * kAlign;
         }
     }
 
@@ -167,9 +169,11 @@ public:
     std::vector<at::Tensor> alloc() {
         std::vector<at::Tensor> out;
         out.reserve(count());
-        if (one_ && total_ > 0) {
+        if (one_ && total_ + rtotal_ > 0) {
             at::Tensor big = at::empty({total_}, opts_.dtype(at::kByte));
             const uintptr_t b0 = (uintptr_t)big.data_ptr();
+            at::Tensor rbig = rtotal_ > 0 ? at::empty({rtotal_}, opts_.dtype(at::kByte)) : at::Tensor();
+            const uintptr_t r0 = rtotal_ > 0 ? (uintptr_t)rbig.data_ptr() : 0;
             for (const Group& g : groups_) {
                 for (size_t r = 0; r < g.row_members.size(); ++r)
                     tbl_[g.r0 + (int64_t)r].dst = (void*)(b0 + (uintptr_t)(g.off + g.row_members[r] * g.member_bytes));
@@ -181,8 +185,8 @@ public:
                 const int64_t es = (int64_t)c10::elementSize(r.dtype), so = box.storage_offset() / es;
                 for (size_t m = 0; m < r.offsets.size(); ++m)
                     out.push_back(storage_view(box, r.dtype, r.sizes[m], r.strides[m], so + r.offsets[m]));
-                r.pending = big.narrow(0, r.off, r.nbytes);
-                tbl_[r.row].src = (const void*)(b0 + (uintptr_t)r.off - r.base);
+                r.pending = rbig.narrow(0, r.off, r.nbytes);
+                tbl_[r.row].src = (const void*)(r0 + (uintptr_t)r.off - r.base);
             }
             return out;
         }
@@ -255,6 +259,7 @@ private:
     at::TensorOptions opts_;
     bool one_ = true;
     int64_t total_ = 0;
+    int64_t rtotal_ = 0;  // (the direct regions' allocation)
 };
 
 class UniformDraw {

@@ -25,7 +25,7 @@ def make_env(
     grad_enabled: bool = False,
     terminated_truncated: bool = False,
     wrapper_kwargs: Optional[dict] = None,
-    graph_step: bool = False,
+    graph_step: Optional[bool] = None,
     **kwargs,
 ):
     """Create a vectorized environment.
@@ -33,8 +33,10 @@ def make_env(
     Same arguments as the reference's ``vmas.make_env``.  ``device`` may be ``"cpu"`` (host
     backend of the native engine) or a ROCm device such as ``"cuda"`` / ``"cuda:0"`` (gfx950
     kernels).  ``scenario`` is a scenario file name from ``scenarios/`` or a BaseScenario.
-    ``graph_step=True`` (ROCm devices; not in the reference) replays each step as one HIP graph
-    once the world is warm, with the same results (simulator/environment/_graph.py).
+    ``graph_step`` (not in the reference): True replays each step as one HIP graph once the world
+    is warm, with the same results (ROCm devices; simulator/environment/_graph.py); False keeps
+    the eager step; None (default) picks the graph where it is known to be exact -- a ROCm device,
+    continuous actions, no autograd, one of this package's scenarios (Environment._auto_graph_step).
     """
     if isinstance(scenario, str):
         if not scenario.endswith(".py"):

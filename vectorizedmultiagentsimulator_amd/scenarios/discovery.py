@@ -487,8 +487,9 @@ class HeuristicPolicy(BaseHeuristicPolicy):
 
 
 def spawn_max_tries() -> int:
-    """Tries per target before the one-launch respawn hands an env over to the reference's loop
-    (VMAS_SPAWN_MAX_TRIES; VMAS_SPAWN_TEST_MAX_TRIES lowers it for tests of that hand-over)."""
+    """Tries per target before the one-launch respawn hands an env over to the reference's loop:
+    0 = the kernel's compiled limit; only the test override VMAS_SPAWN_TEST_MAX_TRIES sets another
+    (tests of that hand-over)."""
     return int(os.environ.get("VMAS_SPAWN_TEST_MAX_TRIES", "0") or 0)
 
 

@@ -98,8 +98,17 @@ def _own_scenario(scenario) -> bool:
     scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                            "scenarios") + os.sep
     cls = type(scenario)
-    return (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
-            and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir))
+    if not (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
+            and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir)):
+        return False
+    # a step-time method overridden on the instance (a monkeypatched reward / post_step ...) may
+    # read a write-only attribute before the class's own code re-binds it
+    inst = getattr(scenario, "__dict__", {})
+    return not any(m in inst for m in _STEP_METHODS)
+
+
+_STEP_METHODS = ("reward", "observation", "done", "info", "pre_step", "post_step", "process_action",
+                 "env_process_action", "extra_render")
 
 
 def _write_only(o, k: str) -> bool:

@@ -156,7 +156,7 @@ class Environment(TorchVectorizedObject):
         clamp_actions: bool = False,
         grad_enabled: bool = False,
         terminated_truncated: bool = False,
-        graph_step: bool = False,
+        graph_step: Optional[bool] = None,
         **kwargs,
     ):
         if multidiscrete_actions:
@@ -200,6 +200,9 @@ class Environment(TorchVectorizedObject):
         self.action_space = self.get_action_space()
         self.observation_space = self.get_observation_space(observations)
         self._graph = None
+        self.graph_auto = graph_step is None
+        if graph_step is None:
+            graph_step = self._auto_graph_step()
         if graph_step:
             if self.device.type != "cuda":
                 raise ValueError("graph_step=True needs a ROCm device (HIP graphs)")
@@ -212,6 +215,21 @@ class Environment(TorchVectorizedObject):
         self.headless = None
         self.visible_display = None
         self.text_lines = None
+
+    def _auto_graph_step(self) -> bool:
+        """graph_step=None (the default; the reference's make_env has no such argument, so an
+        unchanged caller -- torchrl's VmasEnv, the Gym wrappers -- lands here): replay the step as
+        one HIP graph when that is known to give the eager step's results bit for bit -- a ROCm
+        device, continuous actions, no autograd, and one of this package's own scenarios, whose
+        per-step state lives in device tensors (tests/test_graph.py holds each to its eager step).
+        Anything else stays eager.  VMAS_GRAPH_STEP=0 turns the automatic choice off."""
+        if os.environ.get("VMAS_GRAPH_STEP", "auto") == "0":
+            return False
+        if self.device.type != "cuda" or self.grad_enabled or not self.continuous_actions:
+            return False
+        from ._graph import _own_scenario
+
+        return _own_scenario(self.scenario)
 
     @local_seed(vmas_random_state)
     def reset(self, seed: Optional[int] = None, return_observations: bool = True,
