@@ -506,7 +506,8 @@ def main():
     if args.scenario == "balance" and args.envs == 32768:
         metric = "env-steps/sec (num_envs x steps / wall-s), 'balance' @32k envs, 1->8 GPU"  # BASELINE.json
     else:
-        metric = f"env-steps/sec (num_envs x steps / wall-s), '{args.scenario}' @{args.envs} envs/GPU"
+        metric = (f"env-steps/sec (num_envs x steps / wall-s), '{args.scenario}' @{args.envs} envs"
+                  + ("/GPU" if on_gpu else " on CPU"))
     out = {
         "metric": metric,
         "value": round(value, 1),

@@ -11,7 +11,8 @@ oracle carries only its own shaping state, set from the reset state).  Tolerance
     ``rot % pi`` is one remainder);
   * rewards / infos: 1e-4 + 1e-5 |x| (differences of two norms scaled by the shaping factor 100);
   * dones: exact; LIDAR columns: tests/_parity.py's LIDAR tolerance (2e-5 + 2e-5 |x|) with its
-    ray-turn certification.
+    ray-turn certification, then a scan over rays turned by up to 1e-6 rad for near-grazing hits
+    (_scan_certify; counted as scan_certified_rows).
 An env outside these passes only when the oracle certifies it sits on a flag threshold: some
 distance the programs compared with a threshold (overlap, coverage, collision) lies within
 MARGIN_TOL of it, so a last-bit difference of that distance flips the flag.
@@ -33,6 +34,34 @@ SCRIPTED_U_ATOL = 2e-6
 
 def _cpu(t):
     return t.detach().to("cpu")
+
+
+SCAN_DELTA, SCAN_POINTS = 1e-6, 41
+
+
+def _scan_certify(world, snap, idx, ai, rays, spec, got, bad):
+    """A LIDAR value outside the tolerance that no single ray turn of tests/_parity.py reproduces:
+    a near-grazing hit, where dist = |foot - o| - sqrt(r^2 - d^2) turns steep as d -> r, so that
+    last-bit differences of d (hardware sin / cos of the fast LIDAR, ~1e-6 rad) move it by more
+    than the tolerance.  Certified when the oracle, scanned over rays turned by up to SCAN_DELTA
+    (SCAN_POINTS angles), takes the engine's value: equal within the tolerance at a scanned angle,
+    or between the values at two neighbouring scanned angles that both hit (the hit distance is
+    continuous there, so an angle in between gives it exactly).  Returns, per row of ``idx``,
+    whether every bad ray of it is certified."""
+    from oracle import vmas_oracle as O
+
+    sub = {i: {k: v[idx] for k, v in d.items()} for i, d in snap.items()}
+    ow = O.OracleWorld(world, sub)
+    ow.batch_dim = len(idx)
+    r0, gv, bd = rays[idx], got[idx], bad[idx]
+    scan = torch.stack([ow.cast_rays(ai, r0 + dl, spec.max_range, spec.entity_filter)
+                        for dl in torch.linspace(-SCAN_DELTA, SCAN_DELTA, SCAN_POINTS).tolist()])  # [K, n, R]
+    tol = LIDAR_ATOL + LIDAR_RTOL * gv.abs()
+    eq = ((scan - gv).abs() <= tol).any(0)
+    hit = scan < spec.max_range
+    lo, hi = torch.minimum(scan[:-1], scan[1:]), torch.maximum(scan[:-1], scan[1:])
+    between = (hit[:-1] & hit[1:] & (lo - tol <= gv) & (gv <= hi + tol)).any(0)
+    return ((eq | between) | ~bd).all(-1)
 
 
 def _env_err(got, exp, atol, rtol):
@@ -129,20 +158,19 @@ class ScenarioParity:
                 for d in _parity._RAY_CERT_DELTAS:
                     e2 = ow.cast_rays(ai, rays + d, spec.max_range, spec.entity_filter)
                     cert |= (g - e2).abs() <= LIDAR_ATOL + LIDAR_RTOL * e2.abs()
-                unc = (rb & ~cert).any(-1)
+                left = rb & ~cert
+                if left.any():  # near-grazing hits: the scan certification (see _scan_certify)
+                    idx = left.any(-1).nonzero().flatten()
+                    ok = _scan_certify(self.env.world, post, idx, ai, rays, spec, g, left)
+                    lr["scan_certified_rows"] = lr.get("scan_certified_rows", 0) + int(ok.sum())
+                    left[idx[ok]] = False
+                unc = left.any(-1)
                 lr["uncertified_rows"] += int(unc.sum())
                 lidar_bad_rows |= unc
                 for b in unc.nonzero().flatten()[:4].tolist():  # what a reader needs to judge the row
-                    r = (rb & ~cert)[b].nonzero().flatten().tolist()
-                    wide = {}
-                    for d in (3e-6, 1e-5, 3e-5, 1e-4):
-                        ok = False
-                        for s in (-d, d):
-                            e3 = ow.cast_rays(ai, rays + s, spec.max_range, spec.entity_filter)[b]
-                            ok |= bool(((g[b] - e3).abs() <= LIDAR_ATOL + LIDAR_RTOL * e3.abs())[r].all())
-                        wide[d] = ok
+                    r = left[b].nonzero().flatten().tolist()
                     self.failures.append(("lidar row", self.rec["steps"], k, c0, b, r, g[b, r].tolist(),
-                                          e[b, r].tolist(), rays[b, r].tolist(), wide))
+                                          e[b, r].tolist(), rays[b, r].tolist()))
         # the rest of the observations
         assert len(obs) == len(exp["obs"]), (len(obs), len(exp["obs"]))
         for k, (g, e) in enumerate(zip(obs, exp["obs"])):

@@ -9,9 +9,10 @@ from vectorizedmultiagentsimulator_amd import make_env
 
 
 def _pair(device, **kw):
-    a = make_env("balance", num_envs=64, device=device, seed=3, n_agents=3, **kw)
-    b = make_env("balance", num_envs=64, device=device, seed=3, n_agents=3, **kw)
-    b._apply_continuous_actions = lambda actions: False  # force the per-agent path
+    # (eager steps: the action paths themselves; graph mode's own use of them is tests/test_graph.py's)
+    a = make_env("balance", num_envs=64, device=device, seed=3, n_agents=3, graph_step=False, **kw)
+    b = make_env("balance", num_envs=64, device=device, seed=3, n_agents=3, graph_step=False, **kw)
+    b._apply_continuous_actions = lambda actions, *args, **kw: False  # force the per-agent path
     return a, b
 
 

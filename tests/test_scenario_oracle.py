@@ -137,3 +137,23 @@ def test_clamped_actions_match_oracle_gpu(gpu_device):
     acts = lambda env, t: [(torch.rand(32768, 2, generator=g) * 6 - 3).to(gpu_device) for _ in env.agents]  # noqa: E731
     _run(env, "balance", dict(n_agents=4), 5, "C2 balance 32768 envs graph clamp_actions: actions vs oracle",
          actions=acts)
+
+
+def test_c1_plumbing_balance_128_envs_cpu():
+    """BASELINE configs[0] (C1): make_env('balance', num_envs=128, n_agents=4) on CPU, 200 random
+    steps -- every step's actions, observations, rewards, dones and infos against the oracle, and
+    every 25th step the physics itself (teacher-forced World.step, oracle/vmas_oracle.py)."""
+    from oracle import vmas_oracle as O
+
+    env = make_env("balance", num_envs=128, device="cpu", seed=0, n_agents=4)
+    sp = ScenarioParity(env, "balance", dict(n_agents=4))
+    phys = []
+    for t in range(200):
+        sp.step()
+        if t % 25 == 24:
+            phys.append(O.compare_one_step(env.world))  # (an extra World.step: the shaping carried by
+            # both sides is still the last reward's, as the reference's would be)
+    rec = sp.record("C1 balance 128 envs cpu 200 steps: actions + scenario program + physics vs oracle")
+    rec["physics_bad_envs"] = sum(r["bad_envs"] for r in phys)
+    assert sp.ok, f"{sp.failures[:6]!r} {rec!r}"
+    assert all(r["ok"] for r in phys), phys

@@ -902,6 +902,10 @@ struct Gen {
         std::string& o = src;
         o += "// generated by vmas_jit.hip for one world\n";
         if (relaxed) o += std::string(kRelaxedTag) + "\n#define VMAS_PHYS_RELAXED 1\n";
+        // A/B knob: VMAS_JIT_TRIG=guard generates round 4's entity trig (a lane-divergent branch to
+        // the library sin / cos beyond 16 rad) instead of the branch-free reduction (vmas_physics.hpp)
+        if (relaxed && getenv("VMAS_JIT_TRIG") && std::string(getenv("VMAS_JIT_TRIG")) == "guard")
+            o += "#define VMAS_TRIG_GUARD 1\n";
         o += std::string(kFlagsTag) + codegen_flags(relaxed) + "\n";
         if (prof_block >= 0) o += "#define VMAS_JIT_PROFILE_SLOTS 1\n";
         o += "#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
@@ -913,9 +917,6 @@ struct Gen {
              "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
              "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
-             "    if (s0 == 2 && s1 == 1) {\n"
-             "        const float2 v = reinterpret_cast<const float2*>(p)[b];\n"
-             "        return mk(v.x, v.y);\n    }\n"
              "    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);\n}\n\n";
         o += "constexpr WorldK WK{" + fl(cfg.contact_margin) + ", " + fl(cfg.collision_force) + ", " +
              fl(cfg.joint_force) + ", " + fl(cfg.torque_constraint_force) + "};\n";

@@ -85,10 +85,26 @@ VHD Real tclamp(Real x, Real lo, Real hi) { return tmin(tmax(x, lo), hi); }
 #ifdef VMAS_PHYS_RELAXED
 // v_sin / v_cos_f32 take revolutions: the x * (1 / 2 pi) product rounds to |x| * 2^-24 rad (1e-6
 // rad at 16 rad) and the instructions' domain ends at 256 revolutions.  The reference never wraps
-// an entity's rotation (core.py:2907), so a spinning body's angle grows without bound: beyond
-// 16 rad the correctly rounded library functions (a lane-divergent branch, taken only then).
+// an entity's rotation (core.py:2907), so a spinning body's angle grows without bound: the
+// argument is first reduced by 2 pi (Cody-Waite, 2 pi as three floats, the first with 8
+// significant bits so that k * C1 is exact for |k| < 2^16, i.e. |x| < 4e5 rad; fused
+// multiply-adds), branch-free.  |x| < pi gives k = 0 and r = x exactly: the same value as the
+// unreduced instruction.  (Round 4's lane-divergent branch to the library sin / cos beyond 16 rad
+// kept the library's Payne-Hanek code and its registers in every world's kernel: +10 VGPRs and
+// +12.5 % VALU instructions per balance launch)
+#ifdef VMAS_TRIG_GUARD
 VHD Real tsin(Real x) { return fabsf(x) < 16.f ? __sinf(x) : sinf(x); }
 VHD Real tcos(Real x) { return fabsf(x) < 16.f ? __cosf(x) : cosf(x); }
+#else
+VHD Real red2pi(Real x) {
+    const Real k = rintf(x * 0x1.45f306p-3f);
+    Real r = __builtin_fmaf(-k, 6.28125f, x);
+    r = __builtin_fmaf(-k, 0x1.fb5444p-10f, r);
+    return __builtin_fmaf(-k, 0x1.68c234p-37f, r);
+}
+VHD Real tsin(Real x) { return __sinf(red2pi(x)); }
+VHD Real tcos(Real x) { return __cosf(red2pi(x)); }
+#endif
 VHD Real tlog1p(Real y) {
     const Real u = 1.f + y;
     return u == 1.f ? y : __logf(u) * (y / (u - 1.f));

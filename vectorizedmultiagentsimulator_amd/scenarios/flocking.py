@@ -69,10 +69,13 @@ class Scenario(BaseScenario):
                 _fused.check(_fused.lib().vmas_flocking_target_action(
                     _fused.device_index(world), self.t.data_ptr(), world.batch_dim, 30.0, u.data_ptr(),
                     _fused.stream(world)), "vmas_flocking_target_action")
-                agent.action.u = u
-                return
-            t = self.t / 30
-            agent.action.u = torch.stack([torch.cos(t), torch.sin(t)], dim=1)
+            else:
+                t = self.t / 30
+                u = torch.stack([torch.cos(t), torch.sin(t)], dim=1)
+            # cos / sin: |u| <= 1 by construction, so the scripted-action range check (core.py
+            # _range_proven) needs no device work and graph replays need no rollback for it
+            u._vmas_abs_bound = 1.0
+            agent.action.u = u
 
         return action_script
 
