@@ -52,9 +52,10 @@ def parse():
     p.add_argument("--event-launches", type=int, default=20,
                    help="extra eager step launches timed with HIP events after the timed region")
     p.add_argument("--device", default=None, help="override device (e.g. cpu for plumbing tests)")
-    p.add_argument("--graph", default="on", choices=["on", "off"],
-                   help="on: make_env(graph_step=True) -- each step replayed as one HIP graph once warm "
-                        "(same results as eager; falls back to eager if the step cannot be captured)")
+    p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                   help="auto: make_env without graph_step, the reference API's call (the package's "
+                        "scenarios on a ROCm device then replay each step as one HIP graph once warm, with "
+                        "the eager step's results); on: graph_step=True; off: graph_step=False (eager)")
     p.add_argument("--kw", default=None, help='extra scenario kwargs as JSON, e.g. \'{"use_agent_lidar": true}\' '
                                                 '(default: the scenario\'s §8(d) config)')
     args = p.parse_args()
@@ -83,7 +84,8 @@ def make_world_env(args, device, seed):
 
     kw = {"n_agents": args.n_agents} if args.scenario in ("balance", "transport", "discovery", "flocking") else {}
     kw.update(json.loads(args.kw))
-    graph = args.graph == "on" and str(device).startswith("cuda")
+    cuda = str(device).startswith("cuda")
+    graph = {"auto": None, "on": cuda, "off": False}[args.graph] if cuda else False
     env = make_env(args.scenario, num_envs=args.envs if device != "cpu-baseline" else args.cpu_envs,
                    device=device if device != "cpu-baseline" else "cpu", seed=seed, graph_step=graph, **kw)
     if args.substeps:
@@ -432,6 +434,8 @@ def main():
     workload = (f"{args.scenario} {args.envs} envs/GPU, n_agents={args.n_agents}, substeps={world._substeps}, "
                 f"broadphase={args.broadphase}")
     step_mode = env.graph_status if env.graph_status != "off" else "eager"
+    if env.graph_auto:
+        step_mode += " (chosen by make_env's default graph_step=None)"
     if json.loads(args.kw):
         workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)
@@ -538,7 +542,9 @@ def main():
     if group is not None:
         out["process_group"] = group
     if args.scenario == "discovery":  # (respawns the one-launch sampler handed over to the reference loop)
-        out["config"]["respawn_handovers"] = {"timed": handovers[0] - h0, "total": handovers[0]}
+        out["config"]["respawn_handovers"] = {
+            "timed": handovers[0] - h0, "total": handovers[0],
+            "why": type(env.scenario).make_world.__globals__.get("HANDOVER_LOG", [])}
     if rank == 0 and world_size == 1 and args.cpu_steps > 0:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

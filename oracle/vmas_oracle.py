@@ -943,6 +943,7 @@ def sensitivity_band(world, snap, expected, broadphase="batch", n=2, eps=1.2e-7,
 # only).  ``max_bad_frac`` (default 0) additionally allows uncertified envs (kept for callers
 # that opt in; no test does).
 CUTOFF_TOL = 4e-6
+BAND_RETRY_N = 16  # perturbations of the second band estimate (compare_one_step)
 
 
 def cutoff_bound(world) -> Dict[str, float]:
@@ -1049,6 +1050,14 @@ def compare_one_step(world, broadphase: str = "batch", with_band: bool = True, c
     world.step()
     got = snapshot(world)
     rep = compare(got, expected, world, band=band, cutoff=ow.cutoff_margin if certify else None, **tol)
+    if band is not None and rep["uncertified_envs"]:
+        # two random 1-ulp perturbations can miss a stiff env's sensitivity: before calling an
+        # env bad, estimate the oracle's band again from BAND_RETRY_N more (the band is a property
+        # of the oracle at this state, not of the engine) and compare once more
+        more = sensitivity_band(world, snap, expected, broadphase, n=BAND_RETRY_N, seed=98765)
+        band = {i: {k: torch.maximum(band[i][k], more[i][k]) for k in band[i]} for i in band}
+        rep = compare(got, expected, world, band=band, cutoff=ow.cutoff_margin if certify else None, **tol)
+        rep["band_retry"] = BAND_RETRY_N
     rep["iterations"] = getattr(world.engine, "last_iterations", None)
     rep["active_pairs_per_substep"] = [len(x) for x in ow.active_log]
     return rep

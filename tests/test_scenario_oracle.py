@@ -157,3 +157,26 @@ def test_c1_plumbing_balance_128_envs_cpu():
     rec["physics_bad_envs"] = sum(r["bad_envs"] for r in phys)
     assert sp.ok, f"{sp.failures[:6]!r} {rec!r}"
     assert all(r["ok"] for r in phys), phys
+
+
+def test_lidar_scan_certification_cpu():
+    """tests/_scenario_parity._scan_certify runs and is not vacuous: a row moved 1e-3 off the
+    oracle is not certified, the oracle's own row is."""
+    from oracle import vmas_oracle as O
+    from tests._scenario_parity import _scan_certify
+
+    env = _make("flocking", dict(n_agents=5), None, "cpu", 64, seed=3)
+    for _ in range(3):
+        env.step(env.get_random_actions())
+    snap = O.snapshot(env.world)
+    prog = SO.program("flocking", env.world)
+    ai = env.world.entities.index(env.world.policy_agents[0])
+    ow = O.OracleWorld(env.world, snap)
+    exp, rays = prog.lidar.measure(ow, ai)
+    idx = torch.arange(8)
+    bad = torch.zeros_like(exp, dtype=torch.bool)
+    bad[:8, 0] = True
+    assert _scan_certify(env.world, snap, idx, ai, rays, prog.lidar, exp, bad).all()
+    off = exp.clone()
+    off[:8, 0] = torch.where(exp[:8, 0] < 0.2, exp[:8, 0] + 1e-3, exp[:8, 0] - 1e-3)
+    assert not _scan_certify(env.world, snap, idx, ai, rays, prog.lidar, off, bad).any()

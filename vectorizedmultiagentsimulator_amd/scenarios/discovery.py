@@ -565,6 +565,13 @@ def respawn_reference_loop(agents_pos: Tensor, covered: Tensor, min_dist: float,
 
 
 HANDOVERS = [0]  # (respawns redone by the reference loop in this process: bench.py reports it)
+HANDOVER_LOG = []  # why each was redone (the first 16): bench.py reports it
+
+
+def _note_handover(where: str, timed_out: bool, h, T: int) -> None:
+    if len(HANDOVER_LOG) < 16:
+        HANDOVER_LOG.append({"where": where, "timed_out": bool(timed_out), "unresolved": int(h[T]),
+                             "error_word": int(h[T + 1]) if len(h) > T + 1 else None})
 
 
 def _respawn_redo(args, backup: Tensor, offset: int, gen) -> None:
@@ -577,7 +584,31 @@ def _respawn_redo(args, backup: Tensor, offset: int, gen) -> None:
     for i, tp in enumerate(targets):
         tp.copy_(backup[i])
     gen.set_offset(offset)
+    if _redo_per_target(args, offset, gen):
+        return
     respawn_reference_loop(*args[:5], targets)
+
+
+def _redo_per_target(args, offset: int, gen) -> bool:
+    """The hand-over's first resort: the same respawn through the per-target kernels (no window,
+    no list of envs with a covered target -- the windowed chain holds ~480 of them, and the first
+    step after a full reset at C4 has ~650), exact as well (tests/test_spawn.py).  False, with the
+    targets and the generator back where they were, when that one leaves an env unresolved too."""
+    agents_pos, covered, min_dist, xs, ys = args[:5]
+    targets = args[5:]
+    T = len(targets)
+    mx = torch.zeros(N.spawn_words(T), dtype=torch.int32, device=agents_pos.device)
+    bk = torch.empty((T, agents_pos.shape[0], 2), dtype=torch.float32, device=agents_pos.device)
+    io, inc = _spawn_launch(agents_pos, covered, min_dist, xs, ys, targets, mx, backup=bk)
+    h = mx[:N.VMAS_SPAWN_ERR_WORD + 1].tolist()
+    if h[N.VMAS_SPAWN_ERR_WORD] or h[T]:
+        for i, tp in enumerate(targets):
+            tp.copy_(bk[i])
+        gen.set_offset(offset)
+        return False
+    _spawn_consumed(h, T, io.offset, inc, gen)
+    HANDOVER_LOG.append({"redone_by": "per-target kernels"}) if len(HANDOVER_LOG) < 16 else None
+    return True
 
 
 def deferred_respawn() -> bool:
@@ -678,6 +709,7 @@ class DeferredRespawn:
             return False
         gen = torch.cuda.default_generators[self.idx]
         if timed_out or h[self.T + 1] or h[self.T]:
+            _note_handover("channel", timed_out, h, self.T)
             _respawn_redo(self.args, self.chan.backup, self.offset, gen)
             return True
         _spawn_consumed(h, self.T, self.offset, self.inc, gen)
@@ -704,6 +736,7 @@ def respawn_targets_native(agents_pos: Tensor, covered: Tensor, min_dist: float,
     h = mx[:N.VMAS_SPAWN_ERR_WORD + 1].tolist()  # the step's one host wait (maxima, unresolved, error)
     gen = torch.cuda.default_generators[idx]
     if h[N.VMAS_SPAWN_ERR_WORD] or h[T]:
+        _note_handover("eager", bool(h[N.VMAS_SPAWN_ERR_WORD]), h[:T + 1] + [h[N.VMAS_SPAWN_ERR_WORD]], T)
         _respawn_redo((agents_pos, covered, min_dist, x_semidim, y_semidim, *target_pos), backup, io.offset, gen)
         return mx
     _spawn_consumed(h, T, io.offset, inc, gen)
