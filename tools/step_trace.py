@@ -17,6 +17,13 @@ if len(idx) < 5:
     sys.exit(f"only {len(idx)} {anchor} dispatches")
 periods, busy, counts = [], [], []
 stretches = list(zip(idx[:-1], idx[1:]))
+# the steady-state steps: the most common dispatch count among stretches of more than one dispatch
+# (bench.py also launches the step kernel alone, back to back, and the scenario program's calls
+# after the timed region: those stretches have other counts)
+import collections  # noqa: E402
+
+n_common = collections.Counter(b - a for a, b in stretches if b - a > 1).most_common(1)[0][0]
+stretches = [(a, b) for a, b in stretches if b - a == n_common]
 for a, b in stretches:
     periods.append((rows[b]["s"] - rows[a]["s"]) / 1e3)
     busy.append(sum(rows[k]["e"] - rows[k]["s"] for k in range(a, b)) / 1e3)
