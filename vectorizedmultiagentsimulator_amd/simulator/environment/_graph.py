@@ -987,6 +987,7 @@ class StepGraph:
                 if k in _STATE_KEYS and hasattr(type(o), "_fresh"):  # (an EntityState / AgentState)
                     fresh.append((after, k, v1))
         self._carry_ys = [y for _, y in carry]
+        self._carry_names = names  # (reporting: tools/post_table_probe.py)
         x_keys = {_storage_key(x): n for (x, _), n in zip(carry, names)}
         for (_, y), n in zip(carry, names):
             if _storage_key(y) in x_keys:
