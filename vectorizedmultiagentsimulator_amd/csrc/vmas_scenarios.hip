@@ -410,82 +410,6 @@ __global__ void __launch_bounds__(256) k_flocking_fast(VmasFlockingIO io_arg) {
     }
 }
 
-// k_flocking_fast<12, NT> with a wave per (64 envs, policy agent, half of the 12 rays): two waves
-// of one workgroup share an agent's observation rows in LDS (the first also computes the reward
-// and the row's head) and write them out together after one barrier.  The same operations per
-// ray in the same order (bit-identical); 8 192 waves at 32 768 envs x 8 agents instead of 4 096.
-template <int NT>
-__global__ void __launch_bounds__(256) k_flocking_split(VmasFlockingIO io_arg) {
-    constexpr int NR = 12, HR = NR / 2, W = 6 + NR;
-#ifdef __HIP_DEVICE_COMPILE__
-    KFlockingIO& io = *(KFlockingIO*)__builtin_amdgcn_kernarg_segment_ptr();
-    (void)io_arg;
-#else
-    KFlockingIO& io = io_arg;
-#endif
-    __shared__ float S[2][64 * W];
-    const int lane = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
-    const int sub = w >> 1, half = w & 1;
-    const int p = __builtin_amdgcn_readfirstlane((int)blockIdx.y * 2 + sub);
-    const bool active = p < io.n_policy;  // (no early return: the barrier below)
-    const int g0 = (int)blockIdx.x * 64, b = g0 + lane;
-    const bool valid = b < io.batch;
-    const int bb = valid ? b : io.batch - 1;
-    const int row = lane * W;
-    const int nv = io.batch - g0 < 64 ? io.batch - g0 : 64;
-    const OutDelta od = load_out_delta(io);
-    if (active) {
-        const float* ang = io.angles[p] + (long)bb * io.ang_s0[p];
-        const int as1 = io.ang_s1[p];
-        float A[HR];
-#pragma unroll
-        for (int r = 0; r < HR; ++r) A[r] = ang[(long)(half * HR + r) * as1];
-        const VmasVec rv = io.rot[p];
-        const float rot = ld_vec1(rv, bb);
-        const VmasShapeRef ak = io.agents[io.policy[p]];
-        const V2 pk = ref_pos(ak, bb);
-        V2 T[NT];
-        float C[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const float* xp = io.ray_targets[t].pos;
-            const int s0 = io.ray_targets[t].pos_s0, s1 = io.ray_targets[t].pos_s1;
-            const float rad = io.ray_targets[t].radius;
-            T[t] = mk(xp[(long)bb * s0], xp[(long)bb * s0 + s1]) - pk;
-            C[t] = rad * rad - (T[t].x * T[t].x + T[t].y * T[t].y);
-        }
-        if (half == 0 && valid) {
-            const FlockHead h = flock_part0(io, b, p, od, true);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) S[sub][row + i] = h.v[i];
-        }
-#pragma unroll
-        for (int r = 0; r < HR; ++r) {
-            const float a = A[r] + rot;
-            float ds, dc;
-            if (fabsf(a) < kFastTrigMaxAngle) {
-                ds = __sinf(a);
-                dc = __cosf(a);
-            } else {
-                sincosf(a, &ds, &dc);
-            }
-            float best = io.max_range;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) best = min_drop_nan(best, ray_sphere_fast_nan(T[t].x, T[t].y, C[t], dc, ds));
-            S[sub][row + 6 + half * HR + r] = best;
-        }
-        float* lid = io.lidar[p] + (long)g0 * NR;  // (this wave's own columns: no barrier needed)
-        for (int k = lane; k < nv * HR; k += 64) {
-            const int e = k / HR, c = k - e * HR;
-            lid[e * NR + half * HR + c] = S[sub][e * W + 6 + half * HR + c];
-        }
-    }
-    __syncthreads();
-    if (!active) return;
-    float* obs = moved(io.obs[p], od.obs) + (long)g0 * W;
-    for (int k = lane + half * 64; k < nv * W; k += 128) obs[k] = S[sub][k];
-}
-
 // flocking's scripted target: u = stack([cos(t / period), sin(t / period)], dim=1) (the division
 // by a Python scalar as torch's divide kernel computes it: t * (1 / period) in fp32).
 __global__ void __launch_bounds__(256) k_flocking_target(const float* t, int batch, float inv, float* u) {
@@ -1049,21 +973,6 @@ int32_t vmas_flocking_outputs(int32_t device, const VmasFlockingIO* io, void* st
         // flocking's 12 rays with 1..8 targets: the unrolled instantiation (VMAS_FLOCK_UNROLL=0: runtime form)
         static const bool unroll = !getenv("VMAS_FLOCK_UNROLL") || getenv("VMAS_FLOCK_UNROLL")[0] != '0';
         const int nt = unroll && io->n_rays == 12 ? io->n_ray_targets : 0;
-        // a wave per half of the rays when the observations are computed (VMAS_FLOCK_SPLIT=0: per agent, A/B)
-        static const bool split = !(getenv("VMAS_FLOCK_SPLIT") && getenv("VMAS_FLOCK_SPLIT")[0] == '0');
-        if (split && nt > 0 && (io->what & VMAS_SCN_OBS)) {
-            const dim3 g2((io->batch + 63) / 64, (io->n_policy + 1) / 2);
-            switch (nt) {
-#define VMAS_FLOCK_CASE(k) \
-    case k: hipLaunchKernelGGL((k_flocking_split<k>), g2, dim3(256), 0, st, *io); break;
-                VMAS_FLOCK_CASE(1) VMAS_FLOCK_CASE(2) VMAS_FLOCK_CASE(3) VMAS_FLOCK_CASE(4)
-                VMAS_FLOCK_CASE(5) VMAS_FLOCK_CASE(6) VMAS_FLOCK_CASE(7) VMAS_FLOCK_CASE(8)
-#undef VMAS_FLOCK_CASE
-                default: break;
-            }
-            VMAS_AUX_HIP(hipGetLastError());
-            return VMAS_OK;
-        }
         switch (nt) {
 #define VMAS_FLOCK_CASE(k) \
     case k: hipLaunchKernelGGL((k_flocking_fast<12, k>), grid, dim3(256), 0, st, *io); break;
