@@ -436,6 +436,11 @@ def main():
     step_mode = env.graph_status if env.graph_status != "off" else "eager"
     if env.graph_auto:
         step_mode += " (chosen by make_env's default graph_step=None)"
+    g = getattr(env, "_graph", None)
+    if g is not None and env.graph_status == "graph":
+        # how a replay is launched: the graph's kernels on the stream, or hipGraphLaunch
+        step_mode += (f"; replay: {g._chain.n_nodes}-kernel chain" if g._chain is not None
+                      else f"; replay: hipGraphLaunch ({g.chain_why or 'torch replay'})")
     if json.loads(args.kw):
         workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)

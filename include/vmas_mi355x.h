@@ -52,6 +52,7 @@ extern "C" {
 #define VMAS_E_HIP (-2)
 #define VMAS_E_NOMEM (-3)
 #define VMAS_E_NOCONVERGE (-4)
+#define VMAS_E_UNSUPPORTED (-5) /* vmas_graph_chain_build: the graph is not a short chain of kernel nodes */
 
 /* shapes: vmas/simulator/core.py:102-202 */
 #define VMAS_SPHERE 0
@@ -223,6 +224,18 @@ int32_t vmas_stream_abort_capture(void* stream);
  * graph that draws no random numbers, without torch's generator-state prologue (no reference
  * counterpart). */
 int32_t vmas_graph_launch(void* graph_exec, void* stream);
+/* A captured step graph (hipGraph_t, torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()) that
+ * is a chain of 1..max_nodes (<= VMAS_GRAPH_CHAIN_MAX) kernel nodes, replayed as plain kernel
+ * launches on a stream: a replayed graph costs the GPU ~5 us more per launch than its kernels
+ * launched on the stream (graph mode's replay; no reference counterpart).  build: VMAS_E_UNSUPPORTED
+ * when the graph is not such a chain (the caller keeps vmas_graph_launch).  The nodes' arguments
+ * stay owned by the graph, which must outlive the chain. */
+#define VMAS_GRAPH_CHAIN_MAX 16
+typedef struct VmasKernelChain VmasKernelChain;
+int32_t vmas_graph_chain_build(void* graph, int32_t max_nodes, VmasKernelChain** out_chain);
+int32_t vmas_graph_chain_launch(const VmasKernelChain* chain, void* stream);
+int32_t vmas_graph_chain_nodes(const VmasKernelChain* chain); /* kernels per launch (0: null chain) */
+int32_t vmas_graph_chain_free(VmasKernelChain* chain);
 /* Host waits on the device performed by the library so far (stream / event synchronisations and
  * spins on published words; wraps around): graph mode runs one step between two reads of it to
  * tell whether the step can be captured (no reference counterpart). */

@@ -54,6 +54,10 @@ EXPORTED_SYMBOLS = (
     "vmas_last_error",
     "vmas_stream_abort_capture",
     "vmas_graph_launch",
+    "vmas_graph_chain_build",
+    "vmas_graph_chain_launch",
+    "vmas_graph_chain_free",
+    "vmas_graph_chain_nodes",
     "vmas_host_waits",
     "vmas_test_hold",
     "vmas_balance_outputs",
@@ -570,6 +574,14 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_stream_abort_capture.argtypes = [_vp]
     lib.vmas_graph_launch.restype = _i32
     lib.vmas_graph_launch.argtypes = [_vp, _vp]
+    lib.vmas_graph_chain_build.restype = _i32
+    lib.vmas_graph_chain_build.argtypes = [_vp, _i32, ctypes.POINTER(_vp)]
+    lib.vmas_graph_chain_launch.restype = _i32
+    lib.vmas_graph_chain_launch.argtypes = [_vp, _vp]
+    lib.vmas_graph_chain_free.restype = _i32
+    lib.vmas_graph_chain_nodes.restype = _i32
+    lib.vmas_graph_chain_nodes.argtypes = [_vp]
+    lib.vmas_graph_chain_free.argtypes = [_vp]
     lib.vmas_world_create.restype = _i32
     lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
     lib.vmas_world_destroy.restype = _i32

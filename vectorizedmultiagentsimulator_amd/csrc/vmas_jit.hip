@@ -54,6 +54,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -1202,6 +1203,28 @@ int32_t compile(const std::string& src, std::vector<char>* code) {
 
 }  // namespace
 
+// The k_world functions of the loaded world modules: a kernel node of a captured step graph whose
+// function is one of these is a module launch (vmas_graph_chain_build, vmas_kernels.hip).
+namespace vmas {
+namespace {
+std::mutex g_fn_mu;
+std::unordered_set<const void*> g_live_fns;
+}  // namespace
+void fn_register(hipFunction_t f) {
+    std::lock_guard<std::mutex> lk(g_fn_mu);
+    g_live_fns.insert((const void*)f);
+}
+void fn_unregister(hipFunction_t f) {
+    if (!f) return;
+    std::lock_guard<std::mutex> lk(g_fn_mu);
+    g_live_fns.erase((const void*)f);
+}
+bool jit_owns_function(const void* f) {
+    std::lock_guard<std::mutex> lk(g_fn_mu);
+    return g_live_fns.count(f) != 0;
+}
+}  // namespace vmas
+
 struct VmasJitWorld {
     VmasWorldConfig cfg{};
     std::vector<VmasEntityDesc> ed;
@@ -1257,6 +1280,7 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
     if (!W) return VMAS_OK;
     if (W->cfg.device >= 0) {
         (void)hipSetDevice(W->cfg.device);
+        vmas::fn_unregister(W->fn);
         if (W->mod) (void)hipModuleUnload(W->mod);
         if (W->d_mask) (void)hipFree(W->d_mask);
         if (W->d_blk) (void)hipFree(W->d_blk);
@@ -1315,6 +1339,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         std::vector<char> code;
         if (int32_t rc = compile(g.src, &code)) return cleanup(rc);
         if (W->mod) {
+            vmas::fn_unregister(W->fn);
+            W->fn = nullptr;
             (void)hipModuleUnload(W->mod);
             W->mod = nullptr;
         }
@@ -1322,6 +1348,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
         if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
+        vmas::fn_register(W->fn);
         int scratch = 0;
         (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
         if (scratch == 0 || g.nw == kNW) break;

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -882,6 +883,11 @@ std::vector<CheckScratch*> g_checks;
 
 // ================================================================================================
 // C ABI
+namespace vmas {
+bool jit_owns_function(const void* f);  // vmas_jit.hip: a loaded world module's k_world
+}
+constexpr int kChainMaxNodes = VMAS_GRAPH_CHAIN_MAX;
+
 extern "C" {
 
 int32_t vmas_abi_version(void) { return VMAS_ABI_VERSION; }
@@ -924,6 +930,120 @@ int32_t vmas_graph_launch(void* graph_exec, void* stream) {
         (void)hipGetLastError();
         return fail(VMAS_E_HIP, "vmas_graph_launch: %s", hipGetErrorString(e));
     }
+    return VMAS_OK;
+}
+
+// A captured step graph that is a short chain of kernel nodes, replayed as plain launches on the
+// stream.  Measured on MI355X (tools/launch_gap_probe.py, profiles/r05/run7_launch_gap): a replayed
+// graph costs ~5 us of GPU time more than the same kernel launched on the stream (a 20 us kernel:
+// 24.9 vs 20.0 us per iteration, back to back, GPU-bound), and a stream kernel after a graph
+// starts ~2.3 us later than after a stream kernel -- ~7 us of every C2 step of ~56 us.  The
+// nodes' parameters (function, grid, kernel arguments) stay owned by the kept graph
+// (torch.cuda.CUDAGraph(keep_graph=True)), which must outlive the chain.
+struct VmasKernelChain {
+    int n = 0;
+    hipFunction_t fn[kChainMaxNodes];
+    hipKernelNodeParams p[kChainMaxNodes];
+};
+
+int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain** out) {
+    if (!graph_ || !out) return fail(VMAS_E_INVALID, "vmas_graph_chain_build: null argument");
+    *out = nullptr;
+    const hipGraph_t graph = (hipGraph_t)graph_;
+    max_nodes = std::min<int32_t>(max_nodes, kChainMaxNodes);
+    size_t n = 0;
+    if (hipGraphGetNodes(graph, nullptr, &n) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VMAS_E_HIP, "vmas_graph_chain_build: hipGraphGetNodes");
+    }
+    if (n == 0 || (int64_t)n > max_nodes) return fail(VMAS_E_UNSUPPORTED, "graph of %zu nodes (chain: 1..%d)", n, max_nodes);
+    std::vector<hipGraphNode_t> nodes(n);
+    if (hipGraphGetNodes(graph, nodes.data(), &n) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VMAS_E_HIP, "vmas_graph_chain_build: hipGraphGetNodes");
+    }
+    // every node a kernel node; one root, every other node with exactly one dependency and every
+    // node with at most one dependent: a chain, walked from the root
+    std::vector<hipGraphNode_t> dep(n, nullptr);
+    int root = -1;
+    for (size_t i = 0; i < n; ++i) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) {
+            (void)hipGetLastError();
+            return fail(VMAS_E_UNSUPPORTED, "graph node %zu is not a kernel node", i);
+        }
+        size_t nd = 0;
+        if (hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VMAS_E_HIP, "hipGraphNodeGetDependencies");
+        }
+        if (nd > 1) return fail(VMAS_E_UNSUPPORTED, "graph node %zu has %zu dependencies", i, nd);
+        if (nd == 1) {
+            if (hipGraphNodeGetDependencies(nodes[i], &dep[i], &nd) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(VMAS_E_HIP, "hipGraphNodeGetDependencies");
+            }
+        } else {
+            if (root >= 0) return fail(VMAS_E_UNSUPPORTED, "graph has more than one root");
+            root = (int)i;
+        }
+    }
+    if (root < 0) return fail(VMAS_E_UNSUPPORTED, "graph has no root");
+    std::unique_ptr<VmasKernelChain> c(new VmasKernelChain());
+    std::vector<char> used(n, 0);
+    int cur = root;
+    for (size_t k = 0; k < n; ++k) {
+        if (cur < 0 || used[cur]) return fail(VMAS_E_UNSUPPORTED, "graph is not a chain");
+        used[cur] = 1;
+        hipKernelNodeParams p{};
+        if (hipGraphKernelNodeGetParams(nodes[cur], &p) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VMAS_E_HIP, "hipGraphKernelNodeGetParams");
+        }
+        if (!p.func || (!p.kernelParams && !p.extra)) return fail(VMAS_E_UNSUPPORTED, "kernel node without function / arguments");
+        // a registered host stub (hipLaunchKernelGGL, torch's kernels) or a world module's k_world
+        hipFunction_t f = nullptr;
+        if (hipGetFuncBySymbol(&f, p.func) != hipSuccess || !f) {
+            (void)hipGetLastError();
+            if (!vmas::jit_owns_function(p.func)) return fail(VMAS_E_UNSUPPORTED, "kernel node %d: unknown function", (int)k);
+            f = (hipFunction_t)p.func;
+        }
+        c->fn[k] = f;
+        c->p[k] = p;
+        // the next node: the one whose dependency is this one (at most one)
+        int next = -1;
+        for (size_t i = 0; i < n; ++i)
+            if (dep[i] == nodes[cur]) {
+                if (next >= 0) return fail(VMAS_E_UNSUPPORTED, "graph node has two dependents");
+                next = (int)i;
+            }
+        if (k + 1 < n && next < 0) return fail(VMAS_E_UNSUPPORTED, "graph is not a chain");
+        cur = next;
+    }
+    c->n = (int)n;
+    *out = c.release();
+    return VMAS_OK;
+}
+
+int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) {
+    if (!c || c->n <= 0) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch: empty chain");
+    for (int k = 0; k < c->n; ++k) {
+        const hipKernelNodeParams& p = c->p[k];
+        const hipError_t e = hipModuleLaunchKernel(c->fn[k], p.gridDim.x, p.gridDim.y, p.gridDim.z, p.blockDim.x,
+                                                   p.blockDim.y, p.blockDim.z, p.sharedMemBytes, (hipStream_t)stream,
+                                                   p.kernelParams, p.extra);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(VMAS_E_HIP, "vmas_graph_chain_launch: node %d: %s", k, hipGetErrorString(e));
+        }
+    }
+    return VMAS_OK;
+}
+
+int32_t vmas_graph_chain_nodes(const VmasKernelChain* c) { return c ? c->n : 0; }
+
+int32_t vmas_graph_chain_free(VmasKernelChain* c) {
+    delete c;
     return VMAS_OK;
 }
 

@@ -334,6 +334,45 @@ def _reset_generator_capture_state(dev):
         pass
 
 
+class _KernelChain:
+    """A raw-launched step graph that is a chain of at most MAX_NODES kernel nodes, replayed as
+    plain launches of those kernels on the stream (csrc/vmas_kernels.hip vmas_graph_chain_build):
+    on MI355X a replayed graph costs the GPU ~5 us more than its kernels launched on the stream,
+    and the post-replay launch after it starts ~2.3 us later (tools/launch_gap_probe.py,
+    profiles/r05/run7_launch_gap) -- ~7 us of a ~56 us C2 step.  The launches are the captured
+    nodes' own (function, grid, argument block), in the chain's order, so a replay runs the same
+    kernels on the same arguments as the graph would.  Holds the graph: the nodes' argument
+    blocks belong to it."""
+
+    MAX_NODES = int(os.environ.get("VMAS_GRAPH_CHAIN_MAX", "8"))
+
+    def __init__(self, graph, handle, n_nodes):
+        self.graph = graph
+        self.handle = handle
+        self.n_nodes = n_nodes
+
+    @classmethod
+    def build(cls, graph) -> Tuple[Optional["_KernelChain"], str]:
+        try:
+            raw = graph.raw_cuda_graph()
+        except Exception as ex:  # noqa: BLE001 -- a graph not kept: replay it as a graph
+            return None, f"graph not kept ({type(ex).__name__})"
+        lib = N.load_library()
+        out = ctypes.c_void_p()
+        rc = lib.vmas_graph_chain_build(ctypes.c_void_p(raw), cls.MAX_NODES, ctypes.byref(out))
+        if rc != 0 or not out.value:
+            return None, lib.vmas_last_error().decode(errors="replace")
+        return cls(graph, out, lib.vmas_graph_chain_nodes(out)), ""
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h is not None and h.value:
+            try:
+                N.load_library().vmas_graph_chain_free(h)
+            except Exception:  # noqa: BLE001 -- interpreter shutdown
+                pass
+
+
 class _Segments:
     """Capture of a step that contains host holes: code that must run on the host every step
     because it waits on the device -- the spawn sampler's rejection loop (utils.py:272-319),
@@ -355,7 +394,9 @@ class _Segments:
         self.ran = False
 
     def begin(self):
-        self.cur = torch.cuda.CUDAGraph()
+        # keep_graph: the captured hipGraph_t stays readable after instantiation (its kernel nodes
+        # are what a chain replay launches, _KernelChain)
+        self.cur = torch.cuda.CUDAGraph(keep_graph=StepGraph._CHAIN)
         self.cur.capture_begin(pool=self.pool)
 
     def end(self):
@@ -574,6 +615,8 @@ class StepGraph:
         self._bk_dst: List[Tensor] = []
         self._bk_u: Optional[Tensor] = None
         self._raw_exec: Optional[ctypes.c_void_p] = None
+        self._chain: Optional[_KernelChain] = None
+        self.chain_why = ""  # why a replay is not a kernel chain (diagnostics)
         self._segments: List[torch.cuda.CUDAGraph] = []  # one graph per stretch between host holes
         self._holes: List[Tuple[Any, tuple, Tensor]] = []  # (fn, args, output) run after segment i
         self._executed = None  # outputs of a capture step that already ran (segmented capture)
@@ -805,6 +848,7 @@ class StepGraph:
         self._deferred = []
         self.graph = None
         self._raw_exec = None
+        self._chain = None
         self._segments, self._holes = [], []
         self.status = "dropped"
         self.why = why
@@ -857,7 +901,10 @@ class StepGraph:
         gc.disable()
         # contents of every tracked tensor: a capture that hits a host hole runs the segments
         # before the hole for real, so a failure after that has state to restore
-        contents = [(t, t.clone()) for t, _ in versions.values()]
+        # (a view with a zero stride over a dimension of size > 1 -- the LIDAR's expanded angle
+        # row -- cannot be written in place, so the step cannot have changed it)
+        contents = [(t, t.clone()) for t, _ in versions.values()
+                    if not any(st == 0 and n > 1 for st, n in zip(t.stride(), t.shape))]
         segs = _Segments(side)
         self._direct = DirectOutputs(dev) if self._DIRECT else None
         deferred: List[Any] = []
@@ -949,6 +996,7 @@ class StepGraph:
         self.graph = g
         self._segments, self._holes = segs.graphs, segs.holes
         self._raw_exec = None
+        self._chain = None
         self.replays = 0
         self.status = "graph"
         self.why = ""
@@ -1059,10 +1107,11 @@ class StepGraph:
                     fn, args, res = self._holes[i]
                     fn(*args, out=res)
             return
+        if self._chain is not None:  # the graph's kernels as plain launches (_KernelChain)
+            N.check(N.load_library().vmas_graph_chain_launch(self._chain.handle, N.stream_ptr(self._dev_index())),
+                    "vmas_graph_chain_launch")
+            return
         if self._raw_exec is not None:
-            from ... import _native as N
-
-            dev = self.env.device
             N.check(N.load_library().vmas_graph_launch(self._raw_exec, N.stream_ptr(self._dev_index())),
                     "vmas_graph_launch")
             return
@@ -1072,8 +1121,12 @@ class StepGraph:
         self.graph.replay()
         if self.replays == 0 and gen.get_offset() == before and self._RAW_LAUNCH:
             self._raw_exec = ctypes.c_void_p(self.graph.raw_cuda_graph_exec())
+            self._chain, self.chain_why = _KernelChain.build(self.graph) if self._CHAIN else (None, "off")
 
     _RAW_LAUNCH = os.environ.get("VMAS_GRAPH_RAW_LAUNCH", "1") != "0"  # (A/B knob)
+    # a replay whose graph is a short chain of kernel nodes launches them on the stream instead
+    # (_KernelChain); 0: hipGraphLaunch (A/B knob)
+    _CHAIN = os.environ.get("VMAS_GRAPH_CHAIN", "1") != "0"
     # fused programs write the step's outputs into fresh tensors (DirectOutputs); 0: copied out
     _DIRECT = os.environ.get("VMAS_GRAPH_DIRECT_OUTPUTS", "1") != "0"
     # fresh entity-state tensors on first use after each replay (_FreshState); 0: the states stay
