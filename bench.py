@@ -212,7 +212,9 @@ def kernel_source_hash(world) -> str:
     # include/): the kernel's identity is the source AND their text
     h = hashlib.sha256(src.encode())
     for f in ("vectorizedmultiagentsimulator_amd/csrc/vmas_jit_ops.hpp",
-              "vectorizedmultiagentsimulator_amd/csrc/vmas_physics.hpp", "include/vmas_mi355x.h"):
+              "vectorizedmultiagentsimulator_amd/csrc/vmas_physics.hpp", "include/vmas_mi355x.h") + (
+            ("vectorizedmultiagentsimulator_amd/csrc/vmas_programs.hpp",
+             "vectorizedmultiagentsimulator_amd/csrc/vmas_query.hpp") if '#include "vmas_programs.hpp"' in src else ()):
         h.update((ROOT / f).read_bytes())
     return h.hexdigest()
 
@@ -439,7 +441,9 @@ def main():
     g = getattr(env, "_graph", None)
     if g is not None and env.graph_status == "graph":
         # how a replay is launched: the graph's kernels on the stream, or hipGraphLaunch
-        step_mode += (f"; replay: {g._chain.n_nodes}-kernel chain" if g._chain is not None
+        step_mode += (f"; replay: {g._chain.n_nodes}-launch kernel chain"
+                      + (f" ({g._chain.fused} scenario program as k_world's epilogue)" if g._chain.fused else "")
+                      if g._chain is not None
                       else f"; replay: hipGraphLaunch ({g.chain_why or 'torch replay'})")
     if json.loads(args.kw):
         workload += f", {args.kw}"

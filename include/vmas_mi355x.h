@@ -44,7 +44,7 @@ extern "C" {
  * v4: VmasSpawnTargetsIO max_tries / backup; vmas_uniform_columns_snap
  * v5: VmasSpawnTargetsIO scratch / scratch_words (the windowed respawn), vmas_spawn_scratch_words;
  *     the fused programs' out_delta (direct outputs) and VMAS_COPY_STORE64 spans */
-#define VMAS_ABI_VERSION 5
+#define VMAS_ABI_VERSION 6
 
 /* error codes */
 #define VMAS_OK 0
@@ -141,7 +141,15 @@ typedef struct VmasWorldConfig {
     int32_t max_substeps;     /* capacity of the broadphase flag scratch */
     int32_t export_forces;    /* 1: the step fills VmasStepIO.out_fdict / out_tdict (World.forces_dict /
                                  torques_dict, core.py:1975-1992); 0: those pointers must be NULL */
+    int32_t epilogue;         /* (v6) VMAS_EPILOGUE_*: a scenario program the world-specialised module
+                                 also compiles, as its own kernel and as an optional k_world epilogue
+                                 (vmas_jit_program_outputs, vmas_graph_chain_build); ignored by
+                                 vmas_world_create */
+    int32_t pad_cfg;
 } VmasWorldConfig;
+#define VMAS_EPILOGUE_NONE 0
+#define VMAS_EPILOGUE_BALANCE 1 /* balance.py:205-262 (VmasBalanceIO) */
+#define VMAS_EPILOGUE_TRANSPORT 2 /* transport.py:130-190 (VmasTransportIO) */
 
 /* Per-call input pointers.  Strides are in elements (torch .stride()). */
 typedef struct VmasEntityIO {
@@ -234,7 +242,10 @@ int32_t vmas_graph_launch(void* graph_exec, void* stream);
 typedef struct VmasKernelChain VmasKernelChain;
 int32_t vmas_graph_chain_build(void* graph, int32_t max_nodes, VmasKernelChain** out_chain);
 int32_t vmas_graph_chain_launch(const VmasKernelChain* chain, void* stream);
-int32_t vmas_graph_chain_nodes(const VmasKernelChain* chain); /* kernels per launch (0: null chain) */
+int32_t vmas_graph_chain_nodes(const VmasKernelChain* chain); /* launches per replay (0: null chain) */
+/* k_world + k_program_jit node pairs of the graph that run as ONE launch (k_world with its module's
+ * scenario program as the epilogue, Args.epi set; VMAS_GRAPH_FUSE=0 disables) */
+int32_t vmas_graph_chain_fused(const VmasKernelChain* chain);
 int32_t vmas_graph_chain_free(VmasKernelChain* chain);
 /* Host waits on the device performed by the library so far (stream / event synchronisations and
  * spins on published words; wraps around): graph mode runs one step between two reads of it to
@@ -533,6 +544,10 @@ typedef struct VmasBalanceIO {
                                              (simulator/environment/_graph.py DirectOutputs); NULL: none */
 } VmasBalanceIO;
 int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream);
+/* Test utility (no reference counterpart): out[0, n) = the scenario programs' flag-independent
+ * IEEE division a / b (csrc/vmas_balance.hpp xdiv), out[n, 2n) = this build's `/`, out[2n, 3n) =
+ * xsqrt(a), out[3n, 4n) = sqrtf(a) -- equal bit for bit (tests/test_fused.py). */
+int32_t vmas_test_exact_math(int32_t device, const float* a, const float* b, float* out, int64_t n, void* stream);
 
 /* flocking (reference vmas/scenarios/flocking.py:149-206): replaces, for every policy agent at
  * once, Scenario.reward (the first policy agent's `t += 1` and pairwise collision rewards over
@@ -798,6 +813,14 @@ int32_t vmas_jit_world_device_timing(VmasJitWorld* world, int32_t reset, double*
                                      int64_t* launches, double* clock_ghz);
 /* Generated source of a world (length returned; copied into buf when buf != NULL). */
 int32_t vmas_jit_world_source(const VmasJitWorld* world, char* buf, int64_t cap);
+/* The scenario program the world's module was compiled with (VmasWorldConfig.epilogue; 0: none). */
+int32_t vmas_jit_world_epilogue(const VmasJitWorld* world);
+/* A scenario's per-step program launched from the world's module (kind = VmasWorldConfig.epilogue:
+ * VMAS_EPILOGUE_BALANCE with a VmasBalanceIO, reference balance.py:205-262, as vmas_balance_outputs;
+ * VMAS_EPILOGUE_TRANSPORT with a VmasTransportIO, transport.py:130-190, as vmas_transport_outputs):
+ * the same compiled code k_world runs as its epilogue when a replayed step graph fuses k_world and
+ * this launch (vmas_graph_chain_build); IEEE arithmetic, bit-identical to the library kernels. */
+int32_t vmas_jit_program_outputs(VmasJitWorld* world, int32_t kind, const void* io, void* stream);
 /* Generate + compile a world's kernel without a device (build checks); returns the source length. */
 int32_t vmas_jit_compile_check(const VmasWorldConfig* cfg, const VmasEntityDesc* entities,
                                const VmasPairDesc* pairs, const VmasJointDesc* joints, char* buf,

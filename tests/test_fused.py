@@ -220,3 +220,36 @@ def test_relaxed_trig_large_rotation_gpu(gpu_device):
     rep = O.compare_one_step(env.world)
     assert "VMAS_PHYS_RELAXED" in env.world.engine.jit_source()
     assert rep["ok"], rep
+
+
+@pytest.mark.gpu
+def test_exact_math_gpu(gpu_device):
+    """The scenario programs' flag-independent division and square root (csrc/vmas_programs.hpp
+    xdiv / xsqrt, compiled into the relaxed world modules) equal IEEE `/` and sqrtf bit for bit:
+    random bit patterns (normals, denormals, infinities, NaNs) plus edge values."""
+    import ctypes
+
+    from vectorizedmultiagentsimulator_amd import _native as N
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    n = 1 << 22
+    bits = torch.randint(-(1 << 31), (1 << 31) - 1, (2, n), generator=g, dtype=torch.int64).to(torch.int32)
+    ab = bits.view(torch.float32).clone()
+    edge = torch.tensor([0.0, -0.0, 1.0, -1.0, float("inf"), -float("inf"), float("nan"), 1e-45, -1e-45, 1e-38,
+                         3.4e38, float.fromhex("0x1.0p-96"), float.fromhex("0x1.0p-97"), 2.0, 0.5, 1e-30], dtype=torch.float32)
+    k = edge.numel()
+    ab[0, :k * k] = edge.repeat_interleave(k)
+    ab[1, :k * k] = edge.repeat(k)
+    ab[1, k * k:2 * k * k] = 3.0  # (ordinary denominators too)
+    ab[0, 2 * k * k:] = ab[0, 2 * k * k:].abs()  # half the square roots of non-negative values
+    a, b = ab[0].to(gpu_device), ab[1].to(gpu_device)
+    out = torch.empty(4 * n, device=gpu_device, dtype=torch.float32)
+    idx = torch.device(gpu_device).index or 0
+    N.check(N.load_library().vmas_test_exact_math(idx, a.data_ptr(), b.data_ptr(), out.data_ptr(), n,
+                                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+            "vmas_test_exact_math")
+    o = out.view(4, n).cpu()
+    for x, ref, what in ((o[0], o[1], "div"), (o[2], o[3], "sqrt")):
+        same = (x.view(torch.int32) == ref.view(torch.int32)) | (torch.isnan(x) & torch.isnan(ref))
+        bad = (~same).nonzero().flatten()
+        assert bad.numel() == 0, (what, bad[:5].tolist(), x[bad[:5]].tolist(), ref[bad[:5]].tolist())

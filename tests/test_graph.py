@@ -584,8 +584,9 @@ CHAIN_CASES = [("balance", dict(n_agents=4), 10), ("transport", dict(n_agents=4)
 @pytest.mark.parametrize("name,kw,substeps", CHAIN_CASES, ids=[c[0] for c in CHAIN_CASES])
 def test_kernel_chain_replay_matches_graph_launch_gpu(gpu_device, name, kw, substeps):
     """A replay launched as the captured graph's kernels on the stream (_KernelChain,
-    vmas_graph_chain_launch) gives bit-identical outputs and state to hipGraphLaunch of the same
-    graph, through a reset_at and a full reset."""
+    vmas_graph_chain_launch) -- balance's k_world running the scenario program as its epilogue --
+    gives bit-identical outputs and state to hipGraphLaunch of the same graph (two launches),
+    through a reset_at and a full reset."""
     envs = []
     for chain in (True, False):
         saved = _rng_save()
@@ -618,4 +619,7 @@ def test_kernel_chain_replay_matches_graph_launch_gpu(gpu_device, name, kw, subs
     assert b._graph._chain is None
     if name != "discovery":  # (discovery's graph holds the respawn's deferred channel launch)
         assert a._graph._chain is not None, a._graph.chain_why
-        assert a._graph._chain.n_nodes >= 2
+        # balance: k_world with the scenario program as its epilogue, one launch per replay
+        assert (a._graph._chain.n_nodes, a._graph._chain.fused) == ((1, 1) if name == "balance" else
+                                                                    (a._graph._chain.n_nodes, 0))
+        assert a._graph._chain.n_nodes >= (1 if name == "balance" else 2)

@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("VMAS_LIB_PATH") or Path(__file__).resolve().pare
 
 # ------------------------------------------------------------------------------------------------
 # constants mirrored from include/vmas_mi355x.h
-VMAS_ABI_VERSION = 5
+VMAS_ABI_VERSION = 6
 VMAS_SPHERE, VMAS_BOX, VMAS_LINE = 0, 1, 2
 (
     VMAS_PAIR_JOINT,
@@ -46,6 +46,7 @@ F_GRAVITY = 1 << 12
 BROADPHASE_BATCH = 0
 BROADPHASE_ENV = 1
 DIST_POINT, DIST_PAIR, OVERLAP_PAIR = 0, 1, 2
+EPILOGUE_NONE, EPILOGUE_BALANCE, EPILOGUE_TRANSPORT = 0, 1, 2  # VmasWorldConfig.epilogue
 
 # exported symbols (tests check the library exports every one of them)
 EXPORTED_SYMBOLS = (
@@ -58,9 +59,13 @@ EXPORTED_SYMBOLS = (
     "vmas_graph_chain_launch",
     "vmas_graph_chain_free",
     "vmas_graph_chain_nodes",
+    "vmas_graph_chain_fused",
+    "vmas_jit_world_epilogue",
+    "vmas_jit_program_outputs",
     "vmas_host_waits",
     "vmas_test_hold",
     "vmas_balance_outputs",
+    "vmas_test_exact_math",
     "vmas_copy_spans",
     "vmas_spawn_targets",
     "vmas_spawn_scratch_words",
@@ -196,6 +201,8 @@ class VmasWorldConfig(ctypes.Structure):
         ("has_y_semidim", _i32),
         ("max_substeps", _i32),
         ("export_forces", _i32),
+        ("epilogue", _i32),
+        ("pad_cfg", _i32),
     ]
 
 
@@ -536,6 +543,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_test_hold.argtypes = [_i32, _i32, ctypes.c_int64, _vp]
     lib.vmas_balance_outputs.restype = _i32
     lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
+    lib.vmas_test_exact_math.restype = _i32
+    lib.vmas_test_exact_math.argtypes = [_i32, _vp, _vp, _vp, ctypes.c_int64, _vp]
     lib.vmas_discovery_outputs.restype = _i32
     lib.vmas_discovery_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_transport_outputs.restype = _i32
@@ -581,6 +590,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_graph_chain_free.restype = _i32
     lib.vmas_graph_chain_nodes.restype = _i32
     lib.vmas_graph_chain_nodes.argtypes = [_vp]
+    lib.vmas_graph_chain_fused.restype = _i32
+    lib.vmas_graph_chain_fused.argtypes = [_vp]
     lib.vmas_graph_chain_free.argtypes = [_vp]
     lib.vmas_world_create.restype = _i32
     lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]
@@ -661,6 +672,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_jit_stats.restype = _i32
     lib.vmas_jit_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     lib.vmas_jit_last_error.restype = ctypes.c_char_p
+    lib.vmas_jit_world_epilogue.restype = _i32
+    lib.vmas_jit_world_epilogue.argtypes = [_vp]
+    lib.vmas_jit_program_outputs.restype = _i32
+    lib.vmas_jit_program_outputs.argtypes = [_vp, _i32, _vp, _vp]
     ver = lib.vmas_abi_version()
     if ver != VMAS_ABI_VERSION:
         raise NativeLibraryError(f"ABI version mismatch: library {ver}, python {VMAS_ABI_VERSION}")

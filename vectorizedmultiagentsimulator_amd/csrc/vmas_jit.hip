@@ -43,6 +43,7 @@
 
 #include "vmas_aux.hpp"
 #include "vmas_jit_ops.hpp"
+#include "vmas_jit_registry.hpp"
 
 #include <algorithm>
 #include <cstdarg>
@@ -363,7 +364,7 @@ struct Gen {
         // row buffer when it is large enough)
         const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 >= nfl + 2) ? 0 : nfl + 2;
         const long lds = (global_rows ? 0L : (long)n_rows * 256) + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) +
-                         4 * red;
+                         4 * red + (has_epi() && !epi_q_in_rows() ? 16L * 256 : 0L);
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
             return false;
@@ -401,9 +402,25 @@ struct Gen {
     // output pointers: pos, vel, rot, ang_vel, force, torque (+ forces_dict, torques_dict rows)
     size_t n_out() const { return cfg.export_forces ? 8 : 6; }
 
+    // a scenario program compiled into the module (VmasWorldConfig.epilogue): its own kernel and
+    // k_world's optional epilogue, whose argument block pointer is Args.epi
+    bool has_epi() const { return cfg.epilogue == VMAS_EPILOGUE_BALANCE || cfg.epilogue == VMAS_EPILOGUE_TRANSPORT; }
+    // the program's argument block (vmas_programs.hpp program_group overloads)
+    const char* epi_type() const { return cfg.epilogue == VMAS_EPILOGUE_BALANCE ? "VmasBalanceIO" : "VmasTransportIO"; }
+    // the call running the program for group g (vmas_programs.hpp balance_group / transport_group)
+    std::string epi_call(const std::string& io, const std::string& g, const std::string& wave, const std::string& lane,
+                         const std::string& q) const {
+        if (cfg.epilogue == VMAS_EPILOGUE_BALANCE)
+            return "balance_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ", " + q + ")";
+        return "transport_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ")";
+    }
+    bool epi_q_in_rows() const { return !global_rows && n_rows >= 16; }
+    // byte offset of Args.epi (after the fixed pointers: the value slots follow it)
+    size_t epi_offset() const { return 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)); }
+
     size_t arg_bytes() const {  // layout of the generated struct Args
         // (+4 ints: B, S, sdt, max_pass; then the value slots; padded to the 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)) +
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0) + (has_epi() ? 1 : 0)) +
                          4 * (std::max<size_t>(str_src.size(), 2) + 4) +
                          4 * prm_src.size();
         return (n + 7) & ~(size_t)7;
@@ -909,11 +926,14 @@ struct Gen {
             o += "#define VMAS_TRIG_GUARD 1\n";
         o += std::string(kFlagsTag) + codegen_flags(relaxed) + "\n";
         if (prof_block >= 0) o += "#define VMAS_JIT_PROFILE_SLOTS 1\n";
-        o += "#include \"vmas_jit_ops.hpp\"\nusing namespace vmas;\n\n";
+        o += "#include \"vmas_jit_ops.hpp\"\n";
+        if (has_epi()) o += "#include \"vmas_programs.hpp\"\n";
+        o += "using namespace vmas;\n\n";
         o += "struct Args {\n    const float* ptr[" + it(std::max<size_t>(ptr_src.size(), 1)) +
              "];\n    float* out[" + it(n_out()) + "];\n    uint32_t* mask;\n    uint32_t* blk;\n    unsigned long long* prof;\n"
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n" +
              std::string(global_rows ? "    float* rows;\n" : "") +
+             std::string(has_epi() ? std::string("    const ") + epi_type() + "* epi;\n" : std::string()) +
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n"
              "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
              "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
@@ -962,6 +982,7 @@ struct Gen {
         else
             o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
+        if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[16 * 64];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
         // idle between groups), else its own array; QL: steal list + broadcast word
@@ -1014,6 +1035,19 @@ struct Gen {
         for (int w = 0; w < nw; ++w)
             o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
         o += "                default: break;\n            }\n        }\n";
+        if (has_epi()) {
+            // The scenario program of this group (vmas_graph_chain_build fuses a replay's k_world and
+            // k_program_jit into this launch): it reads the group's fields the waves just stored --
+            // visible to the whole workgroup after the barrier (its workgroup-scope release /
+            // acquire; agent-scope fences here write back L2 per group: 38 -> 159 us per launch) --
+            // each pass of the fixed point re-running it after its group, the final pass's writes
+            // last (as the state outputs).  Q: the row buffer, idle between groups.
+            o += "        if (a.epi) {\n"
+                 "            __syncthreads();\n"
+                 "            " + epi_call("*a.epi", "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
+                 "            __syncthreads();\n"
+                 "        }\n";
+        }
         o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, &CUR,\n"
              "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
              "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
@@ -1027,6 +1061,11 @@ struct Gen {
              "}\n\n";
         const std::string bounds = "__launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) + ")";
         o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
+        if (has_epi())  // the eager step's launch of the same program (vmas_jit_program_outputs)
+            o += "\nextern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ") k_program_jit(" + epi_type() + " io_arg) {\n"
+                 "    VMAS_PROGRAM_ARGS(" + epi_type() + ", io_arg);\n"
+                 "    __shared__ float Q[16 * 64];\n"
+                 "    " + epi_call("io", "blockIdx.x", "(int)(threadIdx.x >> 6)", "(int)(threadIdx.x & 63)", "Q") + ";\n}\n";
     }
 };
 
@@ -1203,25 +1242,29 @@ int32_t compile(const std::string& src, std::vector<char>* code) {
 
 }  // namespace
 
-// The k_world functions of the loaded world modules: a kernel node of a captured step graph whose
-// function is one of these is a module launch (vmas_graph_chain_build, vmas_kernels.hip).
+// The kernels of the loaded world modules (k_world, k_program_jit): a kernel node of a captured
+// step graph whose function is one of these is a module launch, and a k_world node followed by its
+// module's k_program_jit node can run as one launch (vmas_graph_chain_build, vmas_kernels.hip).
 namespace vmas {
 namespace {
 std::mutex g_fn_mu;
-std::unordered_set<const void*> g_live_fns;
+std::unordered_map<const void*, JitFnInfo> g_live_fns;
 }  // namespace
-void fn_register(hipFunction_t f) {
+void fn_register(hipFunction_t f, const JitFnInfo& info) {
     std::lock_guard<std::mutex> lk(g_fn_mu);
-    g_live_fns.insert((const void*)f);
+    g_live_fns[(const void*)f] = info;
 }
 void fn_unregister(hipFunction_t f) {
     if (!f) return;
     std::lock_guard<std::mutex> lk(g_fn_mu);
     g_live_fns.erase((const void*)f);
 }
-bool jit_owns_function(const void* f) {
+bool jit_fn_info(const void* f, JitFnInfo* out) {
     std::lock_guard<std::mutex> lk(g_fn_mu);
-    return g_live_fns.count(f) != 0;
+    auto it = g_live_fns.find(f);
+    if (it == g_live_fns.end()) return false;
+    if (out) *out = it->second;
+    return true;
 }
 }  // namespace vmas
 
@@ -1237,6 +1280,8 @@ struct VmasJitWorld {
     int W = 1, nblk = 0, nw = kNW;
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;  // k_world
+    hipFunction_t fn_prog = nullptr;  // k_program_jit (cfg.epilogue: the scenario program's own kernel)
+    size_t epi_offset = 0;           // byte offset of Args.epi (epilogue modules)
     uint32_t *d_mask = nullptr, *d_blk = nullptr, *d_viol = nullptr, *h_viol = nullptr;
     // persistent launches: d_ctl = [kGridCtlWords control words | inverted mask words | claim word
     // per group (u64, kClaimStride apart, from grid_claim_offset)], zeroed at create and never
@@ -1281,6 +1326,7 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
     if (W->cfg.device >= 0) {
         (void)hipSetDevice(W->cfg.device);
         vmas::fn_unregister(W->fn);
+        vmas::fn_unregister(W->fn_prog);
         if (W->mod) (void)hipModuleUnload(W->mod);
         if (W->d_mask) (void)hipFree(W->d_mask);
         if (W->d_blk) (void)hipFree(W->d_blk);
@@ -1339,7 +1385,6 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         std::vector<char> code;
         if (int32_t rc = compile(g.src, &code)) return cleanup(rc);
         if (W->mod) {
-            vmas::fn_unregister(W->fn);
             W->fn = nullptr;
             (void)hipModuleUnload(W->mod);
             W->mod = nullptr;
@@ -1348,7 +1393,6 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             return cleanup(jfail(VMAS_E_HIP, "hipModuleLoadData"));
         if (hipModuleGetFunction(&W->fn, W->mod, "k_world") != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
-        vmas::fn_register(W->fn);
         int scratch = 0;
         (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
         if (scratch == 0 || g.nw == kNW) break;
@@ -1363,6 +1407,28 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
     W->W = g.W;
     W->nw = g.nw;
     W->nblk = (cfg->batch + 63) / 64;
+    if (g.has_epi()) {
+        if (hipModuleGetFunction(&W->fn_prog, W->mod, "k_program_jit") != hipSuccess)
+            return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction(k_program_jit)"));
+        W->epi_offset = g.epi_offset();
+    }
+    {
+        vmas::JitFnInfo info{};
+        info.kind = vmas::kJitFnWorld;
+        info.world = W;
+        info.world_fn = W->fn;
+        info.arg_bytes = W->arg_bytes;
+        info.epi_offset = W->fn_prog ? (long)W->epi_offset : -1L;
+        info.batch = cfg->batch;
+        info.epilogue = g.has_epi() ? cfg->epilogue : VMAS_EPILOGUE_NONE;
+        info.io_bytes = cfg->epilogue == VMAS_EPILOGUE_BALANCE ? sizeof(VmasBalanceIO)
+                        : cfg->epilogue == VMAS_EPILOGUE_TRANSPORT ? sizeof(VmasTransportIO) : 0;
+        vmas::fn_register(W->fn, info);
+        if (W->fn_prog) {
+            info.kind = vmas::kJitFnProgram;
+            vmas::fn_register(W->fn_prog, info);
+        }
+    }
     const size_t nwords = (size_t)cfg->max_substeps * W->W;
     if (hipMalloc((void**)&W->d_mask, nwords * 4) != hipSuccess ||
         hipMalloc((void**)&W->d_blk, (size_t)W->nblk * 2 * nwords * 4) != hipSuccess ||
@@ -1521,6 +1587,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(W->dh_err);
     put_ptr(W->timing && persistent ? W->d_tm : nullptr);
     if (W->global_rows) put_ptr(W->d_rows);
+    if (W->fn_prog) put_ptr(nullptr);  // Args.epi: no epilogue (the chain replay's fused launch sets it)
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
         int32_t v = 0;
@@ -1621,6 +1688,49 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     return jfail(VMAS_E_NOCONVERGE, "broadphase fixed point did not converge");
 }
 
+// The scenario program a world module was compiled with (VMAS_EPILOGUE_*).
+int32_t vmas_jit_world_epilogue(const VmasJitWorld* W) {
+    if (!W) return jfail(VMAS_E_INVALID, "null world");
+    return W->fn_prog ? W->cfg.epilogue : VMAS_EPILOGUE_NONE;
+}
+
+// A scenario program (VMAS_EPILOGUE_*: balance.py:205-262, transport.py:130-190) by the module's
+// k_program_jit: the code k_world runs as its epilogue when a replay fuses the two launches, so the
+// eager step and the replay agree bit for bit (both IEEE: vmas_programs.hpp).
+int32_t vmas_jit_program_outputs(VmasJitWorld* W, int32_t kind, const void* io_, void* stream) {
+    if (!W || !io_) return jfail(VMAS_E_INVALID, "null argument");
+    if (!W->fn_prog || kind != W->cfg.epilogue) return jfail(VMAS_E_INVALID, "the world module has no program %d", kind);
+    size_t size = 0;
+    alignas(16) char buf[sizeof(VmasBalanceIO) > sizeof(VmasTransportIO) ? sizeof(VmasBalanceIO) : sizeof(VmasTransportIO)];
+    if (kind == VMAS_EPILOGUE_BALANCE) {
+        const VmasBalanceIO* io = (const VmasBalanceIO*)io_;
+        if (io->batch != W->cfg.batch || io->n_agents < 0 || io->n_agents > VMAS_SCN_MAX_AGENTS)
+            return jfail(VMAS_E_INVALID, "vmas_jit_program_outputs(balance): bad arguments");
+        if (io->package.shape != VMAS_SPHERE || io->goal.shape != VMAS_SPHERE || io->line.shape != VMAS_LINE ||
+            io->floor.shape != VMAS_BOX)
+            return jfail(VMAS_E_INVALID, "vmas_jit_program_outputs(balance): unexpected entity shapes");
+        size = sizeof *io;
+    } else {
+        const VmasTransportIO* io = (const VmasTransportIO*)io_;
+        if (io->batch != W->cfg.batch || io->n_agents < 0 || io->n_agents > VMAS_TRANSPORT_MAX_AGENTS ||
+            io->n_packages < 0 || io->n_packages > VMAS_TRANSPORT_MAX_PACKAGES)
+            return jfail(VMAS_E_INVALID, "vmas_jit_program_outputs(transport): bad arguments");
+        for (int i = 0; i < io->n_packages; ++i)
+            if (io->package[i].shape != VMAS_BOX || io->goal[i].shape != VMAS_SPHERE)
+                return jfail(VMAS_E_INVALID, "vmas_jit_program_outputs(transport): package %d is not (box, sphere goal)", i);
+        if (io->n_agents > 0 && W->nw < 2) return jfail(VMAS_E_INVALID, "vmas_jit_program_outputs: too few waves");
+        size = sizeof *io;
+    }
+    memcpy(buf, io_, size);
+    int cur = -1;
+    JHIP(hipGetDevice(&cur));
+    if (cur != W->cfg.device) JHIP(hipSetDevice(W->cfg.device));
+    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    JHIP(hipModuleLaunchKernel(W->fn_prog, (W->cfg.batch + 63) / 64, 1, 1, (uint32_t)W->nw * 64, 1, 1, 0,
+                               (hipStream_t)stream, nullptr, extra));
+    return VMAS_OK;
+}
+
 // Passes the last step ran (waits for it).  Also reports a device-side fixed-point failure.
 int32_t vmas_jit_world_passes(VmasJitWorld* W, int32_t* passes) {
     if (!W) return jfail(VMAS_E_INVALID, "null world");
@@ -1652,7 +1762,7 @@ int32_t vmas_jit_world_set_params(VmasJitWorld* W, const VmasWorldConfig* cfg, c
         cfg->collision_force != c.collision_force || cfg->joint_force != c.joint_force ||
         cfg->torque_constraint_force != c.torque_constraint_force || cfg->has_world_gravity != c.has_world_gravity ||
         cfg->has_x_semidim != c.has_x_semidim || cfg->has_y_semidim != c.has_y_semidim ||
-        cfg->max_substeps != c.max_substeps || cfg->export_forces != c.export_forces)
+        cfg->max_substeps != c.max_substeps || cfg->export_forces != c.export_forces || cfg->epilogue != c.epilogue)
         return jfail(VMAS_E_INVALID, "set_params: the world configuration differs in structure");
     for (int e = 0; e < c.n_entities; ++e) {
         const VmasEntityDesc &a = W->ed[e], &b = entities[e];

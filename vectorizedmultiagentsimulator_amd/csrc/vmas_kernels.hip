@@ -32,6 +32,7 @@
 #include "vmas_aux.hpp"
 #include "vmas_physics.hpp"
 #include "vmas_query.hpp"
+#include "vmas_jit_registry.hpp"
 
 using namespace vmas;
 
@@ -883,9 +884,6 @@ std::vector<CheckScratch*> g_checks;
 
 // ================================================================================================
 // C ABI
-namespace vmas {
-bool jit_owns_function(const void* f);  // vmas_jit.hip: a loaded world module's k_world
-}
 constexpr int kChainMaxNodes = VMAS_GRAPH_CHAIN_MAX;
 
 extern "C" {
@@ -940,15 +938,109 @@ int32_t vmas_graph_launch(void* graph_exec, void* stream) {
 // starts ~2.3 us later than after a stream kernel -- ~7 us of every C2 step of ~56 us.  The
 // nodes' parameters (function, grid, kernel arguments) stay owned by the kept graph
 // (torch.cuda.CUDAGraph(keep_graph=True)), which must outlive the chain.
-struct VmasKernelChain {
-    int n = 0;
-    hipFunction_t fn[kChainMaxNodes];
-    hipKernelNodeParams p[kChainMaxNodes];
+struct ChainNode {
+    hipFunction_t fn;
+    dim3 grid, block;
+    unsigned shmem;
+    void** kernel_params;  // the graph node's (owned by the graph)
+    void** extra;          // the graph node's, or a FusedArgs' below
 };
+// A k_world launch that also runs its module's scenario program as the epilogue: the node's argument
+// block with Args.epi pointing at a device copy of the k_program_jit node's argument block.
+struct FusedArgs {
+    std::vector<char> buf;
+    size_t size = 0;
+    void* extra[5];
+};
+struct VmasKernelChain {
+    int n = 0, fused = 0;
+    ChainNode node[kChainMaxNodes];
+    std::vector<std::unique_ptr<FusedArgs>> args;
+    std::vector<void*> dev;  // device copies of the epilogue argument blocks
+};
+
+namespace {
+// Device copies of chains freed since: released at the next build (a chain may be dropped while
+// another stream is being captured, where hipFree is not allowed).
+std::mutex g_chain_free_mu;
+std::vector<void*> g_chain_free;
+
+// The argument block of a captured kernel node whose kernel takes one struct by value: from the
+// node's `extra` buffer (module launches with HIP_LAUNCH_PARAM_BUFFER_POINTER) or its first
+// kernel parameter.  NULL if neither holds at least `expect` bytes.
+const char* node_arg_block(const hipKernelNodeParams& p, size_t expect) {
+    if (p.extra) {
+        const void* buf = nullptr;
+        size_t sz = 0;
+        for (int i = 0; i < 8 && p.extra[i] != HIP_LAUNCH_PARAM_END; i += 2) {
+            if (p.extra[i] == HIP_LAUNCH_PARAM_BUFFER_POINTER) buf = p.extra[i + 1];
+            else if (p.extra[i] == HIP_LAUNCH_PARAM_BUFFER_SIZE) sz = *(const size_t*)p.extra[i + 1];
+            else return nullptr;
+        }
+        return buf && sz >= expect ? (const char*)buf : nullptr;
+    }
+    return p.kernelParams && p.kernelParams[0] ? (const char*)p.kernelParams[0] : nullptr;
+}
+
+// A program may run as k_world's epilogue when every per-env input it reads is a per-env row (no
+// stride-0 view: a row k_world writes for one env must not be read for another).
+bool balance_io_fusable(const VmasBalanceIO& io, int batch) {
+    if (io.batch != batch || io.n_agents < 0 || io.n_agents > VMAS_SCN_MAX_AGENTS) return false;
+    if (io.package.shape != VMAS_SPHERE || io.goal.shape != VMAS_SPHERE || io.line.shape != VMAS_LINE ||
+        io.floor.shape != VMAS_BOX)
+        return false;
+    for (const VmasShapeRef* r : {&io.package, &io.goal, &io.line, &io.floor})
+        if (!r->pos || r->pos_s0 == 0 || (r->rot && r->rot_s0 == 0)) return false;
+    if ((io.what & VMAS_SCN_REWARD) && io.gs_s0 == 0) return false;
+    if (io.what & VMAS_SCN_OBS) {
+        for (const VmasVec* v : {&io.package_vel, &io.line_vel, &io.line_ang_vel})
+            if (!v->p || v->s0 == 0) return false;
+        for (int i = 0; i < io.n_agents; ++i)
+            if (!io.agent_pos[i].p || io.agent_pos[i].s0 == 0 || !io.agent_vel[i].p || io.agent_vel[i].s0 == 0)
+                return false;
+    }
+    return true;
+}
+bool transport_io_fusable(const VmasTransportIO& io, int batch) {
+    if (io.batch != batch || io.n_agents < 0 || io.n_agents > VMAS_TRANSPORT_MAX_AGENTS || io.n_packages < 0 ||
+        io.n_packages > VMAS_TRANSPORT_MAX_PACKAGES)
+        return false;
+    for (int i = 0; i < io.n_packages; ++i) {
+        for (const VmasShapeRef* r : {&io.package[i], &io.goal[i]})
+            if (!r->pos || r->pos_s0 == 0 || (r->rot && r->rot_s0 == 0)) return false;
+        if (io.package[i].shape != VMAS_BOX || io.goal[i].shape != VMAS_SPHERE) return false;
+        if ((io.what & VMAS_SCN_REWARD) && io.gs_s0[i] == 0) return false;
+        if ((io.what & VMAS_SCN_OBS) && (!io.package_vel[i].p || io.package_vel[i].s0 == 0)) return false;
+    }
+    if (io.what & VMAS_SCN_OBS)
+        for (int i = 0; i < io.n_agents; ++i)
+            if (!io.agent_pos[i].p || io.agent_pos[i].s0 == 0 || !io.agent_vel[i].p || io.agent_vel[i].s0 == 0)
+                return false;
+    return true;
+}
+bool program_io_fusable(int kind, const char* io, int batch) {
+    if (kind == VMAS_EPILOGUE_BALANCE) {
+        VmasBalanceIO x;
+        memcpy(&x, io, sizeof x);
+        return balance_io_fusable(x, batch);
+    }
+    if (kind == VMAS_EPILOGUE_TRANSPORT) {
+        VmasTransportIO x;
+        memcpy(&x, io, sizeof x);
+        return transport_io_fusable(x, batch);
+    }
+    return false;
+}
+}  // namespace
 
 int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain** out) {
     if (!graph_ || !out) return fail(VMAS_E_INVALID, "vmas_graph_chain_build: null argument");
     *out = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_chain_free_mu);
+        for (void* d : g_chain_free) (void)hipFree(d);
+        g_chain_free.clear();
+    }
     const hipGraph_t graph = (hipGraph_t)graph_;
     max_nodes = std::min<int32_t>(max_nodes, kChainMaxNodes);
     size_t n = 0;
@@ -989,7 +1081,9 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
         }
     }
     if (root < 0) return fail(VMAS_E_UNSUPPORTED, "graph has no root");
-    std::unique_ptr<VmasKernelChain> c(new VmasKernelChain());
+    // the nodes in chain order, their functions resolved
+    std::vector<hipKernelNodeParams> prm(n);
+    std::vector<hipFunction_t> fns(n);
     std::vector<char> used(n, 0);
     int cur = root;
     for (size_t k = 0; k < n; ++k) {
@@ -1001,17 +1095,16 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
             return fail(VMAS_E_HIP, "hipGraphKernelNodeGetParams");
         }
         if (!p.func || (!p.kernelParams && !p.extra)) return fail(VMAS_E_UNSUPPORTED, "kernel node without function / arguments");
-        // a registered host stub (hipLaunchKernelGGL, torch's kernels) or a world module's k_world
+        // a registered host stub (hipLaunchKernelGGL, torch's kernels) or a world module's kernel
         hipFunction_t f = nullptr;
         if (hipGetFuncBySymbol(&f, p.func) != hipSuccess || !f) {
             (void)hipGetLastError();
-            if (!vmas::jit_owns_function(p.func)) return fail(VMAS_E_UNSUPPORTED, "kernel node %d: unknown function", (int)k);
+            if (!vmas::jit_fn_info(p.func, nullptr)) return fail(VMAS_E_UNSUPPORTED, "kernel node %d: unknown function", (int)k);
             f = (hipFunction_t)p.func;
         }
-        c->fn[k] = f;
-        c->p[k] = p;
-        // the next node: the one whose dependency is this one (at most one)
-        int next = -1;
+        prm[k] = p;
+        fns[k] = f;
+        int next = -1;  // the node whose dependency is this one (at most one)
         for (size_t i = 0; i < n; ++i)
             if (dep[i] == nodes[cur]) {
                 if (next >= 0) return fail(VMAS_E_UNSUPPORTED, "graph node has two dependents");
@@ -1020,7 +1113,47 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
         if (k + 1 < n && next < 0) return fail(VMAS_E_UNSUPPORTED, "graph is not a chain");
         cur = next;
     }
-    c->n = (int)n;
+    std::unique_ptr<VmasKernelChain> c(new VmasKernelChain());
+    const char* fz = getenv("VMAS_GRAPH_FUSE");  // 0: no k_world epilogue (A/B)
+    const bool fuse = !(fz && fz[0] == '0');
+    for (size_t k = 0; k < n; ++k) {
+        const hipKernelNodeParams& p = prm[k];
+        ChainNode nd{fns[k], p.gridDim, p.blockDim, p.sharedMemBytes, p.kernelParams, p.extra};
+        vmas::JitFnInfo a{}, b{};
+        if (fuse && k + 1 < n && vmas::jit_fn_info(p.func, &a) && a.kind == vmas::kJitFnWorld && a.epi_offset >= 0 &&
+            vmas::jit_fn_info(prm[k + 1].func, &b) && b.kind == vmas::kJitFnProgram && b.world == a.world) {
+            const char* wa = node_arg_block(p, a.arg_bytes);
+            const char* io = node_arg_block(prm[k + 1], b.io_bytes);
+            if (wa && io && program_io_fusable(a.epilogue, io, a.batch)) {
+                void* d = nullptr;
+                if (hipMalloc(&d, b.io_bytes) != hipSuccess || hipMemcpy(d, io, b.io_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+                    (void)hipGetLastError();
+                    if (d) (void)hipFree(d);
+                    for (void* x : c->dev) (void)hipFree(x);
+                    return fail(VMAS_E_HIP, "vmas_graph_chain_build: epilogue argument copy");
+                }
+                c->dev.push_back(d);
+                std::unique_ptr<FusedArgs> fa(new FusedArgs());
+                fa->buf.assign(wa, wa + a.arg_bytes);
+                memcpy(fa->buf.data() + a.epi_offset, &d, sizeof d);
+                fa->size = a.arg_bytes;
+                fa->extra[0] = HIP_LAUNCH_PARAM_BUFFER_POINTER;
+                fa->extra[1] = fa->buf.data();
+                fa->extra[2] = HIP_LAUNCH_PARAM_BUFFER_SIZE;
+                fa->extra[3] = &fa->size;
+                fa->extra[4] = HIP_LAUNCH_PARAM_END;
+                nd.fn = a.world_fn;
+                nd.kernel_params = nullptr;
+                nd.extra = fa->extra;
+                c->args.push_back(std::move(fa));
+                c->node[c->n++] = nd;
+                ++c->fused;
+                ++k;  // (the balance node runs inside this launch)
+                continue;
+            }
+        }
+        c->node[c->n++] = nd;
+    }
     *out = c.release();
     return VMAS_OK;
 }
@@ -1028,10 +1161,9 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
 int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) {
     if (!c || c->n <= 0) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch: empty chain");
     for (int k = 0; k < c->n; ++k) {
-        const hipKernelNodeParams& p = c->p[k];
-        const hipError_t e = hipModuleLaunchKernel(c->fn[k], p.gridDim.x, p.gridDim.y, p.gridDim.z, p.blockDim.x,
-                                                   p.blockDim.y, p.blockDim.z, p.sharedMemBytes, (hipStream_t)stream,
-                                                   p.kernelParams, p.extra);
+        const ChainNode& d = c->node[k];
+        const hipError_t e = hipModuleLaunchKernel(d.fn, d.grid.x, d.grid.y, d.grid.z, d.block.x, d.block.y, d.block.z,
+                                                   d.shmem, (hipStream_t)stream, d.kernel_params, d.extra);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             return fail(VMAS_E_HIP, "vmas_graph_chain_launch: node %d: %s", k, hipGetErrorString(e));
@@ -1042,7 +1174,13 @@ int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) {
 
 int32_t vmas_graph_chain_nodes(const VmasKernelChain* c) { return c ? c->n : 0; }
 
+int32_t vmas_graph_chain_fused(const VmasKernelChain* c) { return c ? c->fused : 0; }
+
 int32_t vmas_graph_chain_free(VmasKernelChain* c) {
+    if (c && !c->dev.empty()) {
+        std::lock_guard<std::mutex> lk(g_chain_free_mu);
+        g_chain_free.insert(g_chain_free.end(), c->dev.begin(), c->dev.end());
+    }
     delete c;
     return VMAS_OK;
 }

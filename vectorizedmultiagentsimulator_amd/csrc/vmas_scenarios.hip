@@ -13,6 +13,7 @@
 
 #include "vmas_aux.hpp"
 #include "vmas_mi355x.h"
+#include "vmas_programs.hpp"
 #include "vmas_query.hpp"
 
 using namespace vmas;
@@ -25,40 +26,6 @@ namespace {
 // range-reduced sincosf.  (Ray angles are the sensor's [0, 2 pi) plus the agent's rotation.)
 constexpr float kFastTrigMaxAngle = 16.f;
 
-__device__ __forceinline__ V2 ld_vec2(const VmasVec& v, int b) {
-    return mk(v.p[(long)b * v.s0], v.p[(long)b * v.s0 + v.s1]);
-}
-__device__ __forceinline__ float ld_vec1(const VmasVec& v, int b) { return v.p[(long)b * v.s0]; }
-
-// torch.remainder(a, b) for floating point (ATen's remainder kernel): fmod, moved into the sign
-// of the divisor
-__device__ __forceinline__ float torch_remainder(float a, float b) {
-    float mod = fmodf(a, b);
-    if ((mod != 0.f) && ((b < 0.f) != (mod < 0.f))) mod = mod + b;
-    return mod;
-}
-
-// Graph mode's direct outputs (simulator/environment/_graph.py DirectOutputs): the byte offsets from
-// the captured step's obs / rewards / done buffers to this replay's fresh output tensors, written by
-// the previous post-replay launch; out_delta NULL (every eager launch): in place.
-struct OutDelta {
-    long long obs, rew, done;
-};
-template <class IO>
-__device__ __forceinline__ OutDelta load_out_delta(IO& io) {
-    OutDelta o{0, 0, 0};
-    if (io.out_delta) {
-        o.obs = io.out_delta[0];
-        o.rew = io.out_delta[1];
-        o.done = io.out_delta[2];
-    }
-    return o;
-}
-template <class T>
-__device__ __forceinline__ T* moved(T* p, long long d) {
-    return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + d);
-}
-
 // balance.py:205-262 (restated in scenarios/balance.py): reward of the first agent (on-the-ground
 // test, package-goal distance, ground / position rewards and the global shaping update), every
 // agent's reward (ground_rew + pos_rew), every agent's 16-entry observation, and done
@@ -69,8 +36,9 @@ __device__ __forceinline__ T* moved(T* p, long long d) {
 // 1 + k are the observations of agents 4k .. 4k + 3, one per wave.  (One 64-thread workgroup per
 // (group, part), the box-line distance in one chain: 11 us per step at 32 768 envs, the chain's
 // latency at two waves per CU; before that 128 x 1 workgroups took 16 us.)
-__global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
-    __shared__ float Q[4][4][64];  // [side][q1.x, q1.y, q2.x, q2.y][lane]
+__global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io_arg) {
+    VMAS_PROGRAM_ARGS(VmasBalanceIO, io_arg);
+    __shared__ float Q[16 * 64];  // [side][q1.x, q1.y, q2.x, q2.y][lane] (vmas_programs.hpp bal_q)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
@@ -79,69 +47,19 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io) {
     if (blockIdx.y == 0) {
         if (!(io.what & VMAS_SCN_REWARD)) {
             if (wave != 0 || !valid || !(io.what & VMAS_SCN_DONE)) return;
-            const bool og = io.on_the_ground[b] != 0;
-            moved(io.done, od.done)[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
+            bal_done(io, b, io.on_the_ground[b] != 0, od);
             return;
         }
-        {  // side `wave` of closest_line_box(floor, line) (get_distance's box-line branch)
-            const VmasShapeRef &fl = io.floor, &ln = io.line;
-            const float rb = ref_rot(ln, bb);
-            const Pts q = bl_part(ref_pos(fl, bb), make_trig(ref_rot(fl, bb)), fl.length / 2.f, fl.width / 2.f,
-                                  ref_pos(ln, bb), Trig{cosf(rb), sinf(rb), 0.f, 0.f}, ln.length / 2.f, wave);
-            Q[wave][0][lane] = q.p1.x;
-            Q[wave][1][lane] = q.p1.y;
-            Q[wave][2][lane] = q.p2.x;
-            Q[wave][3][lane] = q.p2.y;
-        }
+        bal_side(io, bb, wave, lane, Q);  // side `wave` of closest_line_box(floor, line)
         __syncthreads();
         if (wave != 0 || !valid) return;
-        V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
-        float bd = INFINITY;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const V2 q1 = mk(Q[i][0][lane], Q[i][1][lane]), q2 = mk(Q[i][2][lane], Q[i][3][lane]);
-            const float d = norm(q1 - q2);
-            if (d < bd) {
-                bd = d;
-                c1 = q1;
-                c2 = q2;
-            }
-        }
-        const V2 pkg = ref_pos(io.package, b), goal = ref_pos(io.goal, b);
-        // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
-        // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
-        const bool og = (norm(c1 - c2) - kLineMinDist < 0.f) || overlap_box_sphere(io.floor, io.package, b);
-        io.on_the_ground[b] = og ? 1 : 0;
-        const float dist = norm(pkg - goal);  // vector_norm(package.pos - goal.pos, dim=1)
-        io.package_dist[b] = dist;
-        const float ground = og ? io.fall_reward : 0.f;  // zeros, masked_fill_(on_the_ground, fall)
-        io.ground_rew[b] = ground;
-        const float gs = dist * io.shaping_factor;
-        const float pos_rew = io.global_shaping[(long)b * io.gs_s0] - gs;
-        io.global_shaping_out[b] = gs;
-        if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
-        io.pos_rew[b] = pos_rew;
-        const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
-        for (int i = 0; i < io.n_agents; ++i) moved(io.rewards[i], od.rew)[b] = r;
-        if (io.what & VMAS_SCN_DONE)  // done = on_the_ground + is_overlapping(package, goal)
-            moved(io.done, od.done)[b] = (og || dist_pair(io.package, io.goal, b) < 0.f) ? 1 : 0;
+        bal_reward(io, b, lane, od, Q);
         return;
     }
     // agent i's observation
     const int i = (blockIdx.y - 1) * 4 + wave;
     if (i >= io.n_agents || !valid) return;
-    const V2 pkg = ref_pos(io.package, b), goal = ref_pos(io.goal, b);
-    const V2 lpos = ref_pos(io.line, b), pv = ld_vec2(io.package_vel, b), lv = ld_vec2(io.line_vel, b);
-    const float law = ld_vec1(io.line_ang_vel, b);
-    const float lrot = torch_remainder(ref_rot(io.line, b), io.pi);
-    const V2 pg = pkg - goal;
-    const V2 p = ld_vec2(io.agent_pos[i], b), v = ld_vec2(io.agent_vel[i], b);
-    const V2 dp = p - pkg, dl = p - lpos;
-    float4* dst = reinterpret_cast<float4*>(moved(io.obs[i], od.obs) + (long)b * 16);
-    dst[0] = make_float4(p.x, p.y, v.x, v.y);
-    dst[1] = make_float4(dp.x, dp.y, dl.x, dl.y);
-    dst[2] = make_float4(pg.x, pg.y, pv.x, pv.y);
-    dst[3] = make_float4(lv.x, lv.y, law, lrot);
+    bal_obs(io, b, i, od);
 }
 
 // The flocking separation term sums n floats in the order of torch's .mean(-1) over a contiguous
@@ -423,63 +341,13 @@ __global__ void __launch_bounds__(256) k_flocking_target(const float* t, int bat
 // 0 the reward (every package) + done, 1 + i agent i's observation.  An observation part of a
 // launch that also computes the reward recomputes on_goal (is_overlapping, deterministic) rather
 // than reading part 0's output.
-__global__ void __launch_bounds__(64) k_transport(VmasTransportIO io) {
-    constexpr int MP = VMAS_TRANSPORT_MAX_PACKAGES;
+__global__ void __launch_bounds__(64) k_transport(VmasTransportIO io_arg) {
+    VMAS_PROGRAM_ARGS(VmasTransportIO, io_arg);
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= io.batch) return;
-    const int part = blockIdx.y, np = io.n_packages;
     const OutDelta od = load_out_delta(io);
-    if (part == 0) {
-        bool all_on = true;
-        if (io.what & VMAS_SCN_REWARD) {
-            float rew = 0.f;  // self.rew = zeros
-#pragma unroll
-            for (int i = 0; i < MP; ++i) {
-                if (i >= np) continue;
-                const float dist = norm(ref_pos(io.package[i], b) - ref_pos(io.goal[i], b));
-                const bool on = overlap_box_sphere(io.package[i], io.goal[i], b);
-                io.dist_to_goal[i][b] = dist;
-                io.on_goal[i][b] = on ? 1 : 0;
-                const float* c = on ? io.green : io.red;  // where(on_goal, green, red)
-                io.color[i][(long)b * 3 + 0] = c[0];
-                io.color[i][(long)b * 3 + 1] = c[1];
-                io.color[i][(long)b * 3 + 2] = c[2];
-                const float shaping = dist * io.shaping_factor;
-                rew = rew + (on ? 0.f : io.global_shaping[i][(long)b * io.gs_s0[i]] - shaping);
-                io.global_shaping_out[i][b] = shaping;
-                all_on = all_on && on;
-            }
-            moved(io.rew, od.rew)[b] = rew;
-        } else if (io.what & VMAS_SCN_DONE) {
-#pragma unroll
-            for (int i = 0; i < MP; ++i)
-                if (i < np) all_on = all_on && io.on_goal_in[i][b] != 0;
-        }
-        if (io.what & VMAS_SCN_DONE) moved(io.done, od.done)[b] = all_on ? 1 : 0;  // all(stack(on_goal), -1)
-        return;
-    }
-    const int a = part - 1;
-    const V2 p = ld_vec2(io.agent_pos[a], b), v = ld_vec2(io.agent_vel[a], b);
-    float* o = moved(io.obs[a], od.obs) + (long)b * (4 + 7 * np);
-    o[0] = p.x;
-    o[1] = p.y;
-    o[2] = v.x;
-    o[3] = v.y;
-#pragma unroll
-    for (int i = 0; i < MP; ++i) {
-        if (i >= np) continue;
-        const V2 pp = ref_pos(io.package[i], b), gp = ref_pos(io.goal[i], b), pv = ld_vec2(io.package_vel[i], b);
-        const bool on = (io.what & VMAS_SCN_REWARD) ? overlap_box_sphere(io.package[i], io.goal[i], b)
-                                                     : io.on_goal_in[i][b] != 0;
-        float* q = o + 4 + 7 * i;
-        q[0] = pp.x - gp.x;
-        q[1] = pp.y - gp.y;
-        q[2] = pp.x - p.x;
-        q[3] = pp.y - p.y;
-        q[4] = pv.x;
-        q[5] = pv.y;
-        q[6] = on ? 1.f : 0.f;
-    }
+    if (blockIdx.y == 0) tr_reward_done(io, b, od);
+    else tr_obs(io, b, blockIdx.y - 1, od);
 }
 
 // (the REWARD launch, workgroup 0) a spawn channel's armed words into the step's respawn words
@@ -924,9 +792,28 @@ __global__ void __launch_bounds__(256) k_discovery_obs_split(VmasDiscoveryIO io_
     for (int k = lane + s * 64; k < nv * W; k += 64 * L) obs[k] = S[sub][k];
 }
 
+// Test kernel (tests/test_fused.py test_exact_math_gpu): the flag-independent division / square
+// root of vmas_programs.hpp next to this translation unit's IEEE `/` and sqrtf.
+__global__ void k_test_exact_math(const float* a, const float* b, float* out, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = xdiv(a[i], b[i]);
+    out[n + i] = a[i] / b[i];
+    out[2 * n + i] = xsqrt(a[i]);
+    out[3 * n + i] = sqrtf(a[i]);
+}
+
 }  // namespace
 
 extern "C" {
+
+int32_t vmas_test_exact_math(int32_t device, const float* a, const float* b, float* out, int64_t n, void* stream) {
+    if (device < 0 || !a || !b || !out || n <= 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_test_exact_math: bad arguments");
+    VMAS_AUX_HIP(hipSetDevice(device));
+    hipLaunchKernelGGL(k_test_exact_math, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a, b, out, (long)n);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
 
 int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stream) {
     if (!io || device < 0 || io->batch <= 0 || io->n_agents < 0 || io->n_agents > VMAS_SCN_MAX_AGENTS)

@@ -60,6 +60,10 @@ class Scenario(BaseScenario):
 
         self.pos_rew = torch.zeros(batch_dim, device=device, dtype=torch.float32)
         self.ground_rew = self.pos_rew.clone()
+        # the fused program below is also compiled into the world's specialised module: the eager
+        # step launches it from there, and a replayed step runs it as k_world's epilogue
+        # (csrc/vmas_programs.hpp; simulator/environment/_graph.py _KernelChain)
+        world._jit_epilogue = N.EPILOGUE_BALANCE
         return world
 
     def _column(self, env_index, low, high):
@@ -228,8 +232,13 @@ class Scenario(BaseScenario):
             io.on_the_ground = og.data_ptr()
             out["done"] = direct[2][0] if direct[2] else torch.empty(B, device=dev, dtype=torch.bool)
             io.done = out["done"].data_ptr()
-        _fused.check(_fused.lib().vmas_balance_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
-                     "vmas_balance_outputs")
+        jit = w.engine.jit_program(N.EPILOGUE_BALANCE)
+        if jit is not None:  # (the world module's k_program_jit: the code a replay runs as k_world's epilogue)
+            N.check_jit(_fused.lib().vmas_jit_program_outputs(jit, N.EPILOGUE_BALANCE, ctypes.byref(io), _fused.stream(w)),
+                        "vmas_jit_program_outputs")
+        else:
+            _fused.check(_fused.lib().vmas_balance_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
+                         "vmas_balance_outputs")
         if what & N.VMAS_SCN_REWARD:
             _fused.bump_version(self.ground_rew)
             if io.pos_rew_prev:

@@ -49,6 +49,9 @@ class Scenario(BaseScenario):
             package.goal = goal
             self.packages.append(package)
             world.add_landmark(package)
+        # the fused program is also compiled into the world's specialised module (csrc/vmas_programs.hpp):
+        # the eager step launches it from there, a replayed step runs it as k_world's epilogue
+        world._jit_epilogue = N.EPILOGUE_TRANSPORT
         return world
 
     def reset_world_at(self, env_index: int = None):
@@ -184,8 +187,13 @@ class Scenario(BaseScenario):
         if what & N.VMAS_SCN_DONE:
             out["done"] = direct[2][0] if direct[2] else torch.empty(B, device=dev, dtype=torch.bool)
             io.done = out["done"].data_ptr()
-        _fused.check(_fused.lib().vmas_transport_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
-                     "vmas_transport_outputs")
+        jit = w.engine.jit_program(N.EPILOGUE_TRANSPORT)
+        if jit is not None:  # (the world module's k_program_jit: the code a replay runs as k_world's epilogue)
+            N.check_jit(_fused.lib().vmas_jit_program_outputs(jit, N.EPILOGUE_TRANSPORT, ctypes.byref(io),
+                                                              _fused.stream(w)), "vmas_jit_program_outputs")
+        else:
+            _fused.check(_fused.lib().vmas_transport_outputs(dev.index, ctypes.byref(io), _fused.stream(w)),
+                         "vmas_transport_outputs")
         if what & N.VMAS_SCN_REWARD:
             self.rew = out["rew"]
             for i, p in enumerate(self.packages):

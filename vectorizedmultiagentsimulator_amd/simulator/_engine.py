@@ -364,6 +364,11 @@ class PhysicsEngine:
         cfg.y_semidim = _f32(w._y_semidim) if w._y_semidim is not None else 0.0
         cfg.max_substeps = max_substeps
         cfg.export_forces = int(bool(w.export_forces))
+        # a scenario program the world module also compiles (its own kernel + k_world's epilogue;
+        # set by the scenario's make_world, e.g. balance)
+        # (VMAS_JIT_EPILOGUE=0: none, an A/B knob)
+        cfg.epilogue = (int(getattr(w, "_jit_epilogue", N.EPILOGUE_NONE))
+                        if os.environ.get("VMAS_JIT_EPILOGUE", "1") != "0" else N.EPILOGUE_NONE)
         handle = ctypes.c_void_p()
         N.check(self.lib.vmas_world_create(ctypes.byref(cfg), ed, pd, jd, ctypes.byref(handle)),
                 "vmas_world_create")
@@ -500,6 +505,16 @@ class PhysicsEngine:
         out = np.zeros(n, dtype=np.uint64)
         N.check_jit(self.lib.vmas_jit_world_profile(self._jit, out.ctypes.data, n), "vmas_jit_world_profile")
         return out.reshape(-1, 16)
+
+    def jit_program(self, kind: int):
+        """The world module's handle when it was compiled with scenario program `kind`
+        (N.EPILOGUE_*; csrc/vmas_jit.hip), else None (no module, a CPU world, another program)."""
+        if self._dev_index < 0:
+            return None
+        self._ensure()
+        if self._jit is None or self.lib.vmas_jit_world_epilogue(self._jit) != kind:
+            return None
+        return self._jit
 
     def jit_compile_check(self) -> str:
         """Generate and hipRTC-compile this world's specialised kernel without a device (build

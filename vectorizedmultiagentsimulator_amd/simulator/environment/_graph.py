@@ -341,15 +341,19 @@ class _KernelChain:
     and the post-replay launch after it starts ~2.3 us later (tools/launch_gap_probe.py,
     profiles/r05/run7_launch_gap) -- ~7 us of a ~56 us C2 step.  The launches are the captured
     nodes' own (function, grid, argument block), in the chain's order, so a replay runs the same
-    kernels on the same arguments as the graph would.  Holds the graph: the nodes' argument
-    blocks belong to it."""
+    kernels on the same arguments as the graph would -- except that a world module's k_world node
+    followed by the same module's scenario-program node (k_program_jit) becomes ONE launch of
+    k_world with the program as its epilogue (Args.epi; csrc/vmas_programs.hpp), the same compiled
+    code on the same values, per 64-env group after the group's step.  Holds the graph: the
+    nodes' argument blocks belong to it."""
 
     MAX_NODES = int(os.environ.get("VMAS_GRAPH_CHAIN_MAX", "8"))
 
-    def __init__(self, graph, handle, n_nodes):
+    def __init__(self, graph, handle, n_nodes, fused):
         self.graph = graph
         self.handle = handle
-        self.n_nodes = n_nodes
+        self.n_nodes = n_nodes  # launches per replay
+        self.fused = fused  # k_world + k_program_jit pairs run as one launch (the program as k_world's epilogue)
 
     @classmethod
     def build(cls, graph) -> Tuple[Optional["_KernelChain"], str]:
@@ -362,7 +366,7 @@ class _KernelChain:
         rc = lib.vmas_graph_chain_build(ctypes.c_void_p(raw), cls.MAX_NODES, ctypes.byref(out))
         if rc != 0 or not out.value:
             return None, lib.vmas_last_error().decode(errors="replace")
-        return cls(graph, out, lib.vmas_graph_chain_nodes(out)), ""
+        return cls(graph, out, lib.vmas_graph_chain_nodes(out), lib.vmas_graph_chain_fused(out)), ""
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
