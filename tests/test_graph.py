@@ -619,7 +619,7 @@ def test_kernel_chain_replay_matches_graph_launch_gpu(gpu_device, name, kw, subs
     assert b._graph._chain is None
     if name != "discovery":  # (discovery's graph holds the respawn's deferred channel launch)
         assert a._graph._chain is not None, a._graph.chain_why
-        # balance: k_world with the scenario program as its epilogue, one launch per replay
-        assert (a._graph._chain.n_nodes, a._graph._chain.fused) == ((1, 1) if name == "balance" else
-                                                                    (a._graph._chain.n_nodes, 0))
-        assert a._graph._chain.n_nodes >= (1 if name == "balance" else 2)
+        # balance / transport: k_world with the scenario program as its epilogue, one launch per replay
+        fused = name in ("balance", "transport")
+        assert a._graph._chain.fused == int(fused)
+        assert a._graph._chain.n_nodes == 1 if fused else a._graph._chain.n_nodes >= 2

@@ -141,6 +141,7 @@ constexpr int kMaxNW = 16;  // column stride of the phase-profile buffer
 constexpr int kProfBlocks = 4096;  // workgroups with a per-workgroup record in profile builds
 constexpr int kProfRec = 24;       // words per record (16 waves' HW_ID at most)
 constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
+constexpr int kEpiQRows = 28;             // LDS rows of a scenario program (vmas_programs.hpp kBalQRows)
 constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
 constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
 
@@ -364,7 +365,7 @@ struct Gen {
         // row buffer when it is large enough)
         const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 >= nfl + 2) ? 0 : nfl + 2;
         const long lds = (global_rows ? 0L : (long)n_rows * 256) + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) +
-                         4 * red + (has_epi() && !epi_q_in_rows() ? 16L * 256 : 0L);
+                         4 * red + (has_epi() && !epi_q_in_rows() ? (long)kEpiQRows * 256 : 0L);
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
             return false;
@@ -414,7 +415,7 @@ struct Gen {
             return "balance_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ", " + q + ")";
         return "transport_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ")";
     }
-    bool epi_q_in_rows() const { return !global_rows && n_rows >= 16; }
+    bool epi_q_in_rows() const { return !global_rows && n_rows >= kEpiQRows; }
     // byte offset of Args.epi (after the fixed pointers: the value slots follow it)
     size_t epi_offset() const { return 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)); }
 
@@ -982,7 +983,7 @@ struct Gen {
         else
             o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
-        if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[16 * 64];\n";
+        if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[" + it((long)kEpiQRows * 64) + "];\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
         // idle between groups), else its own array; QL: steal list + broadcast word
@@ -1064,7 +1065,7 @@ struct Gen {
         if (has_epi())  // the eager step's launch of the same program (vmas_jit_program_outputs)
             o += "\nextern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ") k_program_jit(" + epi_type() + " io_arg) {\n"
                  "    VMAS_PROGRAM_ARGS(" + epi_type() + ", io_arg);\n"
-                 "    __shared__ float Q[16 * 64];\n"
+                 "    __shared__ float Q[" + it((long)kEpiQRows * 64) + "];\n"
                  "    " + epi_call("io", "blockIdx.x", "(int)(threadIdx.x >> 6)", "(int)(threadIdx.x & 63)", "Q") + ";\n}\n";
     }
 };

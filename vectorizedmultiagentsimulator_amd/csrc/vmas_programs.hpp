@@ -166,21 +166,32 @@ __device__ __forceinline__ float xdist_spheres(const VmasShapeRef& a, const Vmas
 #endif
 
 // ---- balance (balance.py:205-262; restated in scenarios/balance.py) -------------------------------
-// Q: 16 rows of 64 floats, [side][q1.x, q1.y, q2.x, q2.y][lane]
-__device__ __forceinline__ float* bal_q(float* Q, int side, int k) { return Q + (side * 4 + k) * 64; }
+// Q: kBalQRows rows of 64 floats: [0, 16) side s of closest_line_box(floor, line) as (q1.x, q1.y,
+// q2.x, q2.y); [16, 28) side s of closest_point_box(floor, package.pos) as (p.x, p.y, |pos - p|).
+// The four sides of both are computed by four waves in parallel; the first strict minimum over
+// them, in side order, is taken after the barrier (the reference's selection order).
+constexpr int kBalQRows = 28;
+__device__ __forceinline__ float* bal_q(float* Q, int row) { return Q + row * 64; }
 
-// side `side` of closest_line_box(floor, line) (get_distance's box-line branch), env bb
+// side `side` of both box queries, env bb
 template <class IO>
 __device__ __forceinline__ void bal_side(IO& io, int bb, int side, int lane, float* Q) {
-    const VmasShapeRef fl = io.floor, ln = io.line;
+    const VmasShapeRef fl = io.floor, ln = io.line, pk = io.package;
     const float rb = ref_rot(ln, bb);
+    const V2 pf = ref_pos(fl, bb);
+    const Trig tf = xtrig(ref_rot(fl, bb));
+    const Seg sd = box_side(pf, tf, fl.length * 0.5f, fl.width * 0.5f, side);
     Pts q;
-    xclosest_points_line_line(box_side(ref_pos(fl, bb), xtrig(ref_rot(fl, bb)), fl.length * 0.5f, fl.width * 0.5f, side),
-                              Seg{ref_pos(ln, bb), mk(cosf(rb), sinf(rb)), ln.length * 0.5f}, &q.p1, &q.p2);
-    bal_q(Q, side, 0)[lane] = q.p1.x;
-    bal_q(Q, side, 1)[lane] = q.p1.y;
-    bal_q(Q, side, 2)[lane] = q.p2.x;
-    bal_q(Q, side, 3)[lane] = q.p2.y;
+    xclosest_points_line_line(sd, Seg{ref_pos(ln, bb), mk(cosf(rb), sinf(rb)), ln.length * 0.5f}, &q.p1, &q.p2);
+    bal_q(Q, 4 * side + 0)[lane] = q.p1.x;
+    bal_q(Q, 4 * side + 1)[lane] = q.p1.y;
+    bal_q(Q, 4 * side + 2)[lane] = q.p2.x;
+    bal_q(Q, 4 * side + 3)[lane] = q.p2.y;
+    const V2 ps = ref_pos(pk, bb);  // closest_point_box (physics.py:262-294), this side's candidate
+    const V2 p = closest_point_line(sd.p, sd.dir, sd.half, ps, true);
+    bal_q(Q, 16 + 3 * side + 0)[lane] = p.x;
+    bal_q(Q, 16 + 3 * side + 1)[lane] = p.y;
+    bal_q(Q, 16 + 3 * side + 2)[lane] = xnorm(ps - p);
 }
 
 // done = on_the_ground + is_overlapping(package, goal)
@@ -190,28 +201,35 @@ __device__ __forceinline__ void bal_done(IO& io, int b, bool og, const OutDelta&
     moved(io.done, od.done)[b] = (og || xdist_spheres(pk, gl, b) < 0.f) ? 1 : 0;
 }
 
-// The reward block of env b from the four sides in Q: the first strict minimum over the sides in
-// order (closest_line_box), compute_on_the_ground, the package-goal distance, ground / position
-// rewards, the global shaping update, every agent's reward; then done.
+// The reward block of env b from the sides in Q: closest_line_box's and closest_point_box's
+// first strict minima over the sides in order, compute_on_the_ground, the package-goal distance,
+// ground / position rewards, the global shaping update, every agent's reward; then done.
 template <class IO>
 __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDelta& od, float* Q) {
-    V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY);
-    float bd = INFINITY;
+    V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY), cp = mk(INFINITY, INFINITY);
+    float bd = INFINITY, bp = INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const V2 q1 = mk(bal_q(Q, i, 0)[lane], bal_q(Q, i, 1)[lane]), q2 = mk(bal_q(Q, i, 2)[lane], bal_q(Q, i, 3)[lane]);
+        const V2 q1 = mk(bal_q(Q, 4 * i)[lane], bal_q(Q, 4 * i + 1)[lane]);
+        const V2 q2 = mk(bal_q(Q, 4 * i + 2)[lane], bal_q(Q, 4 * i + 3)[lane]);
         const float d = xnorm(q1 - q2);
         if (d < bd) {
             bd = d;
             c1 = q1;
             c2 = q2;
         }
+        const float dp = bal_q(Q, 16 + 3 * i + 2)[lane];
+        if (dp < bp) {
+            bp = dp;
+            cp = mk(bal_q(Q, 16 + 3 * i)[lane], bal_q(Q, 16 + 3 * i + 1)[lane]);
+        }
     }
     const VmasShapeRef pk = io.package, gl = io.goal, fl = io.floor;
-    const V2 pkg = ref_pos(pk, b), goal = ref_pos(gl, b);
+    const V2 pkg = ref_pos(pk, b), goal = ref_pos(gl, b), pf = ref_pos(fl, b);
     // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
     // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
-    const bool og = (xnorm(c1 - c2) - kLineMinDist < 0.f) || xoverlap_box_sphere(fl, pk, b);
+    const float dsc = xnorm(pkg - cp), dsb = xnorm(pkg - pf), dcb = xnorm(pf - cp);
+    const bool og = (xnorm(c1 - c2) - kLineMinDist < 0.f) || (dsb < dcb) || (dsc < pk.radius_lmd);
     io.on_the_ground[b] = og ? 1 : 0;
     const float dist = xnorm(pkg - goal);  // vector_norm(package.pos - goal.pos, dim=1)
     io.package_dist[b] = dist;
@@ -249,7 +267,7 @@ __device__ __forceinline__ void bal_obs(IO& io, int b, int i, const OutDelta& od
 
 // The whole program for 64-env group g, by every thread of a workgroup of nwave >= 5 waves (a
 // barrier inside): waves 0-3 the four box sides, waves 4.. the observations, then wave 0 the
-// reward block and done.  Q: 16 x 64 floats of LDS.
+// reward block and done.  Q: kBalQRows x 64 floats of LDS.
 template <class IO>
 __device__ __forceinline__ void balance_group(IO& io, int g, int wave, int nwave, int lane, float* Q) {
     const int b = g * 64 + lane;

@@ -38,7 +38,7 @@ constexpr float kFastTrigMaxAngle = 16.f;
 // latency at two waves per CU; before that 128 x 1 workgroups took 16 us.)
 __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io_arg) {
     VMAS_PROGRAM_ARGS(VmasBalanceIO, io_arg);
-    __shared__ float Q[16 * 64];  // [side][q1.x, q1.y, q2.x, q2.y][lane] (vmas_programs.hpp bal_q)
+    __shared__ float Q[kBalQRows * 64];  // the box queries' sides (vmas_programs.hpp bal_q)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io_arg) {
             bal_done(io, b, io.on_the_ground[b] != 0, od);
             return;
         }
-        bal_side(io, bb, wave, lane, Q);  // side `wave` of closest_line_box(floor, line)
+        bal_side(io, bb, wave, lane, Q);  // side `wave` of the floor's two box queries
         __syncthreads();
         if (wave != 0 || !valid) return;
         bal_reward(io, b, lane, od, Q);
