@@ -917,6 +917,44 @@ struct Gen {
         o += "}\n\n";
     }
 
+    // The group loop: one copy per wave (loop_per_wave, the default), each calling its own run<w>,
+    // or one loop around a switch over the waves (VMAS_JIT_LOOP_PER_WAVE=0).  With one loop the
+    // compiler hoists the loop-invariant address / stride values of EVERY wave's body above it,
+    // all live at once (balance: 106 SGPRs and 163 v_writelane spills of them into VGPR lanes,
+    // read back with v_readlane -- VALU instructions); with a loop per wave only that wave's are.
+    bool loop_per_wave = true;
+    std::string epi_text() const {
+        if (!has_epi()) return "";
+        // The scenario program of this group (vmas_graph_chain_build fuses a replay's k_world and
+        // k_program_jit into this launch): it reads the group's fields the waves just stored --
+        // visible to the whole workgroup after the barrier (its workgroup-scope release / acquire;
+        // agent-scope fences here write back L2 per group: 38 -> 159 us per launch) -- each pass of
+        // the fixed point re-running it after its group, the final pass's writes last (as the
+        // state outputs).  Q: the row buffer, idle between groups.
+        return "        if (a.epi) {\n"
+               "            __syncthreads();\n"
+               "            " + epi_call("*a.epi", "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
+               "            __syncthreads();\n"
+               "        }\n";
+    }
+    std::string loop_text(const std::string& run, const std::string& cur) const {
+        return "    for (;;) {\n"
+               "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, " + cur + ", QL);\n"
+               "        if (g < 0) break;\n" + block_stamp(4, "__builtin_amdgcn_s_memrealtime()") +
+               "        if (persistent) {\n"
+               "            for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
+               "            __syncthreads();\n"
+               "        }\n"
+               "        {\n"
+               "            const int b = g * 64 + lane;\n"
+               "            const bool valid = b < a.B;\n"
+               "            const int bb = valid ? b : (a.B - 1);\n" + run + "        }\n" + epi_text() +
+               "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, " + cur + ",\n"
+               "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
+               "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
+               "    }\n";
+    }
+
     void generate() {
         std::string& o = src;
         o += "// generated by vmas_jit.hip for one world\n";
@@ -977,6 +1015,14 @@ struct Gen {
                          " * a.B; i += blockDim.x) a.out[" + it(k) + "][i] = nan;\n";
             o += "}\n\n";
         }
+        // wave w's group loop (loop_per_wave): its copy of the persistent loop around run<w>
+        if (loop_per_wave) {
+            o += "template <int WAVE>\n__device__ __forceinline__ void group_loop(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, "
+                 "uint32_t* MSK, uint32_t* QL, uint32_t* RED, float* EQ, GridCursor* CURP, uint32_t* claim, TimerStart t0s, "
+                 "bool persistent, int nfl, int nwords, int ngrp, int lane, int wave) {\n    (void)EQ;\n";
+            o += loop_text("            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid);\n", "CURP");
+            o += "}\n\n";
+        }
         o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
         if (global_rows)  // (this workgroup's slab: the same [row][lane] layout as the LDS rows)
             o += "    float* L = a.rows + (size_t)blockIdx.x * " + it((long)std::max(n_rows, 1) * 64) + ";\n";
@@ -1021,38 +1067,22 @@ struct Gen {
                                     " + 8 + wave] = __builtin_amdgcn_s_getreg(63492);\n"
                               : "") +
              (prof_block >= 0 ? "    if (threadIdx.x == 0) vmas_prof_blk = a.prof + " + it((long)(cfg.max_substeps * 4 + 2) * kMaxNW) + ";\n" : "") +
-             "    for (;;) {\n"
-             "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, &CUR, QL);\n"
-             "        if (g < 0) break;\n" + block_stamp(4, "__builtin_amdgcn_s_memrealtime()") +
-             "        if (persistent) {\n"
-             "            for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
-             "            __syncthreads();\n"
-             "        }\n"
-             "        {\n"
-             "            const int b = g * 64 + lane;\n"
-             "            const bool valid = b < a.B;\n"
-             "            const int bb = valid ? b : (a.B - 1);\n"
-             "            switch (wave) {\n";
-        for (int w = 0; w < nw; ++w)
-            o += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
-        o += "                default: break;\n            }\n        }\n";
-        if (has_epi()) {
-            // The scenario program of this group (vmas_graph_chain_build fuses a replay's k_world and
-            // k_program_jit into this launch): it reads the group's fields the waves just stored --
-            // visible to the whole workgroup after the barrier (its workgroup-scope release /
-            // acquire; agent-scope fences here write back L2 per group: 38 -> 159 us per launch) --
-            // each pass of the fixed point re-running it after its group, the final pass's writes
-            // last (as the state outputs).  Q: the row buffer, idle between groups.
-            o += "        if (a.epi) {\n"
-                 "            __syncthreads();\n"
-                 "            " + epi_call("*a.epi", "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
-                 "            __syncthreads();\n"
-                 "        }\n";
+             "";
+        // the group loop (loop_text): one copy per wave (loop_per_wave), or one around a switch
+        if (loop_per_wave) {
+            std::string sw = "    switch (wave) {\n";
+            for (int w = 0; w < nw; ++w)
+                sw += "        case " + it(w) + ": group_loop<" + it(w) + ">(a, L, FL, DONE, MSK, QL, RED, " +
+                      std::string(has_epi() && !epi_q_in_rows() ? "EQ" : "nullptr") +
+                      ", &CUR, claim, t0s, persistent, nfl, nwords, ngrp, lane, wave); break;\n";
+            o += sw + "        default: break;\n    }\n";
+        } else {
+            std::string sw = "            switch (wave) {\n";
+            for (int w = 0; w < nw; ++w)
+                sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
+            o += loop_text(sw + "                default: break;\n            }\n", "&CUR");
         }
-        o += "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, &CUR,\n"
-             "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
-             "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
-             "    }\n" + block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
+        o += block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
              "    if (!persistent) {\n"
              "        if (!a.blk) return;\n"
              "        __syncthreads();\n"
@@ -1070,11 +1100,13 @@ struct Gen {
     }
 };
 
-// Code-generation A/B knobs (environment): VMAS_JIT_PRIO, VMAS_JIT_PRELOAD, VMAS_JIT_PAIR_PRELOAD.
+// Code-generation A/B knobs (environment): VMAS_JIT_PRIO, VMAS_JIT_PRELOAD, VMAS_JIT_PAIR_PRELOAD,
+// VMAS_JIT_LOOP_PER_WAVE.
 void codegen_knobs(Gen& g) {
     if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
     if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
     if (const char* pp = getenv("VMAS_JIT_PAIR_PRELOAD")) g.pair_preload = atoi(pp) != 0;
+    if (const char* lw = getenv("VMAS_JIT_LOOP_PER_WAVE")) g.loop_per_wave = atoi(lw) != 0;
 }
 
 // Plan a world: box pairs split with two workgroups per CU, else unsplit, else unsplit with the

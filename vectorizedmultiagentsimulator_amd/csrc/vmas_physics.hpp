@@ -64,9 +64,17 @@ VHD Real norm(V2 v) { return sqrtf(v.x * v.x + v.y * v.y); }
 VHD Real cross(V2 a, V2 b) { return a.x * b.y - a.y * b.x; }
 // torch.sign: (0 < x) - (x < 0); NaN -> 0
 VHD Real tsign(Real x) { return Real((float)((0.f < x) - (x < 0.f))); }
-// torch.minimum / torch.maximum / torch.min(dim) / torch.max(dim): NaN propagating
+// torch.minimum / torch.maximum / torch.min(dim) / torch.max(dim): NaN propagating.  Relaxed
+// builds (the world-specialised kernels) use gfx950's v_minimum3_f32 / v_maximum3_f32 (IEEE 754-2019
+// minimum / maximum: NaN propagating, one instruction instead of three compares and three selects);
+// they differ from the selects only in the sign of a zero result of comparing +0 with -0.
+#ifdef VMAS_PHYS_RELAXED
+VHD Real tmin(Real a, Real b) { return __builtin_elementwise_minimum(a, b); }
+VHD Real tmax(Real a, Real b) { return __builtin_elementwise_maximum(a, b); }
+#else
 VHD Real tmin(Real a, Real b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
 VHD Real tmax(Real a, Real b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+#endif
 // torch.clamp(x, lo, hi).  Its backward passes the gradient where lo <= x <= hi, bounds
 // included; the gradient build (VMAS_PHYS_GRAD, csrc/vmas_grad.hip) keeps x itself there so a value
 // sitting exactly on a bound (an action clamped last step) carries its tangent as torch's does.
