@@ -13,7 +13,7 @@ step() {  # step <name> <timeout> <cmd...>: stops the session on a crash / timeo
     echo "=== $name rc=$rc"; tail -n 4 "$OUT/$name.log" | cut -c1-400
     case $rc in 124|134|137|139) echo "fatal rc=$rc, stopping"; exit $rc;; esac
 }
-step smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 1100 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread
 step bench_c2 600 python bench.py
 step bench_c3 600 python bench.py --scenario transport --cpu-steps 0
