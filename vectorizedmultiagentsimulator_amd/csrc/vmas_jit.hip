@@ -141,6 +141,8 @@ constexpr int kMaxNW = 16;  // column stride of the phase-profile buffer
 constexpr int kProfBlocks = 4096;  // workgroups with a per-workgroup record in profile builds
 constexpr int kProfRec = 24;       // words per record (16 waves' HW_ID at most)
 constexpr int kMaxArgBytes = 3584;        // HIP kernel argument block limit is 4 KiB
+static_assert(sizeof(VmasBalanceIO) % 8 == 0 && sizeof(VmasTransportIO) % 8 == 0,
+              "a scenario program's argument block is copied into LDS in 8-byte words");
 constexpr int kEpiQRows = 28;             // LDS rows of a scenario program (vmas_programs.hpp kBalQRows)
 constexpr int kLdsTwoPerCu = 64 * 1024;   // keeps two 512-thread workgroups per CU
 constexpr int kLdsOnePerCu = 150 * 1024;  // big worlds: one workgroup per CU (160 KiB LDS)
@@ -365,7 +367,9 @@ struct Gen {
         // row buffer when it is large enough)
         const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 >= nfl + 2) ? 0 : nfl + 2;
         const long lds = (global_rows ? 0L : (long)n_rows * 256) + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) +
-                         4 * red + (has_epi() && !epi_q_in_rows() ? (long)kEpiQRows * 256 : 0L);
+                         4 * red + (has_epi() && !epi_q_in_rows() ? (long)kEpiQRows * 256 : 0L) +
+                         (has_epi() && epi_lds ? (long)(cfg.epilogue == VMAS_EPILOGUE_BALANCE ? sizeof(VmasBalanceIO)
+                                                                                            : sizeof(VmasTransportIO)) : 0L);
         if (lds > lds_budget) {
             *why = "LDS budget exceeded (" + it(lds) + " B)";
             return false;
@@ -923,7 +927,11 @@ struct Gen {
     // all live at once (balance: 106 SGPRs and 163 v_writelane spills of them into VGPR lanes,
     // read back with v_readlane -- VALU instructions); with a loop per wave only that wave's are.
     bool loop_per_wave = true;
-    std::string epi_text() const {
+    // the scenario program's argument block copied into LDS at the launch's start (epi_lds, the
+    // default; VMAS_JIT_EPI_LDS=0: read through Args.epi): the epilogue's field reads are LDS reads
+    // instead of a cold scalar-cache miss per group
+    bool epi_lds = true;
+    std::string epi_text(const std::string& io) const {
         if (!has_epi()) return "";
         // The scenario program of this group (vmas_graph_chain_build fuses a replay's k_world and
         // k_program_jit into this launch): it reads the group's fields the waves just stored --
@@ -933,11 +941,11 @@ struct Gen {
         // state outputs).  Q: the row buffer, idle between groups.
         return "        if (a.epi) {\n"
                "            __syncthreads();\n"
-               "            " + epi_call("*a.epi", "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
+               "            " + epi_call(io, "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
                "            __syncthreads();\n"
                "        }\n";
     }
-    std::string loop_text(const std::string& run, const std::string& cur) const {
+    std::string loop_text(const std::string& run, const std::string& cur, const std::string& io) const {
         return "    for (;;) {\n"
                "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, " + cur + ", QL);\n"
                "        if (g < 0) break;\n" + block_stamp(4, "__builtin_amdgcn_s_memrealtime()") +
@@ -948,7 +956,7 @@ struct Gen {
                "        {\n"
                "            const int b = g * 64 + lane;\n"
                "            const bool valid = b < a.B;\n"
-               "            const int bb = valid ? b : (a.B - 1);\n" + run + "        }\n" + epi_text() +
+               "            const int bb = valid ? b : (a.B - 1);\n" + run + "        }\n" + epi_text(io) +
                "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, " + cur + ",\n"
                "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
                "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
@@ -1019,8 +1027,9 @@ struct Gen {
         if (loop_per_wave) {
             o += "template <int WAVE>\n__device__ __forceinline__ void group_loop(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, "
                  "uint32_t* MSK, uint32_t* QL, uint32_t* RED, float* EQ, GridCursor* CURP, uint32_t* claim, TimerStart t0s, "
-                 "bool persistent, int nfl, int nwords, int ngrp, int lane, int wave) {\n    (void)EQ;\n";
-            o += loop_text("            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid);\n", "CURP");
+                 "bool persistent, int nfl, int nwords, int ngrp, int lane, int wave" +
+                 std::string(has_epi() ? std::string(", const ") + epi_type() + "* PROG_IOP" : std::string()) + ") {\n    (void)EQ;\n";
+            o += loop_text("            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid);\n", "CURP", "*PROG_IOP");
             o += "}\n\n";
         }
         o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
@@ -1030,6 +1039,7 @@ struct Gen {
             o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
         if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[" + it((long)kEpiQRows * 64) + "];\n";
+        if (has_epi() && epi_lds) o += std::string("    __shared__ __attribute__((aligned(16))) ") + epi_type() + " PROG_IO;\n";
         o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
         // idle between groups), else its own array; QL: steal list + broadcast word
@@ -1058,6 +1068,11 @@ struct Gen {
              "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0, 0, persistent ? ld64(&a.ctl[kGridEpoch]) : 0ull};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n" +
+             std::string(has_epi() && epi_lds ?
+                 "    if (a.epi)\n"
+                 "        for (int i = threadIdx.x; i < (int)(sizeof(PROG_IO) / 8); i += blockDim.x)\n"
+                 "            reinterpret_cast<unsigned long long*>(&PROG_IO)[i] = reinterpret_cast<const unsigned long long*>(a.epi)[i];\n"
+                 : "") +
              prm_copy() +
              "    __syncthreads();\n" +
              block_stamp(0, "__builtin_amdgcn_s_memrealtime()") + block_stamp(1, "__builtin_amdgcn_s_getreg(63492)") +
@@ -1074,13 +1089,14 @@ struct Gen {
             for (int w = 0; w < nw; ++w)
                 sw += "        case " + it(w) + ": group_loop<" + it(w) + ">(a, L, FL, DONE, MSK, QL, RED, " +
                       std::string(has_epi() && !epi_q_in_rows() ? "EQ" : "nullptr") +
-                      ", &CUR, claim, t0s, persistent, nfl, nwords, ngrp, lane, wave); break;\n";
+                      ", &CUR, claim, t0s, persistent, nfl, nwords, ngrp, lane, wave" +
+                      std::string(has_epi() ? (epi_lds ? ", &PROG_IO" : ", a.epi") : "") + "); break;\n";
             o += sw + "        default: break;\n    }\n";
         } else {
             std::string sw = "            switch (wave) {\n";
             for (int w = 0; w < nw; ++w)
                 sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
-            o += loop_text(sw + "                default: break;\n            }\n", "&CUR");
+            o += loop_text(sw + "                default: break;\n            }\n", "&CUR", epi_lds ? "PROG_IO" : "*a.epi");
         }
         o += block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
              "    if (!persistent) {\n"
@@ -1101,12 +1117,13 @@ struct Gen {
 };
 
 // Code-generation A/B knobs (environment): VMAS_JIT_PRIO, VMAS_JIT_PRELOAD, VMAS_JIT_PAIR_PRELOAD,
-// VMAS_JIT_LOOP_PER_WAVE.
+// VMAS_JIT_LOOP_PER_WAVE, VMAS_JIT_EPI_LDS.
 void codegen_knobs(Gen& g) {
     if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
     if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
     if (const char* pp = getenv("VMAS_JIT_PAIR_PRELOAD")) g.pair_preload = atoi(pp) != 0;
     if (const char* lw = getenv("VMAS_JIT_LOOP_PER_WAVE")) g.loop_per_wave = atoi(lw) != 0;
+    if (const char* el = getenv("VMAS_JIT_EPI_LDS")) g.epi_lds = atoi(el) != 0;
 }
 
 // Plan a world: box pairs split with two workgroups per CU, else unsplit, else unsplit with the
