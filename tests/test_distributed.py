@@ -35,7 +35,8 @@ def test_bench_two_ranks_gloo():
     rates = pg["per_rank_env_steps_per_s"]
     assert len(rates) == 2 and all(r > 0 for r in rates)
     # value = all ranks' env-steps over the slowest rank's time: <= the sum of the ranks' own rates
-    assert rec["value"] <= sum(rates) * (1 + 1e-9) and rec["value"] >= 2 * min(rates) * (1 - 1e-9)
+    # (the per-rank rates are printed rounded to 0.1 env-steps/s)
+    assert rec["value"] <= sum(rates) + 0.1 * len(rates) and rec["value"] >= 2 * (min(rates) - 0.05) - 1e-6
     assert "balance" in rec["metric"] and "@64 envs on CPU" in rec["metric"]
 
 

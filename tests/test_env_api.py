@@ -196,9 +196,9 @@ def test_default_done_is_a_fresh_all_false_view_after_writes():
 
 
 def test_uniform_signature_sees_every_field_it_keys_on():
-    """The random-action plan's signature (Environment._uniform_sig / _uniform_same): its fast path
-    (the core classes' fields read directly) and the property path both see a change of each field
-    the column plan depends on."""
+    """The random-action plan's signature (Environment._uniform_sig / _uniform_same): its fast paths
+    (nothing assigned since, core.STATIC_VERSION; the core classes' fields read directly) and the
+    property path all see a change of each field the column plan depends on."""
     from vectorizedmultiagentsimulator_amd import make_env
     from vectorizedmultiagentsimulator_amd.simulator.core import Agent
 
@@ -208,10 +208,11 @@ def test_uniform_signature_sees_every_field_it_keys_on():
     a = env.agents[1]
     for field, value in (("_u_range", 0.5), ("_silent", not a._silent), ("action_size", a.action_size + 1)):
         obj = a.action if field == "_u_range" else a
+        # (assigned as attributes: the version fast path, core.STATIC_VERSION, follows assignments)
         old = obj.__dict__[field]
-        obj.__dict__[field] = value
+        setattr(obj, field, value)
         assert not env._uniform_same(sig), field
-        obj.__dict__[field] = old
+        setattr(obj, field, old)
         assert env._uniform_same(sig), field
     old = a._action
     a._action = type(old).__new__(type(old))
@@ -227,7 +228,7 @@ def test_uniform_signature_sees_every_field_it_keys_on():
     a.__class__ = Custom
     sig2 = env._uniform_sig()
     assert not sig2[4] and env._uniform_same(sig2)
-    a.action.__dict__["_u_range"] = 0.25
+    a.action._u_range = 0.25
     assert not env._uniform_same(sig2)
 
 

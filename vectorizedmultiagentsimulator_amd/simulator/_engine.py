@@ -94,6 +94,7 @@ class PhysicsEngine:
         self._sig = None
         self._handle = None
         self._jit = None
+        self._sig_cache = None  # (STATIC_VERSION, signature)
         self.jit_error = None
         self.kernel_name = "k_step"
         self._dev_index = -1
@@ -166,6 +167,18 @@ class PhysicsEngine:
     _AGENT_SIG = operator.attrgetter("_max_f", "_f_range", "_max_t", "_t_range")
 
     def _signature(self):
+        # (recomputed only after an assignment to an attribute it reads: core.STATIC_VERSION)
+        from . import core
+
+        v = core.STATIC_VERSION[0]
+        c = self._sig_cache
+        if c is not None and c[0] == v:
+            return c[1]
+        sig = self._signature_now()
+        self._sig_cache = (v, sig)
+        return sig
+
+    def _signature_now(self):
         w = self.world
         es = []
         for e in w.entities:

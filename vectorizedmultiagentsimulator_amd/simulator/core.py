@@ -41,6 +41,24 @@ from .utils import (
 )
 
 
+# Version of the attributes the physics engine's static tables are built from (simulator/_engine.py
+# _signature): bumped by every assignment to one of them (the __setattr__ hooks below and the
+# world's add_* methods), so the engine rebuilds its per-step structure signature only after
+# something it depends on was assigned (graph mode compares it every step: ~3-6 us of host time).
+STATIC_VERSION = [0]
+_ENTITY_STATIC = frozenset({
+    "_shape", "_movable", "_rotatable", "_collide", "_collision_filter", "_mass", "_drag", "_linear_friction",
+    "_angular_friction", "_max_speed", "_v_range", "_gravity", "_max_f", "_f_range", "_max_t", "_t_range",
+    # (and what the environment's random-action plans depend on: environment.py _uniform_sig)
+    "_action", "_silent", "action_size", "_batch_dim", "_action_script", "__class__",
+})
+_WORLD_STATIC = frozenset({
+    "_agents", "_landmarks", "_joints", "_drag", "_linear_friction", "_angular_friction", "_x_semidim",
+    "_y_semidim", "_collision_force", "_joint_force", "_torque_constraint_force", "_contact_margin", "_gravity",
+    "_collidable_pairs", "_batch_dim", "_device", "export_forces", "_dim_c",
+})
+
+
 class TorchVectorizedObject(object):
     def __init__(self, batch_dim: int = None, device: torch.device = None):
         self._batch_dim = batch_dim
@@ -96,6 +114,11 @@ class Shape(ABC):
 
 
 class Box(Shape):
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name == "hollow":
+            STATIC_VERSION[0] += 1
+
     def __init__(self, length: float = 0.3, width: float = 0.1, hollow: bool = False):
         super().__init__()
         assert length > 0, f"Length must be > 0, got {length}"
@@ -351,6 +374,11 @@ class AgentState(EntityState):
 class Action(TorchVectorizedObject):
     """Agent action container (core.py:413-533)."""
 
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name == "_u_range":  # (environment.py _uniform_sig)
+            STATIC_VERSION[0] += 1
+
     def __init__(self, u_range, u_multiplier, u_noise, action_size: int):
         super().__init__()
         self._u_noise = u_noise
@@ -466,6 +494,11 @@ class Action(TorchVectorizedObject):
 # ------------------------------------------------------------------------------------------------
 # entities (core.py:537-1085)
 class Entity(TorchVectorizedObject, Observable, ABC):
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name in _ENTITY_STATIC:
+            STATIC_VERSION[0] += 1
+
     def __init__(
         self,
         name: str,
@@ -937,6 +970,11 @@ class World(TorchVectorizedObject):
         (core.py:2796-2800) exactly; ``"env"`` simulates every static candidate pair in every env
         (what an independent single-env simulator would do; no host handshake per step).
     """
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name in _WORLD_STATIC:
+            STATIC_VERSION[0] += 1
+
 
     def __init__(
         self,
@@ -1010,6 +1048,7 @@ class World(TorchVectorizedObject):
         agent.to(self._device)
         agent._spawn(dim_c=self._dim_c, dim_p=self.dim_p)
         self._agents.append(agent)
+        STATIC_VERSION[0] += 1
 
     def add_landmark(self, landmark: Landmark):
         """Only way to add landmarks to the world"""
@@ -1017,6 +1056,7 @@ class World(TorchVectorizedObject):
         landmark.to(self._device)
         landmark._spawn(dim_c=self.dim_c, dim_p=self.dim_p)
         self._landmarks.append(landmark)
+        STATIC_VERSION[0] += 1
 
     def add_joint(self, joint: Joint):
         assert self._substeps > 1, "For joints, world substeps needs to be more than 1"
@@ -1024,6 +1064,7 @@ class World(TorchVectorizedObject):
             self.add_landmark(joint.landmark)
         for constraint in joint.joint_constraints:
             self._joints.update({frozenset({constraint.entity_a.name, constraint.entity_b.name}): constraint})
+        STATIC_VERSION[0] += 1
 
     def reset(self, env_index: int):
         for e in self.entities:

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 from torch import Tensor
 
+from .. import core as _core
 from ..core import Agent, TorchVectorizedObject
 from ..scenario import BaseScenario
 from ..utils import AGENT_OBS_TYPE, DEVICE_TYPING, TorchUtils, override
@@ -788,10 +789,14 @@ class Environment(TorchVectorizedObject):
         # plain: every agent and action of the core classes' accessors (the properties only return
         # the underscored fields), so _uniform_same may read the fields without a Python frame each
         plain = all(_plain_accessors(type(a), type(a.action)) for a in self.agents)
-        # the device the plan draws on (env.to(...) moves the world and its agents)
-        return (self.world.dim_c, sig, self.world.device, self.world.batch_dim, plain)
+        # the device the plan draws on (env.to(...) moves the world and its agents); the static
+        # version and the agent list: nothing this compares was assigned since (core.STATIC_VERSION)
+        return (self.world.dim_c, sig, self.world.device, self.world.batch_dim, plain, _core.STATIC_VERSION[0],
+                self.agents)
 
     def _uniform_same(self, sig) -> bool:
+        if sig is not None and sig[5] == _core.STATIC_VERSION[0] and sig[6] is self.agents:
+            return True
         if (sig is None or sig[0] != self.world.dim_c or len(sig[1]) != len(self.agents)
                 or sig[2] != self.world.device or sig[3] != self.world.batch_dim):
             return False

@@ -111,6 +111,13 @@ class Joint(Observer):
 
 class JointConstraint:
     """Uncollidable constraint binding two entities at anchor points at a distance (joints.py:147)."""
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name in ("dist", "rotate", "fixed_rotation"):  # (read by the engine's signature)
+            from . import core
+
+            core.STATIC_VERSION[0] += 1
+
 
     def __init__(
         self,
