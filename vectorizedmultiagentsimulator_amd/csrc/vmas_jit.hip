@@ -287,7 +287,7 @@ struct Gen {
         // other tasks (last in its wave), priced at 3.  Measured (profiles/r01/run27_schedule):
         // k_world balance 66.3 -> 64.4 us, transport 10.2 -> 9.9 us against SS 1.0 and the
         // finish placed after all other tasks.  VMAS_JIT_COST_SS / VMAS_JIT_COST_FINISH /
-        // VMAS_JIT_FINISH_LPT=0 override (A/B).
+        // VMAS_JIT_COST_PART (a box-line part) / VMAS_JIT_FINISH_LPT=0 override (A/B).
         float kCost[7] = {1.5f, 0.5f, 2.0f, 1.8f, 2.2f, 7.4f, 30.f};
         float finish_cost = 3.0f;
         // (measured and rejected, profiles/r02/run10_sched: a table rescaled to relaxed-math VALU
@@ -296,13 +296,15 @@ struct Gen {
         // rotations, so per-SIMD sums even out, and the per-wave makespan is what binds)
         if (const char* c = getenv("VMAS_JIT_COST_SS")) kCost[VMAS_PAIR_SS] = (float)atof(c);
         if (const char* c = getenv("VMAS_JIT_COST_FINISH")) finish_cost = (float)atof(c);
+        float bl_part_cost = 1.8f, bb_part_cost = 3.8f;  // a split box-line / box-box pair's part
+        if (const char* c = getenv("VMAS_JIT_COST_PART")) bl_part_cost = (float)atof(c);
         const char* fl_lpt = getenv("VMAS_JIT_FINISH_LPT");
         const bool finish_in_lpt = !(fl_lpt && fl_lpt[0] == '0');
         std::vector<Task> all, finishes;
         for (int p = 0; p < P; ++p) {
             if (split[p]) {
                 for (int k = 0; k < parts(pd[p].cls); ++k)
-                    all.push_back({p, k, pd[p].cls == VMAS_PAIR_BL ? 1.8f : 3.8f});
+                    all.push_back({p, k, pd[p].cls == VMAS_PAIR_BL ? bl_part_cost : bb_part_cost});
                 (finish_in_lpt ? all : finishes).push_back({p, kFinish, finish_cost});
             } else {
                 all.push_back({p, kWhole, kCost[pd[p].cls]});
