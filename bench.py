@@ -550,10 +550,12 @@ def main():
     }
     if group is not None:
         out["process_group"] = group
-    if args.scenario == "discovery":  # (respawns the one-launch sampler handed over to the reference loop)
+    if args.scenario == "discovery":  # (one-launch respawns redone: by the per-target kernels or the reference loop)
+        g_ = type(env.scenario).make_world.__globals__
         out["config"]["respawn_handovers"] = {
             "timed": handovers[0] - h0, "total": handovers[0],
-            "why": type(env.scenario).make_world.__globals__.get("HANDOVER_LOG", [])}
+            "to_reference_loop": g_.get("REFERENCE_LOOP", [None])[0],
+            "why": g_.get("HANDOVER_LOG", [])}
     if rank == 0 and world_size == 1 and args.cpu_steps > 0:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

@@ -564,7 +564,8 @@ def respawn_reference_loop(agents_pos: Tensor, covered: Tensor, min_dist: float,
         tp.copy_(torch.where(covered[:, i].unsqueeze(-1), pos.squeeze(1), tp))
 
 
-HANDOVERS = [0]  # (respawns redone by the reference loop in this process: bench.py reports it)
+HANDOVERS = [0]  # (one-launch respawns redone in this process: bench.py reports it)
+REFERENCE_LOOP = [0]  # (of those, redone by the reference's host loop, not the per-target kernels)
 HANDOVER_LOG = []  # why each was redone (the first 16): bench.py reports it
 
 
@@ -586,6 +587,7 @@ def _respawn_redo(args, backup: Tensor, offset: int, gen) -> None:
     gen.set_offset(offset)
     if _redo_per_target(args, offset, gen):
         return
+    REFERENCE_LOOP[0] += 1
     respawn_reference_loop(*args[:5], targets)
 
 
