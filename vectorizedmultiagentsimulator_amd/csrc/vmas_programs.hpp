@@ -201,11 +201,23 @@ __device__ __forceinline__ void bal_done(IO& io, int b, bool og, const OutDelta&
     moved(io.done, od.done)[b] = (og || xdist_spheres(pk, gl, b) < 0.f) ? 1 : 0;
 }
 
+// wave 0's own inputs of the reward block, loaded before the barrier (their latency under the
+// four waves' box queries instead of after them): the previous shaping and the goal position
+struct BalPre {
+    float gs;
+    V2 goal;
+};
+template <class IO>
+__device__ __forceinline__ BalPre bal_preload(IO& io, int bb) {
+    const VmasShapeRef gl = io.goal;
+    return BalPre{io.global_shaping[(long)bb * io.gs_s0], ref_pos(gl, bb)};
+}
+
 // The reward block of env b from the sides in Q: closest_line_box's and closest_point_box's
 // first strict minima over the sides in order, compute_on_the_ground, the package-goal distance,
 // ground / position rewards, the global shaping update, every agent's reward; then done.
 template <class IO>
-__device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDelta& od, float* Q) {
+__device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDelta& od, float* Q, const BalPre& pre) {
     V2 c1 = mk(INFINITY, INFINITY), c2 = mk(INFINITY, INFINITY), cp = mk(INFINITY, INFINITY);
     float bd = INFINITY, bp = INFINITY;
 #pragma unroll
@@ -224,8 +236,8 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
             cp = mk(bal_q(Q, 16 + 3 * i)[lane], bal_q(Q, 16 + 3 * i + 1)[lane]);
         }
     }
-    const VmasShapeRef pk = io.package, gl = io.goal, fl = io.floor;
-    const V2 pkg = ref_pos(pk, b), goal = ref_pos(gl, b), pf = ref_pos(fl, b);
+    const VmasShapeRef pk = io.package, fl = io.floor;
+    const V2 pkg = ref_pos(pk, b), goal = pre.goal, pf = ref_pos(fl, b);
     // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
     // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
     const float dsc = xnorm(pkg - cp), dsb = xnorm(pkg - pf), dcb = xnorm(pf - cp);
@@ -236,7 +248,7 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
     const float ground = og ? io.fall_reward : 0.f;  // zeros, masked_fill_(on_the_ground, fall)
     io.ground_rew[b] = ground;
     const float gs = dist * io.shaping_factor;
-    const float pos_rew = io.global_shaping[(long)b * io.gs_s0] - gs;
+    const float pos_rew = pre.gs - gs;
     io.global_shaping_out[b] = gs;
     if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
     io.pos_rew[b] = pos_rew;
@@ -275,12 +287,13 @@ __device__ __forceinline__ void balance_group(IO& io, int g, int wave, int nwave
     const int bb = valid ? b : io.batch - 1;
     const OutDelta od = load_out_delta(io);
     const bool rew = io.what & VMAS_SCN_REWARD;
+    const BalPre pre = rew && wave == 0 ? bal_preload(io, bb) : BalPre{0.f, mk(0.f, 0.f)};
     if (rew && wave < 4) bal_side(io, bb, wave, lane, Q);
     if ((io.what & VMAS_SCN_OBS) && wave >= 4 && valid)
         for (int i = wave - 4; i < io.n_agents; i += nwave - 4) bal_obs(io, b, i, od);
     __syncthreads();
     if (wave != 0 || !valid) return;
-    if (rew) bal_reward(io, b, lane, od, Q);
+    if (rew) bal_reward(io, b, lane, od, Q, pre);
     else if (io.what & VMAS_SCN_DONE) bal_done(io, b, io.on_the_ground[b] != 0, od);
 }
 

@@ -50,10 +50,11 @@ __global__ void __launch_bounds__(256) k_balance(VmasBalanceIO io_arg) {
             bal_done(io, b, io.on_the_ground[b] != 0, od);
             return;
         }
+        const BalPre pre = wave == 0 ? bal_preload(io, bb) : BalPre{0.f, mk(0.f, 0.f)};
         bal_side(io, bb, wave, lane, Q);  // side `wave` of the floor's two box queries
         __syncthreads();
         if (wave != 0 || !valid) return;
-        bal_reward(io, b, lane, od, Q);
+        bal_reward(io, b, lane, od, Q, pre);
         return;
     }
     // agent i's observation
