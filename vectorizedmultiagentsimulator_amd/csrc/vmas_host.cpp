@@ -46,6 +46,7 @@ using UniformColumnsSnapFn = int32_t (*)(int32_t, int64_t, const VmasUniformColu
 using CopySpansDrawFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, int64_t, const VmasUniformColumn*, int32_t,
                                     uint64_t, uint64_t, const uint64_t*, int32_t, int64_t, uint64_t*, void*);
 using LastErrorFn = const char* (*)(void);
+using ChainLaunchFn = int32_t (*)(const void*, void*);
 
 void* current_stream(int device) {
     return (void*)c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
@@ -224,9 +225,18 @@ public:
         if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans failed: ") + last_error_());
     }
 
+    // The replay's kernel chain (vmas_graph_chain_launch at chain_fn; 0: already launched) on the
+    // current stream: a replay and its post-replay launch in one call from Python.
+    void launch_chain(int64_t chain, int64_t chain_fn) {
+        if (!chain) return;
+        const int32_t rc = ((ChainLaunchFn)chain_fn)((const void*)chain, current_stream(device_));
+        if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_graph_chain_launch failed: ") + last_error_());
+    }
+
     // alloc() then the launches: rows [0, mid) and [mid, hi) as two launches when mid > 0 (outputs
     // that lie in a carry destination are copied before the carry), else [0, hi) as one.
-    std::vector<at::Tensor> post(int64_t mid, int64_t hi) {
+    std::vector<at::Tensor> post(int64_t mid, int64_t hi, int64_t chain, int64_t chain_fn) {
+        launch_chain(chain, chain_fn);
         std::vector<at::Tensor> out = alloc();
         if (mid > 0) {
             launch(0, mid);
@@ -371,8 +381,10 @@ inline double now_ns() {
     return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// chain / chain_fn: the replay's kernel chain, launched first (OutputAlloc.launch_chain; 0: none).
 py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, int64_t snap_base, int64_t snap_numel,
-                    int64_t copy_draw_fn, int64_t off_dev) {
+                    int64_t copy_draw_fn, int64_t off_dev, int64_t chain, int64_t chain_fn) {
+    oa.launch_chain(chain, chain_fn);
     const bool tm = g_timing.on;
     double t0 = tm ? now_ns() : 0.0, t1 = 0.0;
     std::vector<at::Tensor> outs = oa.alloc();
@@ -422,12 +434,14 @@ PYBIND11_MODULE(_vmas_host, m) {
         .def("alloc", &OutputAlloc::alloc)
         .def("commit", &OutputAlloc::commit)
         .def("launch", &OutputAlloc::launch)
-        .def("post", &OutputAlloc::post)
+        .def("post", &OutputAlloc::post, py::arg("mid"), py::arg("hi"), py::arg("chain") = 0, py::arg("chain_fn") = 0)
         .def("count", &OutputAlloc::count);
     py::class_<UniformDraw>(m, "UniformDraw")
         .def(py::init<int, int64_t, int64_t, int64_t, py::object, int64_t, int64_t, std::vector<int64_t>, int, int64_t,
                       int64_t>())
         .def("draw", &UniformDraw::draw);
-    m.def("post_draw", &post_draw);
+    m.def("post_draw", &post_draw, py::arg("oa"), py::arg("d"), py::arg("mid"), py::arg("hi"), py::arg("snap_base"),
+          py::arg("snap_numel"), py::arg("copy_draw_fn"), py::arg("off_dev"), py::arg("chain") = 0,
+          py::arg("chain_fn") = 0);
     m.def("versions", &versions);
 }

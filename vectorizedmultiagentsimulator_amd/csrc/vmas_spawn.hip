@@ -759,7 +759,10 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
     const int b = (int)blockIdx.x * 64 + lane;
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
-    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+    if (prof && threadIdx.x == 0) {
+        if (blockIdx.x == 0) prof[0] = __builtin_amdgcn_s_memrealtime();
+        prof[32 + gridDim.x + blockIdx.x] = __builtin_amdgcn_s_memrealtime();  // (group g's start)
+    }
     const int WP = win_pairs(io.max_accepted, wa.pairs);  // (the tries this call evaluates)
     float2* occ = reinterpret_cast<float2*>(win_lds);                // [n_occ][64]
     uint32_t* okw = reinterpret_cast<uint32_t*>(occ + n_occ * 64);   // [T][64][4] the masks
@@ -887,6 +890,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
         }
     }
     __syncthreads();
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[31] = __builtin_amdgcn_s_memrealtime();
     for (int c = (int)threadIdx.x; c < cols; c += kWinThreads) {  // the group's table: max over its 64 envs
         uint32_t acc = 0u;
 #pragma unroll 8
@@ -904,6 +908,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
     const int members = min(kWinCluster, (int)gridDim.x - first);
     if (threadIdx.x == 0) last_s = atomicAdd(&io.max_accepted[win_cluster_word(T) + cl], 1) == members - 1;
     __syncthreads();
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[29] = __builtin_amdgcn_s_memrealtime();
     if (last_s) {
         const int per = kWinThreads / cols, c = (int)threadIdx.x % cols, r0 = (int)threadIdx.x / cols;
         uint32_t acc = 0u;
@@ -1376,7 +1381,7 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     unsigned long long* prof = nullptr;
     static const bool want_prof = getenv("VMAS_SPAWN_PROFILE") && getenv("VMAS_SPAWN_PROFILE")[0] == '1';
     if (want_prof) {
-        const size_t need = std::max<size_t>((size_t)T * n_groups * 6, 32 + (size_t)n_groups);  // (window: [0] cands start, [1, 9 + T) the chain's stamps, [30] group 0's pairs drawn, [32 + g] group g done)
+        const size_t need = std::max<size_t>((size_t)T * n_groups * 6, 32 + 2 * (size_t)n_groups);  // (window: [0] cands start, [1, 7) the chain's stamps, group 0's [30] pairs drawn, [31] sweep done, [29] tables stored, [32 + g] group g done, [32 + G + g] its start)
         if (g_spawn_prof_n < need) {
             if (g_spawn_prof) (void)hipFree(g_spawn_prof);
             VMAS_AUX_HIP(hipMalloc((void**)&g_spawn_prof, need * sizeof(unsigned long long)));

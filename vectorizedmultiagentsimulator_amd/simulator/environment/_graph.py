@@ -352,6 +352,7 @@ class _KernelChain:
     def __init__(self, graph, handle, n_nodes, fused):
         self.graph = graph
         self.handle = handle
+        self.addr = handle.value  # (handed to _vmas_host's post / post_draw, which launch it)
         self.n_nodes = n_nodes  # launches per replay
         self.fused = fused  # k_world + k_program_jit pairs run as one launch (the program as k_world's epilogue)
 
@@ -1095,7 +1096,7 @@ class StepGraph:
         return self.env.world.engine.graph_token() == self._sig
 
     # ---- replay ---------------------------------------------------------------------------------
-    def _launch(self):
+    def _launch(self, defer_chain: bool = False):
         """One replay.  The first goes through torch (its prologue refreshes the generator state
         that captured random ops read); if it did not advance the device generator, the graph
         draws no random numbers and later replays launch the instantiated graph directly
@@ -1112,6 +1113,8 @@ class StepGraph:
                     fn(*args, out=res)
             return
         if self._chain is not None:  # the graph's kernels as plain launches (_KernelChain)
+            if defer_chain:  # (launched by the post-replay call: _post_replay(chain=...))
+                return self._chain
             N.check(N.load_library().vmas_graph_chain_launch(self._chain.handle, N.stream_ptr(self._dev_index())),
                     "vmas_graph_chain_launch")
             return
@@ -1131,6 +1134,9 @@ class StepGraph:
     # a replay whose graph is a short chain of kernel nodes launches them on the stream instead
     # (_KernelChain); 0: hipGraphLaunch (A/B knob)
     _CHAIN = os.environ.get("VMAS_GRAPH_CHAIN", "1") != "0"
+    # a pre-applied replay's kernel chain launched by the post-replay C++ call (_vmas_host post /
+    # post_draw) instead of its own ctypes call; 0: launched from Python first (A/B knob)
+    _CHAIN_IN_POST = os.environ.get("VMAS_GRAPH_CHAIN_IN_POST", "1") != "0"
     # fused programs write the step's outputs into fresh tensors (DirectOutputs); 0: copied out
     _DIRECT = os.environ.get("VMAS_GRAPH_DIRECT_OUTPUTS", "1") != "0"
     # fresh entity-state tensors on first use after each replay (_FreshState); 0: the states stay
@@ -1187,9 +1193,9 @@ class StepGraph:
         that has no device asserts (rollback_free): the speculative replay without its backups and
         generator snapshot, which only a rollback reads."""
         self._first_replay = False
-        self._launch()
+        chain = self._launch(defer_chain=self._CHAIN_IN_POST)
         self.replays += 1
-        out = self._post_replay()
+        out = self._post_replay(chain=chain)
         self._finish_deferred(out=out)
         return out
 
@@ -1239,6 +1245,18 @@ class StepGraph:
         torch.cuda.set_rng_state(rng, self.env.device)
 
     # ---- copies after a replay -----------------------------------------------------------------
+    def _launch_chain(self, chain) -> None:
+        N.check(N.load_library().vmas_graph_chain_launch(chain.handle, N.stream_ptr(self._dev_index())),
+                "vmas_graph_chain_launch")
+
+    _chain_fn_addr = None
+
+    @classmethod
+    def _chain_fn(cls) -> int:
+        if cls._chain_fn_addr is None:
+            cls._chain_fn_addr = N.fn_addr("vmas_graph_chain_launch")
+        return cls._chain_fn_addr
+
     def _dev_index(self) -> int:
         dev = torch.device(self.env.device)
         return dev.index if dev.index is not None else torch.cuda.current_device()
@@ -1288,7 +1306,7 @@ class StepGraph:
         views, rest = self._clone_alloc(t)
         return t, views, rest
 
-    def _post_replay(self, prep=None):
+    def _post_replay(self, prep=None, chain=None):
         """After a replay, in ONE native launch (vmas_copy_spans): the fresh copies of the
         outputs, the carry of the re-bound state to the next step (Y -> X, which before_actions
         then skips while no Y changes) and the next step's backups (which backup() then skips
@@ -1296,12 +1314,17 @@ class StepGraph:
         of them lies in a carry destination (two launches).  The span table is built once per
         (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
         t = self._post_table() if prep is None else None
+        if chain is not None and (t is None or t["plain"] or t.get("host") is None):
+            self._launch_chain(chain)  # (a replay's kernel chain not yet launched: now, before anything else)
+            chain = None
         if t is not None and not t["plain"]:
-            # the common case in one C++ call (csrc/vmas_host.cpp OutputAlloc.post): fresh outputs,
-            # their addresses into the table, the launch(es)
+            # the common case in one C++ call (csrc/vmas_host.cpp OutputAlloc.post): the replay's
+            # kernel chain (chain: not launched yet), fresh outputs, their addresses into the table,
+            # the launch(es)
             if t["steps_row"] is not None:
                 self._steps_current(t)
             host = t.get("host") or self._host_alloc(t)
+            ch = (chain.addr, self._chain_fn()) if chain is not None else (0, 0)
             mid, hi = (t["n_out"] if t["clash"] else 0), t["n_all"]
             # (with a deferred launch -- discovery's respawn, whose host side advances the generator
             # after this -- the draw reads its offset where the respawn launch leaves it)
@@ -1311,10 +1334,10 @@ class StepGraph:
             if ahead is not None:  # (+ the next step's random actions in the same launch)
                 st, drawer, P = ahead
                 views, acts, snap, seed, off, inc = N.load_host().post_draw(
-                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"), off_dev)
+                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"), off_dev, *ch)
                 self.env._drew_ahead(st, acts, snap, seed, off, inc)
             else:
-                views = host.post(mid, hi)
+                views = host.post(mid, hi, *ch)
             rest = [(views[k], s) for k, s in t["loose"]]
             self._clone_finish(rest)
             self._post = {"carry_ver": tuple(map(_VERSION, self._carry_ys)),
