@@ -1,6 +1,8 @@
 """Spawn sampler: the native resolver of ScenarioUtils.find_random_pos_for_entity
 must return the reference loop's positions bit-for-bit AND leave the generator exactly where the
 reference loop leaves it (same number of uniform_ draws), so every later random number matches."""
+import time
+
 import pytest
 import torch
 
@@ -139,7 +141,7 @@ def test_respawn_targets_matches_reference_loop_gpu(gpu_device, monkeypatch, b, 
 @pytest.mark.gpu
 def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device, monkeypatch):
     """The one-launch respawn's resident kernel needs every 64-env group's workgroup running at
-    once.  Here a kernel on a second stream holds 250 CUs for 1.5 s -- longer than the
+    once.  Here a kernel on a second stream holds 250 CUs for 2 s -- longer than the
     launch's 1 s bounded wait -- so the groups that cannot start make the others time out.  The
     call then undoes the launch from its backup and redoes the respawn with the reference's loop:
     the reference's positions and generator use, no error."""
@@ -166,8 +168,9 @@ def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device, monkeypatch):
     g.manual_seed(12)
     side = torch.cuda.Stream()
     torch.cuda.synchronize()
-    N.check_aux(N.load_library().vmas_test_hold(0, 250, 1_500_000, ctypes.c_void_p(side.cuda_stream)),
+    N.check_aux(N.load_library().vmas_test_hold(0, 250, 2_000_000, ctypes.c_void_p(side.cuda_stream)),
                 "vmas_test_hold")
+    time.sleep(0.2)  # (the holding kernel resident before the respawn launch: not a race between the streams)
     mx = respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
     after_native = torch.rand(4, device=dev)
     torch.cuda.synchronize()
