@@ -650,10 +650,8 @@ struct WinArgs {
     uint32_t* part;   // [groups][T * 32]: a group's table, 4 start pairs (bytes) per word
     uint32_t* crow;   // [clusters][T * 32]: a cluster's table
     uint32_t* list;   // [cap][2 + 4 T]: env, covered bits, T 128-bit masks
-    int cap, pairs, q0, n_clusters;
+    int cap, pairs, q0;
 };
-// (max_accepted words) clusters whose row is stored: the last one runs the chain (the fused form)
-constexpr int kWinDoneWord = 48;
 constexpr int kWinCluster = 16;  // groups per cluster (the first reduction of the tables)
 // The window of a call: the previous call's consumption + kWinMargin tries, rounded up to 16 (its
 // chain kernel leaves it in the words at kWinNextWord; 0, or anything else, means the full window).
@@ -668,24 +666,6 @@ __host__ __device__ inline int win_cluster_word(int T) { return 96 + 32 * T; }
 
 __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// AG (the fused chain, which reads what other workgroups of its own launch wrote): agent-scope
-// loads / stores (another XCD's L2 may hold the lines); else plain ones (a kernel boundary between)
-template <bool AG>
-__device__ __forceinline__ void st_word(uint32_t* p, uint32_t v) {
-    if (AG) st_agent(p, v);
-    else *p = v;
-}
-template <bool AG>
-__device__ __forceinline__ uint32_t ld_word(const uint32_t* p) {
-    return AG ? ld_agent(p) : *p;
-}
-template <bool AG>
-__device__ __forceinline__ uint4 ld_row4(const uint4* p) {
-    if (!AG) return *p;
-    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
-    const unsigned long long lo = ld_agent(q), hi = ld_agent(q + 1);
-    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -768,18 +748,9 @@ __device__ __noinline__ float2 spawn_pair_call(float x_lo, float x_hi, float y_l
     return make_float2(uniform_at(seed, o, g, b, x_lo, x_hi, mode), uniform_at(seed, o + inc, g, b, y_lo, y_hi, mode));
 }
 
-template <bool Q0, bool AG>
-__device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, const DrawGrid& g, float d2_min,
-                                                 const WinArgs& wa, int n_rows, unsigned long long* prof,
-                                                 const ChanArgs& ch, unsigned char* win_lds);
-
 // ---- every group: candidates, masks, the group's table (and its listed envs) ----------------------
-// R pairs per wave (window 16 R); Q0: torch's grid covers the batch in one round (draw_q0).
-// FUSED: the last cluster's reducer then runs the chain (spawn_chain_body) in the same launch --
-// no kernel boundary between the tables and the chain (the launch then holds the chain's LDS: one
-// workgroup per CU, chosen when the groups fit the CUs); its rows, the listed envs and their count
-// go through agent-scope stores / loads.
-template <int R, bool Q0, bool FUSED = false>
+// R pairs per wave (window 16 R); Q0: torch's grid covers the batch in one round (draw_q0)
+template <int R, bool Q0>
 __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
                                                              WinArgs wa, unsigned long long* prof, ChanArgs ch) {
     extern __shared__ __align__(16) unsigned char win_lds[];
@@ -892,16 +863,10 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
         const int d = atomicAdd(&io.max_accepted[kWinListWord], 1);
         if (d < wa.cap) {
             uint32_t* e = wa.list + (long)d * (2 + 4 * T);
-            if (FUSED) {
-                st_agent(e, (uint32_t)b);
-                st_agent(e + 1, covm);
-                for (int q = 0; q < 4 * T; ++q) st_agent(e + 2 + q, okw[((q >> 2) * 64 + lane) * 4 + (q & 3)]);
-            } else {
-                e[0] = (uint32_t)b;
-                e[1] = covm;
-                for (int i = 0; i < T; ++i)
-                    *reinterpret_cast<uint4*>(e + 2 + 4 * i) = *reinterpret_cast<const uint4*>(&okw[(i * 64 + lane) * 4]);
-            }
+            e[0] = (uint32_t)b;
+            e[1] = covm;
+            for (int i = 0; i < T; ++i)
+                *reinterpret_cast<uint4*>(e + 2 + 4 * i) = *reinterpret_cast<const uint4*>(&okw[(i * 64 + lane) * 4]);
         }
     }
     __syncthreads();  // (the masks are in registers: the space becomes the table)
@@ -962,19 +927,7 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
         __syncthreads();
         if ((int)threadIdx.x < cols) {
             for (int r = 1; r < per; ++r) acc = bytes_max(acc, red[r * cols + threadIdx.x]);
-            st_word<FUSED>(wa.crow + (long)cl * cols + threadIdx.x, acc);
-        }
-        if (FUSED) {  // the last cluster stored: this workgroup runs the chain
-            __shared__ int chain_s;
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
-            if (threadIdx.x == 0) chain_s = atomicAdd(&io.max_accepted[kWinDoneWord], 1) == wa.n_clusters - 1;
-            __syncthreads();
-            if (chain_s) {
-                if (prof && threadIdx.x == 0) prof[32 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-                spawn_chain_body<Q0, true>(io, g, d2_min, wa, wa.n_clusters, prof, ch, win_lds);
-                return;
-            }
+            wa.crow[(long)cl * cols + threadIdx.x] = acc;
         }
     }
     if (prof && threadIdx.x == 0) prof[32 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -990,10 +943,11 @@ __global__ void __launch_bounds__(kWinThreads) k_spawn_cands(VmasSpawnTargetsIO 
 // target's clean maximum, the clean chain is the chain; else it is rebuilt from the first such
 // target with the listed envs' maxima, one target at a time (P_j for the targets before it are
 // right: their maxima held).
-template <bool Q0, bool AG>
-__device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, const DrawGrid& g, float d2_min,
-                                                 const WinArgs& wa, int n_rows, unsigned long long* prof,
-                                                 const ChanArgs& ch, unsigned char* win_lds) {
+template <bool Q0>
+__global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
+                                                             WinArgs wa, int n_rows, unsigned long long* prof,
+                                                             ChanArgs ch) {
+    extern __shared__ __align__(16) unsigned char win_lds[];
     __shared__ unsigned long long rng_s[3];
     __shared__ int red_s[2][kWinWaves];  // (double-buffered: one barrier per step)
     __shared__ int ps_s[VMAS_SPAWN_MAX_TARGETS + 1], mc_s[VMAS_SPAWN_MAX_TARGETS], lmax_s[VMAS_SPAWN_MAX_TARGETS];
@@ -1015,7 +969,7 @@ __device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, c
     const bool stamp = prof && threadIdx.x == 0;
     if (stamp) stamp_s[0] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) launch_rng(io, ch, &rng_s[0], &rng_s[1], &rng_s[2]);
-    const int n_listed = (int)ld_word<AG>(reinterpret_cast<const uint32_t*>(W + kWinListWord));
+    const int n_listed = W[kWinListWord];
     const int n_list = n_listed < cap ? n_listed : cap;
     if ((int)threadIdx.x < c4) {  // column c of the tables: max over every cluster's row, 16 loads in flight
         const uint4* src = reinterpret_cast<const uint4*>(wa.crow) + threadIdx.x;
@@ -1023,8 +977,7 @@ __device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, c
         for (int r0 = 0; r0 < n_rows; r0 += 16) {
             uint4 v[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                v[u] = r0 + u < n_rows ? ld_row4<AG>(src + (long)(r0 + u) * c4) : make_uint4(0u, 0u, 0u, 0u);
+            for (int u = 0; u < 16; ++u) v[u] = r0 + u < n_rows ? src[(long)(r0 + u) * c4] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 acc.x = bytes_max(acc.x, v[u].x);
@@ -1043,7 +996,7 @@ __device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, c
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int q = q0i + u * kWinThreads + (int)threadIdx.x;
-                v[u] = q < n_list * E ? ld_word<AG>(wa.list + q) : 0u;
+                v[u] = q < n_list * E ? wa.list[q] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1188,7 +1141,6 @@ __device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, c
     // the words the next call's candidates count on, back to zero (a prestaged call has no clear
     // kernel): the listed envs and every cluster's count (read above; the candidates are done)
     if (threadIdx.x == 0) W[kWinListWord] = 0;
-    if (AG && threadIdx.x == 0) W[kWinDoneWord] = 0;
     for (int c = (int)threadIdx.x; c < n_rows; c += kWinThreads) W[win_cluster_word(T) + c] = 0;
     if (threadIdx.x == 0) {
         int used = 0;  // (the tries the reference loop consumes: the next call's window from it)
@@ -1213,14 +1165,6 @@ __device__ __forceinline__ void spawn_chain_body(const VmasSpawnTargetsIO& io, c
     }
 }
 
-template <bool Q0>
-__global__ void __launch_bounds__(kWinThreads) k_spawn_chain(VmasSpawnTargetsIO io, DrawGrid g, float d2_min,
-                                                             WinArgs wa, int n_rows, unsigned long long* prof,
-                                                             ChanArgs ch) {
-    extern __shared__ __align__(16) unsigned char win_lds[];
-    spawn_chain_body<Q0, false>(io, g, d2_min, wa, n_rows, prof, ch, win_lds);
-}
-
 size_t win_cands_lds_bytes(int A, int T) {
     const size_t p1a = (size_t)(A + T) * 64 * 8 + (size_t)T * 64 * 16 + 64 * 4 + 3 * 8;
     const size_t p1b = (size_t)64 * (T * 32 + 1) * 4;
@@ -1230,21 +1174,6 @@ size_t win_cands_lds_bytes(int A, int T) {
 size_t win_chain_lds_bytes(int T) {
     const size_t cap = (size_t)win_list_cap(T);
     return cap * (44 * T + 8) + (size_t)T * kWinMaxPairs;
-}
-
-using CandsFn = void (*)(VmasSpawnTargetsIO, DrawGrid, float, WinArgs, unsigned long long*, ChanArgs);
-template <bool F>
-CandsFn pick_cands(int pairs, bool q0) {
-    switch (pairs * 2 + (q0 ? 1 : 0)) {
-        case 16 * 2 + 1: return k_spawn_cands<1, true, F>;
-        case 16 * 2: return k_spawn_cands<1, false, F>;
-        case 64 * 2 + 1: return k_spawn_cands<4, true, F>;
-        case 64 * 2: return k_spawn_cands<4, false, F>;
-        case 96 * 2 + 1: return k_spawn_cands<6, true, F>;
-        case 96 * 2: return k_spawn_cands<6, false, F>;
-        case 128 * 2 + 1: return k_spawn_cands<8, true, F>;
-        default: return k_spawn_cands<8, false, F>;
-    }
 }
 
 // The smallest float x >= 0 with sqrtf(x) >= min_dist (binary search over the ordered bit patterns
@@ -1421,11 +1350,10 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
     int cur = -1;
     VMAS_AUX_HIP(hipGetDevice(&cur));
     if (cur != device) VMAS_AUX_HIP(hipSetDevice(device));
-    static int max_blocks[64] = {0}, resident[64] = {0}, resident_static[64] = {0}, cus[64] = {0};
+    static int max_blocks[64] = {0}, resident[64] = {0}, resident_static[64] = {0};
     if (!max_blocks[device]) {
         hipDeviceProp_t prop;
         VMAS_AUX_HIP(hipGetDeviceProperties(&prop, device));
-        cus[device] = prop.multiProcessorCount;
         max_blocks[device] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / kUniformThreads);
         if (max_blocks[device] <= 0) return vmas_aux::fail(VMAS_E_HIP, "vmas_spawn_targets: device properties");
         int per_cu = 0;
@@ -1480,11 +1408,18 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
         const int cap = win_list_cap(T);
         const size_t lds1 = win_cands_lds_bytes(io->n_agents, T), lds2 = win_chain_lds_bytes(T);
         const bool q0 = g.step >= B;
-        // the chain inside the candidates launch (k_spawn_cands FUSED) when every group has a CU of its
-        // own (it then holds the chain's LDS); VMAS_SPAWN_FUSED_CHAIN=0: two launches (an A/B knob)
-        static const bool fuse_ok = !(getenv("VMAS_SPAWN_FUSED_CHAIN") && getenv("VMAS_SPAWN_FUSED_CHAIN")[0] == '0');
-        const bool fused = fuse_ok && n_groups <= cus[device];
-        CandsFn cands = fused ? pick_cands<true>(pairs, q0) : pick_cands<false>(pairs, q0);
+        using CandsFn = void (*)(VmasSpawnTargetsIO, DrawGrid, float, WinArgs, unsigned long long*, ChanArgs);
+        CandsFn cands = nullptr;
+        switch (pairs * 2 + (q0 ? 1 : 0)) {
+            case 16 * 2 + 1: cands = k_spawn_cands<1, true>; break;
+            case 16 * 2: cands = k_spawn_cands<1, false>; break;
+            case 64 * 2 + 1: cands = k_spawn_cands<4, true>; break;
+            case 64 * 2: cands = k_spawn_cands<4, false>; break;
+            case 96 * 2 + 1: cands = k_spawn_cands<6, true>; break;
+            case 96 * 2: cands = k_spawn_cands<6, false>; break;
+            case 128 * 2 + 1: cands = k_spawn_cands<8, true>; break;
+            default: cands = k_spawn_cands<8, false>; break;
+        }
         static bool attr[64] = {false};
         if (!attr[device]) {  // (as k_step: > 64 KiB of dynamic LDS; HIP on gfx950 may refuse the attribute and
                               // launch anyway -- the launch's own error check below is the one that counts)
@@ -1492,27 +1427,17 @@ int32_t vmas_spawn_targets(int32_t device, const VmasSpawnTargetsIO* io, uint64_
                                       (int)lds2);
             (void)hipFuncSetAttribute((const void*)k_spawn_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds2);
-            for (int pr : {16, 64, 96, 128})
-                for (bool qq : {true, false})
-                    (void)hipFuncSetAttribute((const void*)pick_cands<true>(pr, qq),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::max(lds1, lds2));
             (void)hipGetLastError();
             attr[device] = true;
         }
         const int n_clusters = (n_groups + kWinCluster - 1) / kWinCluster;
         uint32_t* sw = reinterpret_cast<uint32_t*>(io->scratch);
         WinArgs wa{sw, sw + (size_t)n_groups * T * 32, sw + (size_t)(n_groups + n_clusters) * T * 32, cap, pairs,
-                   q0 ? 1 : 0, n_clusters};
+                   q0 ? 1 : 0};
         if (!(io->prestaged && ch.in))  // (prestaged: cleaned by the previous call, staged by the step)
             hipLaunchKernelGGL(k_spawn_clear, dim3(1), dim3(256), 0, st, io->max_accepted, (int)VMAS_SPAWN_WORDS(T),
                                ch.in);
-        hipLaunchKernelGGL(cands, dim3((unsigned)n_groups), dim3(kWinThreads), fused ? std::max(lds1, lds2) : lds1, st,
-                           *io, g, d2_min, wa, prof, ch);
-        if (fused) {
-            VMAS_AUX_HIP(hipGetLastError());
-            *increment = g.inc;
-            return VMAS_OK;
-        }
+        hipLaunchKernelGGL(cands, dim3((unsigned)n_groups), dim3(kWinThreads), lds1, st, *io, g, d2_min, wa, prof, ch);
         if (q0)
             hipLaunchKernelGGL(k_spawn_chain<true>, dim3(1), dim3(kWinThreads), lds2, st, *io, g, d2_min, wa, n_clusters,
                                prof, ch);
