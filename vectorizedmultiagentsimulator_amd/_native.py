@@ -738,6 +738,13 @@ def load_host():
     return mod
 
 
+_fn_addrs = {}
+
+
 def fn_addr(name: str) -> int:
-    """Address of a C entry point of the loaded library (handed to _vmas_host)."""
-    return ctypes.cast(getattr(load_library(), name), ctypes.c_void_p).value
+    """Address of a C entry point of the loaded library (handed to _vmas_host; cached: the library
+    stays loaded for the process's life)."""
+    a = _fn_addrs.get(name)
+    if a is None:
+        a = _fn_addrs[name] = ctypes.cast(getattr(load_library(), name), ctypes.c_void_p).value
+    return a
