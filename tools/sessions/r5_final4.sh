@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5 closing evidence, fourth pass (the chain launched by the post-replay call):
-# smoke, the whole -m gpu suite, the bench lines, rocprofv3 of the default bench command, and the PMC
-# passes of the plain step kernel (eager bench: k_world without the epilogue, the kernel the headline times).
+# smoke, the whole -m gpu suite, the bench lines and rocprofv3 of the default bench command (k_world's
+# source is final3's: its PMC record stands).
 set -u
 OUT=${OUT:-gpurun_out/r5final4}; mkdir -p $OUT
 export TMPDIR=/tmp
