@@ -201,16 +201,21 @@ __device__ __forceinline__ void bal_done(IO& io, int b, bool og, const OutDelta&
     moved(io.done, od.done)[b] = (og || xdist_spheres(pk, gl, b) < 0.f) ? 1 : 0;
 }
 
+// (an A/B knob of the package / floor preload: -DVMAS_BAL_PRELOAD_POS=0 through VMAS_JIT_CFLAGS)
+#ifndef VMAS_BAL_PRELOAD_POS
+#define VMAS_BAL_PRELOAD_POS 1
+#endif
 // wave 0's own inputs of the reward block, loaded before the barrier (their latency under the
-// four waves' box queries instead of after them): the previous shaping and the goal position
+// four waves' box queries instead of after them): the previous shaping, the goal, package and
+// floor positions
 struct BalPre {
     float gs;
-    V2 goal;
+    V2 goal, pkg, pf;
 };
 template <class IO>
 __device__ __forceinline__ BalPre bal_preload(IO& io, int bb) {
-    const VmasShapeRef gl = io.goal;
-    return BalPre{io.global_shaping[(long)bb * io.gs_s0], ref_pos(gl, bb)};
+    const VmasShapeRef gl = io.goal, pk = io.package, fl = io.floor;
+    return BalPre{io.global_shaping[(long)bb * io.gs_s0], ref_pos(gl, bb), ref_pos(pk, bb), ref_pos(fl, bb)};
 }
 
 // The reward block of env b from the sides in Q: closest_line_box's and closest_point_box's
@@ -236,8 +241,12 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
             cp = mk(bal_q(Q, 16 + 3 * i)[lane], bal_q(Q, 16 + 3 * i + 1)[lane]);
         }
     }
-    const VmasShapeRef pk = io.package, fl = io.floor;
-    const V2 pkg = ref_pos(pk, b), goal = pre.goal, pf = ref_pos(fl, b);
+    const VmasShapeRef pk = io.package;
+#if VMAS_BAL_PRELOAD_POS
+    const V2 pkg = pre.pkg, goal = pre.goal, pf = pre.pf;  // (b == bb: wave 0's valid lanes only)
+#else
+    const V2 pkg = ref_pos(pk, b), goal = pre.goal, pf = ref_pos(io.floor, b);
+#endif
     // compute_on_the_ground: is_overlapping(line, floor) + is_overlapping(package, floor)
     // (canonical (box, line) / (box, sphere) branches, core.py:1932-1968)
     const float dsc = xnorm(pkg - cp), dsb = xnorm(pkg - pf), dcb = xnorm(pf - cp);
@@ -254,7 +263,10 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
     io.pos_rew[b] = pos_rew;
     const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
     for (int i = 0; i < io.n_agents; ++i) moved(io.rewards[i], od.rew)[b] = r;
-    if (io.what & VMAS_SCN_DONE) bal_done(io, b, og, od);
+    if (io.what & VMAS_SCN_DONE) {  // bal_done on the loaded positions (xdist_spheres' arithmetic)
+        const VmasShapeRef gl = io.goal;
+        moved(io.done, od.done)[b] = (og || (xnorm(pkg - goal) - pk.radius) - gl.radius < 0.f) ? 1 : 0;
+    }
 }
 
 // agent i's 16-entry observation in env b
@@ -287,7 +299,7 @@ __device__ __forceinline__ void balance_group(IO& io, int g, int wave, int nwave
     const int bb = valid ? b : io.batch - 1;
     const OutDelta od = load_out_delta(io);
     const bool rew = io.what & VMAS_SCN_REWARD;
-    const BalPre pre = rew && wave == 0 ? bal_preload(io, bb) : BalPre{0.f, mk(0.f, 0.f)};
+    const BalPre pre = rew && wave == 0 ? bal_preload(io, bb) : BalPre{0.f, mk(0.f, 0.f), mk(0.f, 0.f), mk(0.f, 0.f)};
     if (rew && wave < 4) bal_side(io, bb, wave, lane, Q);
     if ((io.what & VMAS_SCN_OBS) && wave >= 4 && valid)
         for (int i = wave - 4; i < io.n_agents; i += nwave - 4) bal_obs(io, b, i, od);
