@@ -111,25 +111,6 @@ _STEP_METHODS = ("reward", "observation", "done", "info", "pre_step", "post_step
                  "env_process_action", "extra_render")
 
 
-def _byte_ranges(pairs):
-    """The merged byte ranges [lo, hi) of the Y tensors of carried pairs that share their storages
-    (X and Y at the same offsets), or None when one is not contiguous."""
-    spans = []
-    for _, y in pairs:
-        if not y.is_contiguous():
-            return None
-        lo = y.storage_offset() * y.element_size()
-        spans.append((lo, lo + y.numel() * y.element_size()))
-    spans.sort()
-    out = [list(spans[0])]
-    for lo, hi in spans[1:]:
-        if lo <= out[-1][1]:
-            out[-1][1] = max(out[-1][1], hi)
-        else:
-            out.append([lo, hi])
-    return [tuple(r) for r in out]
-
-
 def _write_only(o, k: str) -> bool:
     """Attribute k of o is declared write-only within a step by o's own class (not inherited: a
     subclass may read it): `_vmas_graph_write_only`, a set of attribute names each step re-binds
@@ -1037,16 +1018,6 @@ class StepGraph:
         # sensors declare them): not carried; a rollback restores them from the backups (_inplace)
         own = self._WRITE_ONLY and _own_scenario(self.env.scenario)
         self._write_only_ys = []
-        # the agents whose dynamics re-bind state.force every step before anything reads it
-        # (Holonomic / HolonomicWithRotation.process_action: force = u view, so the captured
-        # step's kernels read the action buffer, never the previous force X): force not carried
-        forced = set()
-        if own and self._FORCE_WRITE_ONLY:
-            from ..dynamics.holonomic import Holonomic
-            from ..dynamics.holonomic_with_rot import HolonomicWithRotation
-            forced = {id(a._state) for a in self.env.world.agents
-                      if type(getattr(a, "dynamics", None)) in (Holonomic, HolonomicWithRotation)}
-        trimmed = set()  # Y storages with a pair left out of the carry
         for o, before in snap:
             after = o.__dict__
             for k, v0 in before.items():
@@ -1063,12 +1034,6 @@ class StepGraph:
                     continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
                 if own and _write_only(o, k):  # (no step reads X: Y needs no carry, see _write_only)
                     self._write_only_ys.append(v1)
-                    continue
-                if k == "_force" and id(o) in forced:  # (as a write-only attribute; still a fresh state)
-                    self._write_only_ys.append(v1)
-                    trimmed.add(_storage_key(v1))
-                    if hasattr(type(o), "_fresh"):
-                        fresh.append((after, k, v1))
                     continue
                 carry.append((v0, v1))
                 names.append(f"{type(o).__name__}.{k}")
@@ -1093,14 +1058,7 @@ class StepGraph:
             whole = (len(pairs) > 1 and sx.nbytes() == sy.nbytes()
                      and all(x.storage_offset() == y.storage_offset() and x.stride() == y.stride()
                              for x, y in pairs))
-            ranges = _byte_ranges(pairs) if whole and _storage_key(y0) in trimmed else None
-            if ranges is not None:  # (a pair left out: the carried pairs' merged byte ranges only)
-                bx = torch.empty(0, dtype=torch.uint8, device=x0.device).set_(sx)
-                by = torch.empty(0, dtype=torch.uint8, device=y0.device).set_(sy)
-                for lo, hi in ranges:
-                    dst.append(bx[lo:hi])
-                    src.append(by[lo:hi])
-            elif whole:
+            if whole:
                 dst.append(torch.empty(0, dtype=torch.uint8, device=x0.device).set_(sx))
                 src.append(torch.empty(0, dtype=torch.uint8, device=y0.device).set_(sy))
             else:
@@ -1186,8 +1144,6 @@ class StepGraph:
     _FRESH_STATES = os.environ.get("VMAS_GRAPH_FRESH_STATES", "1") != "0"
     # declared write-only attributes (_write_only) are not carried between replays; 0: carried
     _WRITE_ONLY = os.environ.get("VMAS_GRAPH_WRITE_ONLY", "1") != "0"
-    # holonomic agents' state.force left out of the carry (_plan); 0: carried (A/B knob)
-    _FORCE_WRITE_ONLY = os.environ.get("VMAS_GRAPH_FORCE_WRITE_ONLY", "1") != "0"
 
     def _replay(self):
         asserts = self._asserts is not None and bool(self._asserts.msgs)
