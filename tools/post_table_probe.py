@@ -37,6 +37,10 @@ print(f"rows: {n_out} output (+ direct words / step counter), {len(carry_rows)} 
 print(f"bytes: outputs {out_b / 1e6:.2f} MB, carry {sum(int(r['nbytes']) for r in carry_rows) / 1e6:.2f} MB, "
       f"backups {sum(int(r['nbytes']) for r in bk_rows) / 1e6:.2f} MB")
 print("carried attributes:", getattr(g, "_carry_names", "?"))
+from vectorizedmultiagentsimulator_amd.simulator.environment._graph import _own_scenario  # noqa: E402
+print("own scenario:", _own_scenario(env.scenario), "; agent dynamics:",
+      sorted({type(getattr(a, "dynamics", None)).__module__ + "." + type(getattr(a, "dynamics", None)).__name__
+              for a in env.world.agents}), "; write-only ys:", len(g._write_only_ys))
 print("in-place (backed up) tensors:", len(g._inplace), [tuple(x.shape) for x in g._inplace][:12])
 print("direct categories:", len(g._direct.enabled) if g._direct is not None else 0,
       "; clone groups:", [(str(dt), tuple(sh), n) for dt, sh, n in g._clone_groups])
