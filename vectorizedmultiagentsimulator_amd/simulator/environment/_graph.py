@@ -62,6 +62,7 @@ import torch
 from torch import Tensor
 
 from ... import _native as N
+from ..core import Agent
 
 _VERSION = operator.attrgetter("_version")  # a tensor's version counter (map() without a Python frame)
 
@@ -111,11 +112,16 @@ _STEP_METHODS = ("reward", "observation", "done", "info", "pre_step", "post_step
                  "env_process_action", "extra_render")
 
 
-def _write_only(o, k: str) -> bool:
+def _write_only(o, k: str, scn_cls=None) -> bool:
     """Attribute k of o is declared write-only within a step by o's own class (not inherited: a
     subclass may read it): `_vmas_graph_write_only`, a set of attribute names each step re-binds
-    before anything in the step reads it.  The replays then need no carry of its previous value."""
-    return k in type(o).__dict__.get("_vmas_graph_write_only", ())
+    before anything in the step reads it -- or, for an attribute the scenario sets on its agents,
+    by the scenario class (`_vmas_graph_write_only_agents`).  The replays then need no carry of its
+    previous value."""
+    if k in type(o).__dict__.get("_vmas_graph_write_only", ()):
+        return True
+    return (scn_cls is not None and isinstance(o, Agent)
+            and k in scn_cls.__dict__.get("_vmas_graph_write_only_agents", ()))
 
 
 def _host_rng_states():
@@ -1032,7 +1038,7 @@ class StepGraph:
                 if (_storage_key(v1) == _storage_key(v0) and v1.storage_offset() == v0.storage_offset()
                         and v1.stride() == v0.stride()):
                     continue  # a new view of the same memory (e.g. force = u[:, :2] every step)
-                if own and _write_only(o, k):  # (no step reads X: Y needs no carry, see _write_only)
+                if own and _write_only(o, k, type(self.env.scenario)):  # (no step reads X: no carry, see _write_only)
                     self._write_only_ys.append(v1)
                     continue
                 carry.append((v0, v1))
