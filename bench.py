@@ -8,9 +8,14 @@ every rank simulates its own 32 768 independent envs, no data-path collective).
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus:
-  roofline      -- HBM roofline of the dominant kernel (k_step), timed with HIP events on its
-                   launch stream inside the library; algorithmic bytes per env-step from
-                   SURVEY.md §8d (24*E_all + 24*E_dyn + 12*A)
+  roofline      -- HBM roofline of the dominant kernel (k_world, the world-specialised step
+                   kernel; k_step on worlds it cannot specialise): algorithmic bytes per env-step
+                   from SURVEY.md §8d (24*E_all + 24*E_dyn + 12*A) over its time per
+                   launch, HIP events on the stream it runs on; `frac` is the variant the timed
+                   steps run (with the scenario program as its epilogue when the replay fuses it),
+                   `plain` the step kernel alone
+  process_group -- (N > 1) the live group: backend, world size, per-rank rates and each rank's
+                   device identity (PCI address / UUID of its GPU)
   cpu_baseline  -- the CPU oracle (PyTorch restatement of the reference tensor program) driving
                    the same host layer, timed on this host on a bounded sample (rank 0, N=1)
 """
@@ -20,6 +25,7 @@ import argparse
 import hashlib
 import json
 import os
+import socket
 import statistics
 import subprocess
 import sys
@@ -294,6 +300,26 @@ def cpu_baseline(args):
     }
 
 
+def device_identity(device: str, rank: int, local_rank: int) -> dict:
+    """Which device this rank ran on, as the rank itself sees it: the PCI address and UUID of its
+    GPU (torch.cuda.get_device_properties), the visible-device lists it was started with, its host
+    and pid -- so a multi-GPU line can show that N distinct GPUs ran (VERDICT r5 "Next" #8)."""
+    ident = {"rank": rank, "local_rank": local_rank, "device": device, "host": socket.gethostname(),
+             "pid": os.getpid()}
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if os.environ.get(k) is not None:
+            ident[k] = os.environ[k]
+    if device.startswith("cuda"):
+        pr = torch.cuda.get_device_properties(torch.device(device))
+        ident["pci"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+        ident["uuid"] = str(getattr(pr, "uuid", ""))
+        ident["name"] = pr.name
+        ident["key"] = f"{ident['host']}/{ident['pci']}"
+    else:  # (CPU ranks: distinct processes)
+        ident["key"] = f"{ident['host']}/cpu/pid{ident['pid']}"
+    return ident
+
+
 def free_port() -> int:
     import socket
 
@@ -426,9 +452,13 @@ def main():
         dist.all_gather(ranks, t)
         per_rank = [args.envs * args.steps / float(r.item()) for r in ranks]
         elapsed = max(float(r.item()) for r in ranks)
+        idents = [None] * dist.get_world_size()
+        dist.all_gather_object(idents, device_identity(device, rank, local_rank))
         group = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
                  "per_rank_env_steps_per_s": [round(r, 1) for r in per_rank],
-                 "timing": "max over ranks of each rank's barrier-bracketed wall time"}
+                 "timing": "max over ranks of each rank's barrier-bracketed wall time",
+                 "devices": idents,
+                 "distinct_devices": len({d["key"] for d in idents})}
         world_size = dist.get_world_size()
 
     total_envs = args.envs * world_size

@@ -247,6 +247,14 @@ int32_t vmas_graph_chain_nodes(const VmasKernelChain* chain); /* launches per re
  * scenario program as the epilogue, Args.epi set; VMAS_GRAPH_FUSE=0 disables) */
 int32_t vmas_graph_chain_fused(const VmasKernelChain* chain);
 int32_t vmas_graph_chain_free(VmasKernelChain* chain);
+/* The state write-back variant of a chain (graph mode's rollback-free replays; no reference
+ * counterpart): the chain's k_world launch with its backup delta set, so the step also writes its
+ * integrated state into its own input tensors (a re-run fixed-point pass reads the pre-step state
+ * from input + backup_delta, which the first pass stores) and the replay needs no post-replay carry
+ * of that state.  set: VMAS_E_UNSUPPORTED when the chain has no k_world launch; 0 removes it.
+ * launch_wb: vmas_graph_chain_launch with that variant. */
+int32_t vmas_graph_chain_set_writeback(VmasKernelChain* chain, int64_t backup_delta);
+int32_t vmas_graph_chain_launch_wb(const VmasKernelChain* chain, void* stream);
 /* Host waits on the device performed by the library so far (stream / event synchronisations and
  * spins on published words; wraps around): graph mode runs one step between two reads of it to
  * tell whether the step can be captured (no reference counterpart). */

@@ -203,10 +203,12 @@ def test_fast_lidar_rotated_agents_gpu(gpu_device):
 
 
 @pytest.mark.gpu
-def test_relaxed_trig_large_rotation_gpu(gpu_device):
+@pytest.mark.parametrize("max_turns", [60, 16_000, 160_000], ids=["4e2rad", "1e5rad", "1e6rad"])
+def test_relaxed_trig_large_rotation_gpu(gpu_device, max_turns):
     """Relaxed math (the GPU default of jointless worlds) with rotatable boxes and lines turned by
-    hundreds of radians (the reference never wraps rot, core.py:2907): one teacher-forced step
-    against the oracle (entity trig beyond 16 rad goes through the library sin / cos)."""
+    up to 4e2 / 1e5 / 1e6 radians (the reference never wraps rot, core.py:2907): one teacher-forced
+    step against the oracle (the entity trig's branch-free 2 pi reduction, vmas_physics.hpp red2pi:
+    accurate to ~2e-7 well past these magnitudes)."""
     from oracle import vmas_oracle as O
     from tests._parity import make
 
@@ -215,7 +217,7 @@ def test_relaxed_trig_large_rotation_gpu(gpu_device):
     g = torch.Generator(device="cpu").manual_seed(1)
     for e in env.world.entities:
         if e.rotatable:
-            turns = torch.randint(-60, 61, (2048, 1), generator=g).float() * (2 * math.pi)
+            turns = torch.randint(-max_turns, max_turns + 1, (2048, 1), generator=g).float() * (2 * math.pi)
             e.set_rot(e.state.rot + turns.to(gpu_device), batch_index=None)
     rep = O.compare_one_step(env.world)
     assert "VMAS_PHYS_RELAXED" in env.world.engine.jit_source()

@@ -383,19 +383,28 @@ def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,kw,substeps", [("balance", dict(n_agents=4), 10), ("flocking", dict(n_agents=4), None),
                                                ("discovery", dict(n_agents=4), None),
-                                               ("discovery-redo", dict(n_agents=4), None)],
-                         ids=["balance", "flocking", "discovery", "discovery-redo"])
+                                               ("discovery-redo", dict(n_agents=4), None),
+                                               ("balance-2pass", dict(n_agents=4), 10),
+                                               ("transport-2pass", dict(n_agents=4), None)],
+                         ids=["balance", "flocking", "discovery", "discovery-redo", "balance-2pass", "transport-2pass"])
 def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name, kw, substeps):
     """env.step(env.get_random_actions()) in graph mode: the draw kernel also writes the applied
     actions into the graph's action buffer, and the step launches no action kernel.  Bit-identical
     to the eager step on the same draws; an in-place edit of the drawn tensors, or other tensors,
     take the normal action path.  Discovery: the next draw is made ahead at the generator offset
     the in-graph respawn leaves on the device; "discovery-redo" hands every respawn over to the
-    reference loop (VMAS_SPAWN_TEST_MAX_TRIES=1), so every such draw is dropped and made anew."""
+    reference loop (VMAS_SPAWN_TEST_MAX_TRIES=1), so every such draw is dropped and made anew.
+    A pre-applied replay of a kernel chain writes the step's state back into its inputs (no carry,
+    StepGraph._writeback_ready); "-2pass" forces a second fixed-point pass on every step
+    (VMAS_JIT_TEST_PASSES=2), whose re-run reads the pre-step state from the first pass's backup."""
     redo = name == "discovery-redo"
     if redo:
         monkeypatch.setenv("VMAS_SPAWN_TEST_MAX_TRIES", "1")
         name = "discovery"
+    two_pass = name.endswith("-2pass")
+    if two_pass:
+        monkeypatch.setenv("VMAS_JIT_TEST_PASSES", "2")
+        name = name[:-len("-2pass")]
     eager, graph = _twin_envs(gpu_device, name, **kw)
     for env in (eager, graph):
         if substeps:
@@ -436,6 +445,15 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name
         assert graph._SPEC_DRAW and getattr(graph, "drawn_ahead", 0) >= 3
     if redo:
         assert getattr(graph, "drawn_ahead", 0) == 0
+    if name in ("balance", "flocking", "transport"):  # (kernel-chain replays: the state written back by k_world)
+        wb = graph._graph._wb
+        assert isinstance(wb, dict) and wb["chain"] is graph._graph._chain, (wb, graph._graph.chain_why)
+        x = graph._graph._carry_dst[graph._graph._state_idx]
+        tbl = graph._graph._post_cache_wb[4]["tbl"]
+        assert x.data_ptr() not in {int(r["dst"]) for r in tbl}  # (no carry span into the state buffer)
+    if two_pass:
+        assert "VMAS_GRID_MIN_PASSES 2" in graph.world.engine.jit_source()
+        assert graph.world.engine.last_iterations == 2
 
 
 @pytest.mark.gpu
@@ -623,3 +641,148 @@ def test_kernel_chain_replay_matches_graph_launch_gpu(gpu_device, name, kw, subs
         fused = name in ("balance", "transport")
         assert a._graph._chain.fused == int(fused)
         assert a._graph._chain.n_nodes == 1 if fused else a._graph._chain.n_nodes >= 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw,substeps", CHAIN_CASES[:2], ids=[c[0] for c in CHAIN_CASES[:2]])
+def test_fused_epilogue_rerun_by_a_second_pass_matches_eager_gpu(gpu_device, monkeypatch, name, kw, substeps):
+    """a replay whose k_world runs the scenario program as its epilogue re-runs the
+    program after every fixed-point pass of a group.  With a second pass forced on every step
+    (VMAS_JIT_TEST_PASSES=2: the decider treats pass 0 as violated) the fused replay still equals
+    the one-pass eager step bit for bit -- the programs are idempotent (global shaping written out of
+    place, the old pos_rew zeroed) -- through a reset_at and a full reset."""
+    envs = []
+    for forced in (True, False):
+        if forced:
+            monkeypatch.setenv("VMAS_JIT_TEST_PASSES", "2")
+        else:
+            monkeypatch.delenv("VMAS_JIT_TEST_PASSES", raising=False)
+        saved = _rng_save()
+        env = make_env(name, num_envs=1024, device=gpu_device, seed=3, graph_step=forced, **kw)
+        if substeps:
+            env.world._substeps = substeps
+            env.world._sub_dt = env.world._dt / substeps
+        env.world.engine._ensure()  # (the knob is read when the kernel is generated)
+        envs.append(env)
+        if forced:
+            _rng_load(saved)
+    a, b = envs
+    gen = torch.Generator(device=gpu_device).manual_seed(6)
+    for t in range(12):
+        actions = [torch.rand(1024, ag.action_size, device=gpu_device, generator=gen) * 2 - 1 for ag in a.agents]
+        if t in (7, 10):
+            for env in (a, b):
+                s = _rng_save()
+                env.reset_at(5) if t == 7 else env.reset()
+                _rng_load(s)
+        outs = _step_both(a, b, actions)
+        _assert_same(outs[0], outs[1], f"{name} outputs step {t}")
+        _assert_same(_state(a), _state(b), f"{name} state step {t}")
+    assert a.graph_status == "graph", a.graph_reason
+    assert a._graph._chain is not None and a._graph._chain.fused == 1, a._graph.chain_why
+    assert "VMAS_GRID_MIN_PASSES 2" in a.world.engine.jit_source()
+    assert a.world.engine.last_iterations == 2 and b.world.engine.last_iterations == 1
+
+
+# ---- a user's scenario (not one of the package's) on the default step (VERDICT r5 "Next" #7) -----
+from vectorizedmultiagentsimulator_amd.simulator.core import Agent, Box, Landmark, Line, Sphere, World  # noqa: E402
+from vectorizedmultiagentsimulator_amd.simulator.scenario import BaseScenario  # noqa: E402
+
+
+class PushScenario(BaseScenario):
+    """A small scenario written the way a user writes one (reference API only): agents push a box to
+    a goal past a wall line; shaping reward kept in a device tensor, per-agent collision counts."""
+
+    def make_world(self, batch_dim, device, n_agents=3, history=False):
+        world = World(batch_dim, device, substeps=3, x_semidim=1.2, y_semidim=1.2)
+        for i in range(n_agents):
+            world.add_agent(Agent(name=f"agent_{i}", shape=Sphere(0.05), u_multiplier=0.8))
+        self.box = Landmark(name="box", shape=Box(length=0.3, width=0.2), movable=True, rotatable=True, mass=2.0)
+        world.add_landmark(self.box)
+        self.goal = Landmark(name="goal", shape=Sphere(0.08), collide=False)
+        world.add_landmark(self.goal)
+        world.add_landmark(Landmark(name="wall", shape=Line(length=1.0)))
+        self.shaping = torch.zeros(batch_dim, device=device)
+        self.history = [] if history else None
+        return world
+
+    def reset_world_at(self, env_index=None):
+        n = 1 if env_index is not None else self.world.batch_dim
+        dev = self.world.device
+        for i, a in enumerate(self.world.agents):
+            a.set_pos(torch.rand(n, 2, device=dev) * 1.6 - 0.8, batch_index=env_index)
+        self.box.set_pos(torch.rand(n, 2, device=dev) * 0.8 - 0.4, batch_index=env_index)
+        self.box.set_rot(torch.rand(n, 1, device=dev) * 3.0, batch_index=env_index)
+        self.goal.set_pos(torch.tensor([[0.9, 0.9]], device=dev).expand(n, 2), batch_index=env_index)
+        wall = self.world.landmarks[2]
+        wall.set_pos(torch.tensor([[0.0, -0.9]], device=dev).expand(n, 2), batch_index=env_index)
+        d = torch.linalg.vector_norm(self.box.state.pos - self.goal.state.pos, dim=-1)
+        if env_index is None:
+            self.shaping = d * 10
+        else:
+            self.shaping[env_index] = d[env_index] * 10
+
+    def reward(self, agent):
+        if agent is self.world.agents[0]:
+            d = torch.linalg.vector_norm(self.box.state.pos - self.goal.state.pos, dim=-1)
+            new = d * 10
+            self.rew = self.shaping - new
+            self.shaping = new
+            if self.history is not None:
+                self.history.append(1)  # (Python-side step state: a replay would freeze it)
+        close = torch.linalg.vector_norm(agent.state.pos - self.box.state.pos, dim=-1) < 0.25
+        return self.rew + close.float() * 0.01
+
+    def observation(self, agent):
+        return torch.cat([agent.state.pos, agent.state.vel, self.box.state.pos - agent.state.pos,
+                          self.box.state.rot, self.goal.state.pos - self.box.state.pos], dim=-1)
+
+    def info(self, agent):
+        return {"dist": torch.linalg.vector_norm(self.box.state.pos - self.goal.state.pos, dim=-1)}
+
+
+@pytest.mark.gpu
+def test_user_scenario_replays_by_default_and_matches_eager_gpu(gpu_device):
+    """A scenario defined outside the package gets the graph step from make_env's default
+    (graph_step=None; environment.py _auto_graph_step) -- untrusted: no write-only attributes, no
+    direct outputs, no state write-back -- and matches its eager twin bit for bit through reset_at
+    and reset."""
+    envs = []
+    for graph in (None, False):
+        saved = _rng_save()
+        envs.append(make_env(PushScenario(), num_envs=512, device=gpu_device, seed=4, graph_step=graph))
+        if graph is None:
+            _rng_load(saved)
+    auto, eager = envs
+    assert auto.graph_auto and auto._graph is not None
+    gen = torch.Generator(device=gpu_device).manual_seed(8)
+    for t in range(14):
+        actions = [torch.rand(512, 2, device=gpu_device, generator=gen) * 2 - 1 for _ in auto.agents]
+        if t == 6:
+            for env in (auto, eager):
+                s2 = _rng_save()
+                env.reset_at(7)
+                _rng_load(s2)
+        if t == 10:
+            for env in (auto, eager):
+                s2 = _rng_save()
+                env.reset()
+                _rng_load(s2)
+        outs = _step_both(eager, auto, actions)
+        _assert_same(outs[0], outs[1], f"user scenario outputs step {t}")
+        _assert_same(_state(eager), _state(auto), f"user scenario state step {t}")
+    assert auto.graph_status == "graph", auto.graph_reason
+    g = auto._graph
+    assert g.replays >= 5 and not g._write_only_ys and not (g._direct and g._direct.enabled)
+    assert g._wb in (None, False)  # (untrusted: the carry stays)
+
+
+@pytest.mark.gpu
+def test_user_scenario_with_python_step_state_stays_eager_gpu(gpu_device):
+    """The same scenario keeping Python-side step state in a list it appends to (an in-place change
+    the plain-attribute watch cannot see): the strict watch of an untrusted scenario keeps it eager."""
+    env = make_env(PushScenario(), num_envs=64, device=gpu_device, seed=0, history=True)
+    for _ in range(5):
+        env.step(env.get_random_actions())
+    assert env.graph_status == "eager", env.graph_reason
+    assert "Python-side state" in env.graph_reason and "history" in env.graph_reason, env.graph_reason

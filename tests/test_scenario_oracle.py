@@ -101,6 +101,55 @@ def test_oracle_catches_a_misread_program_cpu(mutation):
     assert not sp.ok
 
 
+# ---- the scenarios' construction, independently of the product (VERDICT r5 "Next" #4) -----------
+BUILD_CASES = [
+    ("balance", dict(n_agents=4)), ("transport", dict(n_agents=4)),
+    ("discovery", dict(n_agents=8, use_agent_lidar=True)), ("flocking", dict(n_agents=8)),
+    ("balance", {}), ("transport", dict(n_agents=3, n_packages=2)), ("discovery", {}), ("flocking", {}),
+]
+
+
+@pytest.mark.parametrize("name,kw", BUILD_CASES, ids=[f"{c[0]}-{'-'.join(f'{k}{v}' for k, v in c[1].items())}"
+                                                     for c in BUILD_CASES])
+def test_make_env_world_matches_reference_construction_cpu(name, kw):
+    """Every world / entity / agent / LIDAR constant a benchmark scenario's make_world sets (world
+    dt, substeps, drag, collision force, gravity, semidims; each entity's shape, mass, movable /
+    rotatable / collide; each agent's u_multiplier, u_range and LIDARs) equals the oracle's table,
+    restated from the reference's files with their file:line (oracle/vmas_scenario_oracle.py
+    scenario_construction)."""
+    env = make_env(name, num_envs=4, device="cpu", seed=0, **kw)
+    bad = SO.construction_mismatches(SO.scenario_construction(name, **kw), SO.world_construction(env.world))
+    assert not bad, bad
+
+
+def _line(env):
+    return next(e for e in env.world.entities if e.name == "line")
+
+
+MUTATIONS = {
+    "line_length": ("balance", lambda env: setattr(_line(env).shape, "_length", 0.81)),
+    "agent_radius": ("balance", lambda env: setattr(env.agents[0].shape, "_radius", 0.031)),
+    "u_multiplier": ("transport", lambda env: setattr(env.agents[2].action, "_u_multiplier", 0.61)),
+    "collision_force": ("discovery", lambda env: setattr(env.world, "_collision_force", 499.0)),
+    "substeps": ("flocking", lambda env: setattr(env.world, "_substeps", 4)),
+    "lidar_range": ("flocking", lambda env: setattr(env.agents[1].sensors[0], "_max_range", 0.21)),
+    "package_mass": ("balance", lambda env: setattr(env.world.landmarks[1], "_mass", 5.5)),
+}
+
+
+@pytest.mark.parametrize("mutation", sorted(MUTATIONS))
+def test_construction_pin_catches_a_misread_constant_cpu(mutation):
+    """Not vacuous: one constant of a product world changed after make_world (as a misread constant
+    in a product scenario would leave it) fails the comparison, naming the field."""
+    name, mutate = MUTATIONS[mutation]
+    kw = dict(n_agents=4)
+    env = make_env(name, num_envs=4, device="cpu", seed=0, **kw)
+    assert not SO.construction_mismatches(SO.scenario_construction(name, **kw), SO.world_construction(env.world))
+    mutate(env)
+    bad = SO.construction_mismatches(SO.scenario_construction(name, **kw), SO.world_construction(env.world))
+    assert len(bad) == 1, bad
+
+
 # ---- GPU worlds: fused actions + fused scenario programs vs the oracle ---------------------------
 FULL = [
     ("balance", dict(n_agents=4), 10, 32768, "C2"),

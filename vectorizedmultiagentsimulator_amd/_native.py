@@ -60,6 +60,8 @@ EXPORTED_SYMBOLS = (
     "vmas_graph_chain_free",
     "vmas_graph_chain_nodes",
     "vmas_graph_chain_fused",
+    "vmas_graph_chain_set_writeback",
+    "vmas_graph_chain_launch_wb",
     "vmas_jit_world_epilogue",
     "vmas_jit_program_outputs",
     "vmas_host_waits",
@@ -592,6 +594,10 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_graph_chain_nodes.argtypes = [_vp]
     lib.vmas_graph_chain_fused.restype = _i32
     lib.vmas_graph_chain_fused.argtypes = [_vp]
+    lib.vmas_graph_chain_set_writeback.restype = _i32
+    lib.vmas_graph_chain_set_writeback.argtypes = [_vp, ctypes.c_int64]
+    lib.vmas_graph_chain_launch_wb.restype = _i32
+    lib.vmas_graph_chain_launch_wb.argtypes = [_vp, _vp]
     lib.vmas_graph_chain_free.argtypes = [_vp]
     lib.vmas_world_create.restype = _i32
     lib.vmas_world_create.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]

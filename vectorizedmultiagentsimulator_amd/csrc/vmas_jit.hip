@@ -193,7 +193,12 @@ struct Gen {
     // exceed one workgroup's LDS (hundreds of box pairs) still run the world-specialised step and
     // its persistent fixed point; the rows' traffic then goes through L1 / L2
     bool global_rows = false;
-    int nw = kNW;         // waves per workgroup
+    int nw = kNW;         // waves per 64-env group
+    // 64-env groups per claimed work item (VMAS_JIT_NG, A/B): ng > 1 runs ng groups in one
+    // workgroup of nw * ng waves in lockstep -- waves [k * nw, (k + 1) * nw) run group k's copy of
+    // the per-wave code on its own LDS rows, all sharing the workgroup's barriers -- so the groups a
+    // CU holds finish together instead of the second workgroup of a CU trailing the first
+    int ng = 1;
     int prof_block = -1;  // >= 0: stamp s_memtime at every phase boundary of this workgroup
     bool relaxed = false;  // relaxed fp32 math (VMAS_JIT_MATH=relaxed, worlds without joints; see compile())
     int prio_mode = 1;     // VMAS_JIT_PRIO=0 turns off the wave issue priority falling with the substep
@@ -367,9 +372,9 @@ struct Gen {
         for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : res_rows(p));
         // rows + FL + DONE + the pass's mask words + the fixed point's reduction words (in the
         // row buffer when it is large enough)
-        const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 >= nfl + 2) ? 0 : nfl + 2;
-        const long lds = (global_rows ? 0L : (long)n_rows * 256) + (long)nfl * 4 + 4 * (n_split + 1) + 4L * (nfl / 2) +
-                         4 * red + (has_epi() && !epi_q_in_rows() ? (long)kEpiQRows * 256 : 0L) +
+        const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 * ng >= nfl + 2) ? 0 : nfl + 2;
+        const long lds = (global_rows ? 0L : (long)n_rows * 256 * ng) + (long)nfl * 4 + 4 * (n_split * ng + 1) +
+                         4L * (nfl / 2) + 4 * red + (has_epi() && !epi_q_in_rows() ? (long)kEpiQRows * 256 * ng : 0L) +
                          (has_epi() && epi_lds ? (long)(cfg.epilogue == VMAS_EPILOGUE_BALANCE ? sizeof(VmasBalanceIO)
                                                                                             : sizeof(VmasTransportIO)) : 0L);
         if (lds > lds_budget) {
@@ -424,10 +429,12 @@ struct Gen {
     bool epi_q_in_rows() const { return !global_rows && n_rows >= kEpiQRows; }
     // byte offset of Args.epi (after the fixed pointers: the value slots follow it)
     size_t epi_offset() const { return 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)); }
+    // byte offset of Args.wbd (after epi): the state write-back's backup delta (0: off; see wb_text)
+    size_t wbd_offset() const { return epi_offset() + (has_epi() ? 8 : 0); }
 
     size_t arg_bytes() const {  // layout of the generated struct Args
         // (+4 ints: B, S, sdt, max_pass; then the value slots; padded to the 8-byte alignment)
-        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0) + (has_epi() ? 1 : 0)) +
+        const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0) + (has_epi() ? 1 : 0) + 1) +
                          4 * (std::max<size_t>(str_src.size(), 2) + 4) +
                          4 * prm_src.size();
         return (n + 7) & ~(size_t)7;
@@ -487,10 +494,13 @@ struct Gen {
     }
     std::string P_(Src s, int i) const { return "a.ptr[" + it(ptr_of[s][i]) + "]"; }
     std::string S_(Src s, int k, int i) const { return "a.str[" + it(str_of[s][k][i]) + "]"; }
-    std::string ld2(Src s, int i) const {
-        return "ld2(" + P_(s, i) + ", " + S_(s, 0, i) + ", " + S_(s, 1, i) + ", bb)";
+    // rb: a field the state write-back overwrites, read from the backup in a re-run pass (rbd)
+    std::string ld2(Src s, int i, bool rb = false) const {
+        return "ld2(" + (rb ? "rbp(" + P_(s, i) + ", rbd)" : P_(s, i)) + ", " + S_(s, 0, i) + ", " + S_(s, 1, i) + ", bb)";
     }
-    std::string ld1(Src s, int i) const { return P_(s, i) + "[(long)bb * " + S_(s, 0, i) + "]"; }
+    std::string ld1(Src s, int i, bool rb = false) const {
+        return (rb ? "rbp(" + P_(s, i) + ", rbd)" : P_(s, i)) + "[(long)bb * " + S_(s, 0, i) + "]";
+    }
     std::string mbit(int p) const { return "(m" + it(p >> 5) + " & " + it(1u << (p & 31)) + "u)"; }
     // first of the 4 result rows (fa.x, fa.y, ta, tb) of pair p
     int res(int p) const { return split[p] ? r_res[p] + 4 * parts(pd[p].cls) + 4 : r_res[p]; }
@@ -764,7 +774,7 @@ struct Gen {
     void wave_body(std::string& o, int w) {
         o += "template <> __device__ __forceinline__ void run<" + it(w) +
              ">(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, "
-             "bool valid) {\n";
+             "bool valid, long long rbd, bool bk, bool wbk) {\n";
         // prologue: static pair entities (loaded once), dynamic entities into registers
         for (int e : wave_static[w]) {
             o += "    {  // static entity " + it(e) + "\n";
@@ -779,8 +789,20 @@ struct Gen {
         for (int e : wave_ents[w]) {
             const VmasEntityDesc& d = ed[e];
             const std::string s = it(e);
-            o += "    V2 p" + s + " = " + ld2(S_POS, e) + ", v" + s + " = " + ld2(S_VEL, e) + ";\n";
-            o += "    float r" + s + " = " + ld1(S_ROT, e) + ", w" + s + " = " + ld1(S_ANG, e) + ";\n";
+            const bool lin = d.out_lin >= 0, rotf = d.out_rot >= 0;  // (the fields a write-back overwrites)
+            o += "    V2 p" + s + " = " + ld2(S_POS, e, lin) + ", v" + s + " = " + ld2(S_VEL, e, lin) + ";\n";
+            o += "    float r" + s + " = " + ld1(S_ROT, e, rotf) + ", w" + s + " = " + ld1(S_ANG, e, rotf) + ";\n";
+            if (lin || rotf) {
+                o += "    if (bk && valid) {\n";
+                if (lin)
+                    o += "        bk2(" + P_(S_POS, e) + ", " + S_(S_POS, 0, e) + ", " + S_(S_POS, 1, e) + ", bb, a.wbd, p" + s +
+                         ");\n        bk2(" + P_(S_VEL, e) + ", " + S_(S_VEL, 0, e) + ", " + S_(S_VEL, 1, e) +
+                         ", bb, a.wbd, v" + s + ");\n";
+                if (rotf)
+                    o += "        bk1(" + P_(S_ROT, e) + ", " + S_(S_ROT, 0, e) + ", bb, a.wbd, r" + s + ");\n        bk1(" +
+                         P_(S_ANG, e) + ", " + S_(S_ANG, 0, e) + ", bb, a.wbd, w" + s + ");\n";
+                o += "    }\n";
+            }
             if (d.agent_index >= 0)
                 o += "    V2 af" + s + " = " + ld2(S_FORCE, d.agent_index) + "; float at" + s + " = " +
                      ld1(S_TORQUE, d.agent_index) + ";\n";
@@ -917,10 +939,43 @@ struct Gen {
                 if (cfg.export_forces)
                     o += "        st_out2(a.out[6], (size_t)" + s + " * a.B + b, mk(lfx" + s + ", lfy" + s +
                          "));\n        st_out1(a.out[7], (size_t)" + s + " * a.B + b, ltq" + s + ");\n";
+                if (d.out_lin >= 0 || d.out_rot >= 0) {  // the state write-back into this step's inputs
+                    o += "        if (wbk) {\n";
+                    if (d.out_lin >= 0)
+                        o += "            wb2(" + P_(S_POS, e) + ", " + S_(S_POS, 0, e) + ", " + S_(S_POS, 1, e) + ", b, p" + s +
+                             ");\n            wb2(" + P_(S_VEL, e) + ", " + S_(S_VEL, 0, e) + ", " + S_(S_VEL, 1, e) + ", b, v" +
+                             s + ");\n";
+                    if (d.out_rot >= 0)
+                        o += "            wb1(" + P_(S_ROT, e) + ", " + S_(S_ROT, 0, e) + ", b, r" + s + ");\n            wb1(" +
+                             P_(S_ANG, e) + ", " + S_(S_ANG, 0, e) + ", b, w" + s + ");\n";
+                    o += "        }\n";
+                }
             }
             o += "    }\n";
         }
         o += "}\n\n";
+    }
+
+    // The state write-back (Args.wbd != 0; graph mode's rollback-free replays, vmas_graph_chain_set_writeback):
+    // the step writes its integrated fields into its own inputs as well as into the fresh outputs, so
+    // the replay needs no post-replay carry of the state (outputs -> inputs, simulator/environment/
+    // _graph.py).  A group re-run in a later fixed-point pass must read the PRE-step state, which the
+    // write-back has overwritten: the first pass stores each group's loaded state into a backup at
+    // the same offsets (input + wbd; sc1, handed between workgroups like the outputs) and a re-run pass
+    // reads it from there (rbp); the re-run's write-back lands last.  Stores only -- no extra loads on
+    // the path that runs (one pass).
+    std::string wb_helpers() const {
+        return "__device__ __forceinline__ const float* rbp(const float* p, long long d) {\n"
+               "    return reinterpret_cast<const float*>(reinterpret_cast<const char*>(p) + d);\n}\n"
+               "__device__ __forceinline__ void bk1(const float* p, int s0, int b, long long d, float v) {\n"
+               "    st_out1(const_cast<float*>(rbp(p, d)), (size_t)((long)b * s0), v);\n}\n"
+               "__device__ __forceinline__ void bk2(const float* p, int s0, int s1, int b, long long d, V2 v) {\n"
+               "    float* q = const_cast<float*>(rbp(p, d));\n"
+               "    st_out1(q, (size_t)((long)b * s0), v.x);\n    st_out1(q, (size_t)((long)b * s0 + s1), v.y);\n}\n"
+               "__device__ __forceinline__ void wb1(const float* p, int s0, int b, float v) {\n"
+               "    const_cast<float*>(p)[(long)b * s0] = v;\n}\n"
+               "__device__ __forceinline__ void wb2(const float* p, int s0, int s1, int b, V2 v) {\n"
+               "    float* q = const_cast<float*>(p);\n    q[(long)b * s0] = v.x;\n    q[(long)b * s0 + s1] = v.y;\n}\n\n";
     }
 
     // The group loop: one copy per wave (loop_per_wave, the default), each calling its own run<w>,
@@ -928,7 +983,7 @@ struct Gen {
     // compiler hoists the loop-invariant address / stride values of EVERY wave's body above it,
     // all live at once (balance: 106 SGPRs and 163 v_writelane spills of them into VGPR lanes,
     // read back with v_readlane -- VALU instructions); with a loop per wave only that wave's are.
-    bool loop_per_wave = true;
+    bool loop_per_wave = true;  // (required by ng > 1)
     // the scenario program's argument block copied into LDS at the launch's start (epi_lds, the
     // default; VMAS_JIT_EPI_LDS=0: read through Args.epi): the epilogue's field reads are LDS reads
     // instead of a cold scalar-cache miss per group
@@ -941,9 +996,12 @@ struct Gen {
         // agent-scope fences here write back L2 per group: 38 -> 159 us per launch) -- each pass of
         // the fixed point re-running it after its group, the final pass's writes last (as the
         // state outputs).  Q: the row buffer, idle between groups.
+        const std::string q = epi_q_in_rows() ? (ng > 1 ? "Ls" : "L")
+                                               : (ng > 1 ? "EQ + sub * " + it((long)kEpiQRows * 64) : "EQ");
         return "        if (a.epi) {\n"
                "            __syncthreads();\n"
-               "            " + epi_call(io, "g", "wave", "lane", epi_q_in_rows() ? "L" : "EQ") + ";\n"
+               "            " + (ng > 1 ? epi_call(io, "g * " + it(ng) + " + sub", "WAVE", "lane", q)
+                                        : epi_call(io, "g", "wave", "lane", q)) + ";\n"
                "            __syncthreads();\n"
                "        }\n";
     }
@@ -956,9 +1014,13 @@ struct Gen {
                "            __syncthreads();\n"
                "        }\n"
                "        {\n"
-               "            const int b = g * 64 + lane;\n"
+               "            const int b = " + std::string(ng > 1 ? "(g * " + it(ng) + " + sub) * 64 + lane" : "g * 64 + lane") + ";\n"
                "            const bool valid = b < a.B;\n"
-               "            const int bb = valid ? b : (a.B - 1);\n" + run + "        }\n" + epi_text(io) +
+               "            const int bb = valid ? b : (a.B - 1);\n"
+               "            // the state write-back (Args.wbd, wb_text): this pass's inputs, its backup\n"
+               "            const bool wbx = persistent && a.wbd != 0;\n"
+               "            const long long rbd = (wbx && (" + cur + ")->pass > 0) ? a.wbd : 0ll;\n"
+               "            const bool bk = wbx && (" + cur + ")->pass == 0;\n" + run + "        }\n" + epi_text(io) +
                "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, " + cur + ",\n"
                "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
                "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
@@ -975,6 +1037,8 @@ struct Gen {
             o += "#define VMAS_TRIG_GUARD 1\n";
         o += std::string(kFlagsTag) + codegen_flags(relaxed) + "\n";
         if (prof_block >= 0) o += "#define VMAS_JIT_PROFILE_SLOTS 1\n";
+        if (const char* mp = getenv("VMAS_JIT_TEST_PASSES"))  // (test knob: vmas_jit_ops.hpp grid_decide)
+            o += "#define VMAS_GRID_MIN_PASSES " + it(std::max(1, atoi(mp))) + "\n";
         o += "#include \"vmas_jit_ops.hpp\"\n";
         if (has_epi()) o += "#include \"vmas_programs.hpp\"\n";
         o += "using namespace vmas;\n\n";
@@ -983,11 +1047,13 @@ struct Gen {
              "    uint32_t* ctl;\n    uint32_t* err;\n    uint32_t* herr;\n    unsigned long long* tm;\n" +
              std::string(global_rows ? "    float* rows;\n" : "") +
              std::string(has_epi() ? std::string("    const ") + epi_type() + "* epi;\n" : std::string()) +
+             "    long long wbd;\n" +
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n"
              "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
              "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);\n}\n\n";
+        o += wb_helpers();
         o += "constexpr WorldK WK{" + fl(cfg.contact_margin) + ", " + fl(cfg.collision_force) + ", " +
              fl(cfg.joint_force) + ", " + fl(cfg.torque_constraint_force) + "};\n";
         // world gravity and semidims: whether they apply is structure, their values are arguments
@@ -1008,10 +1074,10 @@ struct Gen {
         for (int e = 0; e < E; ++e)
             if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + "c" + desc(e) + ";\n";
         o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
-             "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid);\n\n";
+             "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid, long long rbd, bool bk, bool wbk);\n\n";
         for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
-        const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw / 4;
+        const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw * ng / 4;
         // NaN over every output field of the step (one workgroup; only after a fixed point that
         // did not converge within max_pass passes): the bad step is visible in its own results
         {
@@ -1030,31 +1096,38 @@ struct Gen {
             o += "template <int WAVE>\n__device__ __forceinline__ void group_loop(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, "
                  "uint32_t* MSK, uint32_t* QL, uint32_t* RED, float* EQ, GridCursor* CURP, uint32_t* claim, TimerStart t0s, "
                  "bool persistent, int nfl, int nwords, int ngrp, int lane, int wave" +
+                 std::string(ng > 1 ? ", int sub" : "") +
                  std::string(has_epi() ? std::string(", const ") + epi_type() + "* PROG_IOP" : std::string()) + ") {\n    (void)EQ;\n";
-            o += loop_text("            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid);\n", "CURP", "*PROG_IOP");
+            if (ng > 1)  // (this wave's group: its rows and split-pair counters)
+                o += "    float* const Ls = L + sub * " + it((long)std::max(n_rows, 1) * 64) + ";\n"
+                     "    uint32_t* const DONEs = DONE + sub * " + it(n_split) + ";\n    (void)Ls;\n";
+            o += loop_text(ng > 1 ? "            run<WAVE>(a, Ls, FL, DONEs, MSK, lane, b, bb, valid, rbd, bk, wbx);\n"
+                                  : "            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx);\n",
+                           "CURP", "*PROG_IOP");
             o += "}\n\n";
         }
         o += "__device__ __forceinline__ void world_body(const Args& a) {\n";
         if (global_rows)  // (this workgroup's slab: the same [row][lane] layout as the LDS rows)
             o += "    float* L = a.rows + (size_t)blockIdx.x * " + it((long)std::max(n_rows, 1) * 64) + ";\n";
         else
-            o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64) + "];\n";
+            o += "    __shared__ __attribute__((aligned(16))) float L[" + it(std::max(n_rows, 1) * 64 * ng) + "];\n";
         o += "    __shared__ uint32_t FL[" + it(nfl) + "];\n";
-        if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[" + it((long)kEpiQRows * 64) + "];\n";
+        if (has_epi() && !epi_q_in_rows()) o += "    __shared__ float EQ[" + it((long)kEpiQRows * 64 * ng) + "];\n";
         if (has_epi() && epi_lds) o += std::string("    __shared__ __attribute__((aligned(16))) ") + epi_type() + " PROG_IO;\n";
-        o += "    __shared__ uint32_t DONE[" + it(std::max(n_split, 1)) + "];\n";
+        o += "    __shared__ uint32_t DONE[" + it(std::max(n_split * ng, 1)) + "];\n";
         // LDS of the device-side fixed point: the row buffer when it is large enough (it is
         // idle between groups), else its own array; QL: steal list + broadcast word
         const int red_words = nfl + 2;
         o += "    __shared__ uint32_t MSK[" + it(std::max(nfl / 2, 1)) + "];\n";
         o += "    __shared__ uint32_t QL[66];\n";
-        if (!global_rows && (long)std::max(n_rows, 1) * 64 >= red_words)
+        if (!global_rows && (long)std::max(n_rows, 1) * 64 * ng >= red_words)
             o += "    uint32_t* RED = reinterpret_cast<uint32_t*>(L);\n";
         else
             o += "    __shared__ uint32_t RED[" + it(red_words) + "];\n";
         o += "    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n";
-        o += "    const int nfl = 2 * a.S * " + it(W) + ", nwords = a.S * " + it(W) + ", ngrp = (a.B + 63) >> 6;\n"
-             "    for (int i = threadIdx.x; i < " + it(n_split) + "; i += blockDim.x) DONE[i] = 0u;\n";
+        o += "    const int nfl = 2 * a.S * " + it(W) + ", nwords = a.S * " + it(W) + ", ngrp = " +
+             (ng > 1 ? "(a.B + " + it(64 * ng - 1) + ") / " + it(64 * ng) : std::string("(a.B + 63) >> 6")) + ";\n"
+             "    for (int i = threadIdx.x; i < " + it(n_split * ng) + "; i += blockDim.x) DONE[i] = 0u;\n";
         // Host-driven loop (a.ctl null): one pass per launch, each workgroup strides over the
         // 64-env groups and ORs their activity words into its own blk row (read by
         // k_jit_flags_reduce).  Persistent launch (a.ctl set): the broadphase fixed point on the
@@ -1087,17 +1160,19 @@ struct Gen {
              "";
         // the group loop (loop_text): one copy per wave (loop_per_wave), or one around a switch
         if (loop_per_wave) {
-            std::string sw = "    switch (wave) {\n";
+            // (ng > 1: one call site per wave body, the group index a run-time value)
+            std::string sw = ng > 1 ? "    switch (wave % " + it(nw) + ") {\n" : "    switch (wave) {\n";
             for (int w = 0; w < nw; ++w)
                 sw += "        case " + it(w) + ": group_loop<" + it(w) + ">(a, L, FL, DONE, MSK, QL, RED, " +
                       std::string(has_epi() && !epi_q_in_rows() ? "EQ" : "nullptr") +
                       ", &CUR, claim, t0s, persistent, nfl, nwords, ngrp, lane, wave" +
+                      std::string(ng > 1 ? ", wave / " + it(nw) : "") +
                       std::string(has_epi() ? (epi_lds ? ", &PROG_IO" : ", a.epi") : "") + "); break;\n";
             o += sw + "        default: break;\n    }\n";
         } else {
             std::string sw = "            switch (wave) {\n";
             for (int w = 0; w < nw; ++w)
-                sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid); break;\n";
+                sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx); break;\n";
             o += loop_text(sw + "                default: break;\n            }\n", "&CUR", epi_lds ? "PROG_IO" : "*a.epi");
         }
         o += block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
@@ -1108,7 +1183,7 @@ struct Gen {
              "        return;\n"
              "    }\n"
              "}\n\n";
-        const std::string bounds = "__launch_bounds__(" + it(nw * 64) + ", " + it(waves_per_eu) + ")";
+        const std::string bounds = "__launch_bounds__(" + it(nw * ng * 64) + ", " + it(waves_per_eu) + ")";
         o += "extern \"C\" __global__ void " + bounds + " k_world(Args a) {\n    world_body(a);\n}\n";
         if (has_epi())  // the eager step's launch of the same program (vmas_jit_program_outputs)
             o += "\nextern \"C\" __global__ void __launch_bounds__(" + it(nw * 64) + ") k_program_jit(" + epi_type() + " io_arg) {\n"
@@ -1124,7 +1199,7 @@ void codegen_knobs(Gen& g) {
     if (const char* pr = getenv("VMAS_JIT_PRIO")) g.prio_mode = atoi(pr);
     if (const char* pl = getenv("VMAS_JIT_PRELOAD")) g.entity_preload = atoi(pl) != 0;
     if (const char* pp = getenv("VMAS_JIT_PAIR_PRELOAD")) g.pair_preload = atoi(pp) != 0;
-    if (const char* lw = getenv("VMAS_JIT_LOOP_PER_WAVE")) g.loop_per_wave = atoi(lw) != 0;
+    if (const char* lw = getenv("VMAS_JIT_LOOP_PER_WAVE")) g.loop_per_wave = atoi(lw) != 0 || g.ng > 1;
     if (const char* el = getenv("VMAS_JIT_EPI_LDS")) g.epi_lds = atoi(el) != 0;
 }
 
@@ -1141,16 +1216,23 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
         bool global_rows;
     } tries[] = {{true, kLdsTwoPerCu, false}, {false, kLdsTwoPerCu, false}, {false, kLdsOnePerCu, false},
                  {false, kLdsOnePerCu, true}};
+    // VMAS_JIT_NG=2 (A/B): two 64-env groups per workgroup in lockstep (Gen::ng), LDS rows of both,
+    // one workgroup per CU; not for worlds whose rows live in global memory
+    const char* ngs = getenv("VMAS_JIT_NG");
+    const int ng_want = ngs && atoi(ngs) == 2 ? 2 : 1;
+    for (int ng = ng_want; ng >= 1; --ng)  // (a world too big for two groups' rows plans with one)
     for (const auto& t : tries) {
         if (t.split && !allow_split) continue;
+        if (ng > 1 && t.global_rows) continue;
         std::unique_ptr<Gen> g(new Gen(cfg, ed, pd, jd));
+        g->ng = ng;
         if (const char* pm = getenv("VMAS_JIT_PRM_MASK")) g->prm_mask = (unsigned)strtoul(pm, nullptr, 0) & 0xFFFu;
         if ((size_t)cfg.max_substeps * g->W > 1024) {
             *why = "too many substeps x pairs";
             return nullptr;
         }
         g->split_boxes = t.split;
-        g->lds_budget = t.budget;
+        g->lds_budget = ng > 1 ? kLdsOnePerCu : t.budget;  // (ng > 1: one workgroup per CU)
         g->global_rows = t.global_rows;
         // 16 waves per workgroup once there are enough pair tasks to spread (measured: flocking
         // 81 pairs 72 -> 59 us, discovery 19.2 -> 16.3 us; balance's 24 tasks 67.7 -> 69.7 us)
@@ -1160,6 +1242,7 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
         g->nw = n_tasks >= 32 ? 16 : kNW;
         if (const char* nws = getenv("VMAS_JIT_WAVES")) g->nw = atoi(nws) == 16 ? 16 : kNW;
         if (force_nw) g->nw = force_nw;
+        if (g->ng > 1) g->nw = kNW;  // (8 waves per group: 16 per workgroup)
         why->clear();
         if (g->plan(why)) return g;
     }
@@ -1330,6 +1413,7 @@ struct VmasJitWorld {
     unsigned prm_mask = kPrmMaskDefault;  // value fields passed as arguments (the others are folded in)
     size_t arg_bytes = 0;
     int W = 1, nblk = 0, nw = kNW;
+    int ng = 1;  // 64-env groups per work item (k_world runs nw * ng waves per workgroup)
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;  // k_world
     hipFunction_t fn_prog = nullptr;  // k_program_jit (cfg.epilogue: the scenario program's own kernel)
@@ -1377,6 +1461,7 @@ int32_t vmas_jit_world_destroy(VmasJitWorld* W) {
     if (!W) return VMAS_OK;
     if (W->cfg.device >= 0) {
         (void)hipSetDevice(W->cfg.device);
+        vmas::chain_free_drain();
         vmas::fn_unregister(W->fn);
         vmas::fn_unregister(W->fn_prog);
         if (W->mod) (void)hipModuleUnload(W->mod);
@@ -1447,7 +1532,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction"));
         int scratch = 0;
         (void)hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, W->fn);
-        if (scratch == 0 || g.nw == kNW) break;
+        if (scratch == 0 || g.nw == kNW || g.ng > 1) break;
     }
     Gen& g = *gp;
     W->src = g.src;
@@ -1458,7 +1543,8 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
     W->arg_bytes = g.arg_bytes();
     W->W = g.W;
     W->nw = g.nw;
-    W->nblk = (cfg->batch + 63) / 64;
+    W->ng = g.ng;
+    W->nblk = (cfg->batch + 64 * g.ng - 1) / (64 * g.ng);
     if (g.has_epi()) {
         if (hipModuleGetFunction(&W->fn_prog, W->mod, "k_program_jit") != hipSuccess)
             return cleanup(jfail(VMAS_E_HIP, "hipModuleGetFunction(k_program_jit)"));
@@ -1471,6 +1557,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         info.world_fn = W->fn;
         info.arg_bytes = W->arg_bytes;
         info.epi_offset = W->fn_prog ? (long)W->epi_offset : -1L;
+        info.wbd_offset = (long)g.wbd_offset();
         info.batch = cfg->batch;
         info.epilogue = g.has_epi() ? cfg->epilogue : VMAS_EPILOGUE_NONE;
         info.io_bytes = cfg->epilogue == VMAS_EPILOGUE_BALANCE ? sizeof(VmasBalanceIO)
@@ -1511,7 +1598,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         const std::string mode = gm ? gm : "persistent";
         int per_cu = 0, cus = 0;
         if (mode != "host" &&
-            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, W->fn, W->nw * 64, 0) == hipSuccess &&
+            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, W->fn, W->nw * W->ng * 64, 0) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
             per_cu > 0 && cus > 0) {
             W->grid = std::min(W->nblk, per_cu * cus);
@@ -1640,6 +1727,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     put_ptr(W->timing && persistent ? W->d_tm : nullptr);
     if (W->global_rows) put_ptr(W->d_rows);
     if (W->fn_prog) put_ptr(nullptr);  // Args.epi: no epilogue (the chain replay's fused launch sets it)
+    put_ptr(nullptr);                  // Args.wbd: no state write-back (the chain's write-back variant sets it)
     for (const auto& s : W->str_src) {
         const int kind = s.first / 4, k = s.first % 4, i = s.second;
         int32_t v = 0;
@@ -1706,7 +1794,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     JHIP(hipStreamIsCapturing(stream, &cap));
     const bool capturing = cap == hipStreamCaptureStatusActive;
     auto launch_plain = [&](int blocks, hipFunction_t fn, bool timed) -> int32_t {
-        const uint32_t threads = (uint32_t)W->nw * 64;
+        const uint32_t threads = (uint32_t)(W->nw * W->ng) * 64;
         if (!W->timing || capturing || !timed) {  // (a captured launch is timed by the device timer)
             JHIP(hipModuleLaunchKernel(fn, blocks, 1, 1, threads, 1, 1, 0, stream, nullptr, extra));
             return VMAS_OK;

@@ -253,6 +253,14 @@ struct GridCursor {
     u64 base;
 };
 
+// Test knob (VMAS_JIT_TEST_PASSES=<n>, compiled into the generated source): every step runs at least
+// n passes -- the decider treats the earlier passes as violated, with the mask re-derived from the
+// rows as for a real violation -- so the re-run path (and a fused scenario program re-run after each
+// pass, vmas_jit.hip epi_text) is exercised; the results must equal the one-pass step's.
+#ifndef VMAS_GRID_MIN_PASSES
+#define VMAS_GRID_MIN_PASSES 1
+#endif
+
 // The decider of global pass G = E + pass (all threads): every group's row is in blk and the
 // pass's mask is MSK (LDS, 1 = active).  RED: 2 * nwords + 2 words of LDS.  Returns true when the
 // final pass did NOT converge (the caller then poisons the step's outputs with NaN, so that the
@@ -261,7 +269,8 @@ __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, const u
                                    uint32_t* herr, int nwords, int ngrp, u64 G, int pass, int max_pass, uint32_t* RED,
                                    unsigned long long* tm, TimerStart t0s, GridCursor* CUR) {
     const int nw2 = 2 * nwords;
-    if (threadIdx.x == 0) RED[nw2] = ld64(&ctl[kGridCand]) == G + 1ull ? 1u : 0u;
+    const bool force = pass + 1 < VMAS_GRID_MIN_PASSES;  // (test knob: another pass regardless)
+    if (threadIdx.x == 0) RED[nw2] = (force || ld64(&ctl[kGridCand]) == G + 1ull) ? 1u : 0u;
     for (int w = threadIdx.x; w < nw2; w += blockDim.x) RED[w] = 0u;
     if (threadIdx.x == 0) RED[nw2 + 1] = 0u;
     __syncthreads();
@@ -296,7 +305,7 @@ __device__ inline bool grid_decide(const uint32_t* blk, uint32_t* nmask, const u
         }
     }
     __syncthreads();
-    const bool viol = RED[nw2 + 1] != 0u;
+    const bool viol = RED[nw2 + 1] != 0u || force;
     const bool more = viol && pass + 1 < max_pass;
     if (more)
         for (int w = threadIdx.x; w < nwords; w += blockDim.x) st_agent(&nmask[w], ~RED[w]);

@@ -17,11 +17,18 @@ struct JitFnInfo {
     hipFunction_t world_fn;  // its k_world
     size_t arg_bytes;     // k_world's argument block
     long epi_offset;      // byte offset of Args.epi in it (-1: no epilogue)
+    long wbd_offset;      // byte offset of Args.wbd (the state write-back's backup delta, vmas_jit.hip wb_helpers)
     int batch;
     int epilogue;         // VMAS_EPILOGUE_*
     size_t io_bytes;      // the program's argument block (VmasBalanceIO / VmasTransportIO)
 };
 
 bool jit_fn_info(const void* f, JitFnInfo* out);
+
+// Release the device copies of freed kernel chains (vmas_graph_chain_free defers them: a chain may
+// be dropped while a stream is capturing, where hipFree is not allowed).  Called at the next chain
+// build and when a world is destroyed (never during a capture: engines dropped while a stream
+// captures are destroyed later, simulator/_engine.py drain_deferred).
+void chain_free_drain();
 
 }  // namespace vmas

@@ -957,6 +957,12 @@ struct VmasKernelChain {
     ChainNode node[kChainMaxNodes];
     std::vector<std::unique_ptr<FusedArgs>> args;
     std::vector<void*> dev;  // device copies of the epilogue argument blocks
+    // the chain's k_world launch (-1: none), its argument block (the node's, or its FusedArgs') and
+    // registry entry; wb: the same block with Args.wbd set (vmas_graph_chain_set_writeback)
+    int world = -1;
+    const char* world_args = nullptr;
+    vmas::JitFnInfo world_info{};
+    std::unique_ptr<FusedArgs> wb;
 };
 
 namespace {
@@ -964,6 +970,19 @@ namespace {
 // another stream is being captured, where hipFree is not allowed).
 std::mutex g_chain_free_mu;
 std::vector<void*> g_chain_free;
+}  // namespace
+
+extern "C++" {
+namespace vmas {
+void chain_free_drain() {
+    std::lock_guard<std::mutex> lk(g_chain_free_mu);
+    for (void* d : g_chain_free) (void)hipFree(d);
+    g_chain_free.clear();
+}
+}  // namespace vmas
+}
+
+namespace {
 
 // The argument block of a captured kernel node whose kernel takes one struct by value: from the
 // node's `extra` buffer (module launches with HIP_LAUNCH_PARAM_BUFFER_POINTER) or its first
@@ -1036,11 +1055,7 @@ bool program_io_fusable(int kind, const char* io, int batch) {
 int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain** out) {
     if (!graph_ || !out) return fail(VMAS_E_INVALID, "vmas_graph_chain_build: null argument");
     *out = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_chain_free_mu);
-        for (void* d : g_chain_free) (void)hipFree(d);
-        g_chain_free.clear();
-    }
+    vmas::chain_free_drain();
     const hipGraph_t graph = (hipGraph_t)graph_;
     max_nodes = std::min<int32_t>(max_nodes, kChainMaxNodes);
     size_t n = 0;
@@ -1145,11 +1160,24 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
                 nd.fn = a.world_fn;
                 nd.kernel_params = nullptr;
                 nd.extra = fa->extra;
+                if (c->world < 0) {
+                    c->world = c->n;
+                    c->world_args = fa->buf.data();
+                    c->world_info = a;
+                }
                 c->args.push_back(std::move(fa));
                 c->node[c->n++] = nd;
                 ++c->fused;
                 ++k;  // (the balance node runs inside this launch)
                 continue;
+            }
+        }
+        if (c->world < 0 && vmas::jit_fn_info(p.func, &a) && a.kind == vmas::kJitFnWorld) {
+            const char* wa = node_arg_block(p, a.arg_bytes);
+            if (wa) {
+                c->world = c->n;
+                c->world_args = wa;
+                c->world_info = a;
             }
         }
         c->node[c->n++] = nd;
@@ -1158,12 +1186,41 @@ int32_t vmas_graph_chain_build(void* graph_, int32_t max_nodes, VmasKernelChain*
     return VMAS_OK;
 }
 
-int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) {
+// The state write-back variant of a chain (graph mode's rollback-free replays): the chain's k_world
+// launch with Args.wbd = backup_delta, so the step also writes its integrated state into its own
+// inputs (and backs them up at input + backup_delta for a re-run pass; vmas_jit.hip wb_helpers) --
+// the replay then needs no post-replay carry of that state.  backup_delta 0 removes the variant.
+int32_t vmas_graph_chain_set_writeback(VmasKernelChain* c, int64_t backup_delta) {
+    if (!c) return fail(VMAS_E_INVALID, "vmas_graph_chain_set_writeback: null chain");
+    if (backup_delta == 0) {
+        c->wb.reset();
+        return VMAS_OK;
+    }
+    if (c->world < 0 || !c->world_args || c->world_info.wbd_offset <= 0 ||
+        (size_t)c->world_info.wbd_offset + 8 > c->world_info.arg_bytes)
+        return fail(VMAS_E_UNSUPPORTED, "vmas_graph_chain_set_writeback: the chain has no k_world launch");
+    std::unique_ptr<FusedArgs> fa(new FusedArgs());
+    fa->buf.assign(c->world_args, c->world_args + c->world_info.arg_bytes);
+    memcpy(fa->buf.data() + c->world_info.wbd_offset, &backup_delta, sizeof backup_delta);
+    fa->size = c->world_info.arg_bytes;
+    fa->extra[0] = HIP_LAUNCH_PARAM_BUFFER_POINTER;
+    fa->extra[1] = fa->buf.data();
+    fa->extra[2] = HIP_LAUNCH_PARAM_BUFFER_SIZE;
+    fa->extra[3] = &fa->size;
+    fa->extra[4] = HIP_LAUNCH_PARAM_END;
+    c->wb = std::move(fa);
+    return VMAS_OK;
+}
+
+static int32_t chain_launch(const VmasKernelChain* c, void* stream, bool wb) {
     if (!c || c->n <= 0) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch: empty chain");
+    if (wb && !c->wb) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch_wb: no write-back variant");
     for (int k = 0; k < c->n; ++k) {
         const ChainNode& d = c->node[k];
+        const bool w = wb && k == c->world;
         const hipError_t e = hipModuleLaunchKernel(d.fn, d.grid.x, d.grid.y, d.grid.z, d.block.x, d.block.y, d.block.z,
-                                                   d.shmem, (hipStream_t)stream, d.kernel_params, d.extra);
+                                                   d.shmem, (hipStream_t)stream, w ? nullptr : d.kernel_params,
+                                                   w ? c->wb->extra : d.extra);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             return fail(VMAS_E_HIP, "vmas_graph_chain_launch: node %d: %s", k, hipGetErrorString(e));
@@ -1171,6 +1228,11 @@ int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) {
     }
     return VMAS_OK;
 }
+
+int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) { return chain_launch(c, stream, false); }
+
+// The chain with its write-back variant of the k_world launch (vmas_graph_chain_set_writeback).
+int32_t vmas_graph_chain_launch_wb(const VmasKernelChain* c, void* stream) { return chain_launch(c, stream, true); }
 
 int32_t vmas_graph_chain_nodes(const VmasKernelChain* c) { return c ? c->n : 0; }
 
@@ -1404,6 +1466,7 @@ int32_t vmas_world_destroy(VmasWorld* W) {
     if (!W) return VMAS_OK;
     if (W->cfg.device >= 0) {
         use_device(W->cfg.device);
+        vmas::chain_free_drain();
         if (W->d_tables) (void)hipFree(W->d_tables);
         if (W->d_mask) (void)hipFree(W->d_mask);
         if (W->d_blk) (void)hipFree(W->d_blk);

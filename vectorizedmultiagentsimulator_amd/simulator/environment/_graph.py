@@ -111,6 +111,20 @@ def _own_scenario(scenario) -> bool:
 _STEP_METHODS = ("reward", "observation", "done", "info", "pre_step", "post_step", "process_action",
                  "env_process_action", "extra_render")
 
+# The scenarios whose step code the replay trusts beyond the watched eager step (write-only
+# attributes, direct outputs): the four benchmark scenarios, each held to its eager step by
+# tests/test_graph.py (not every file of the scenarios directory -- the debug scenarios
+# are replayed like a user's scenario).
+_TRUSTED_FILES = ("balance.py", "transport.py", "discovery.py", "flocking.py")
+
+
+def _trusted_scenario(scenario) -> bool:
+    if not _own_scenario(scenario):
+        return False
+    f = os.path.abspath(type(scenario).make_world.__code__.co_filename)
+    scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "scenarios")
+    return os.path.dirname(f) == scn_dir and os.path.basename(f) in _TRUSTED_FILES
+
 
 def _write_only(o, k: str, scn_cls=None) -> bool:
     """Attribute k of o is declared write-only within a step by o's own class (not inherited: a
@@ -141,13 +155,42 @@ def _host_rng_changed(a, b) -> Optional[str]:
 _PLAIN = (bool, int, float, str)
 
 
-def _plain_attrs(objs) -> Dict[Tuple[int, str], Any]:
-    """Plain Python number / string attributes of the tracked objects (Python-side step state)."""
+def _fingerprint(v, depth: int = 0):
+    """What a step could change in place inside a Python container: its length and its plain
+    values, tensors by identity (a tensor appended or re-bound inside a list), numpy arrays by
+    content; None for anything else (not compared)."""
+    t = type(v)
+    if t in _PLAIN or v is None:
+        return v
+    if isinstance(v, Tensor):
+        return ("tensor", id(v))
+    if isinstance(v, np.ndarray):
+        return ("ndarray", v.shape, str(v.dtype), v.tobytes() if v.size <= 4096 else hash(v.tobytes()))
+    if depth >= 3:
+        return None
+    if t in (list, tuple) or isinstance(v, (list, tuple)):
+        return (t.__name__, len(v), tuple(_fingerprint(x, depth + 1) for x in v[:256]))
+    if isinstance(v, dict):
+        items = list(v.items())[:256]
+        return ("dict", len(v), tuple((repr(k), _fingerprint(x, depth + 1)) for k, x in items))
+    if isinstance(v, (set, frozenset)):
+        return (t.__name__, len(v))
+    return None
+
+
+def _plain_attrs(objs, strict: bool = False) -> Dict[Tuple[int, str], Any]:
+    """Plain Python number / string attributes of the tracked objects (Python-side step state);
+    strict (a scenario outside the trusted set): also the contents of Python containers and numpy
+    arrays held by them (a history list appended to in place, a numpy counter ...)."""
     out = {}
     for o in objs:
         for k, v in o.__dict__.items():
             if type(v) in _PLAIN:
                 out[(id(o), k)] = v
+            elif strict and not isinstance(v, Tensor):
+                fp = _fingerprint(v)
+                if fp is not None:
+                    out[(id(o), k)] = fp
     return out
 
 
@@ -375,6 +418,11 @@ class _KernelChain:
             return None, lib.vmas_last_error().decode(errors="replace")
         return cls(graph, out, lib.vmas_graph_chain_nodes(out), lib.vmas_graph_chain_fused(out)), ""
 
+    def set_writeback(self, backup_delta: int) -> bool:
+        """The write-back variant of the chain's k_world launch (vmas_graph_chain_set_writeback):
+        False when the chain has no k_world launch."""
+        return N.load_library().vmas_graph_chain_set_writeback(self.handle, int(backup_delta)) == 0
+
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
         if h is not None and h.value:
@@ -430,6 +478,7 @@ class _Segments:
 
 
 _STATE_KEYS = ("_pos", "_vel", "_rot", "_ang_vel", "_force", "_torque")
+_WB_KEYS = ("_pos", "_vel", "_rot", "_ang_vel")  # (the fields k_world's state write-back covers)
 
 
 class DirectOutputs:
@@ -481,7 +530,7 @@ class DirectOutputs:
 
     def finalize(self, out_tensors, scenario) -> None:
         """Which categories the replays relocate (see the class notes)."""
-        own = _own_scenario(scenario)
+        own = _trusted_scenario(scenario)
         ids = {id(t) for t in out_tensors}
         self.enabled = [r for r in self.regions
                         if own and r["buf"]._version == 0 and all(id(m) in ids for m in r["members"])]
@@ -644,6 +693,10 @@ class StepGraph:
         self._steps_folded = False
         self._steps_t = None
         self._fresh: Optional[_FreshState] = None  # fresh entity states on first use after a replay
+        # the state write-back (_writeback_ready): the carry index of the engine's state buffer, and
+        # None (not tried) / False (not possible) / {chain, backup}
+        self._state_idx: Optional[int] = None
+        self._wb = None
 
     # ---- the step -------------------------------------------------------------------------------
     def body(self):
@@ -772,7 +825,8 @@ class StepGraph:
 
             self.env.world._hole_sink = hole
             objs = _tracked_objects(self.env)
-            plain0 = _plain_attrs(objs)
+            strict = not _trusted_scenario(self.env.scenario)
+            plain0 = _plain_attrs(objs, strict)
             try:
                 with consts:
                     out = self.body()
@@ -783,7 +837,7 @@ class StepGraph:
             if rng_used[0] is None:
                 rng_used[0] = _host_rng_changed(rng_cur[0], _host_rng_states())
             self._device_rng_outside_holes = (dgen.get_offset() - d_off0 - hole_adv[0]) != 0
-            plain1 = _plain_attrs(objs)
+            plain1 = _plain_attrs(objs, strict)
             changed = sorted(k for k in set(plain0) | set(plain1) if plain0.get(k) != plain1.get(k))
         self._trial_consts = consts  # the arena outlives the copies that read it
         # torch's warning: "called a synchronizing CUDA operation" (not the notice that the mode
@@ -867,6 +921,7 @@ class StepGraph:
         self._out_tree = None
         self._out_tensors = []
         self._carry_dst, self._carry_src, self._watch = [], [], []
+        self._state_idx, self._wb = None, None
         self._watch_cols = None
         self._carry_ys, self._post = [], None
         self._steps_folded = False
@@ -1019,10 +1074,11 @@ class StepGraph:
     def _plan(self, objs, snap, out):
         carry: List[Tuple[Tensor, Tensor]] = []
         names: List[str] = []
+        state_field: List[bool] = []  # (an entity state's pos / vel / rot / ang_vel: what k_world integrates)
         fresh = []  # carried entity-state attributes: re-bound to fresh tensors on first use (_FreshState)
         # re-bound attributes no step reads before re-binding them (the package's own scenarios and
         # sensors declare them): not carried; a rollback restores them from the backups (_inplace)
-        own = self._WRITE_ONLY and _own_scenario(self.env.scenario)
+        own = self._WRITE_ONLY and _trusted_scenario(self.env.scenario)
         self._write_only_ys = []
         for o, before in snap:
             after = o.__dict__
@@ -1043,6 +1099,7 @@ class StepGraph:
                     continue
                 carry.append((v0, v1))
                 names.append(f"{type(o).__name__}.{k}")
+                state_field.append(k in _WB_KEYS and hasattr(type(o), "_fresh"))
                 if k in _STATE_KEYS and hasattr(type(o), "_fresh"):  # (an EntityState / AgentState)
                     fresh.append((after, k, v1))
         self._carry_ys = [y for _, y in carry]
@@ -1055,10 +1112,14 @@ class StepGraph:
         # group carried pairs by (X storage, Y storage): same offsets / strides / storage size ->
         # one whole-storage copy (the engine's output buffer: every dynamic field at once)
         groups: Dict[Tuple[int, int], List[Tuple[Tensor, Tensor]]] = {}
-        for x, y in carry:
-            groups.setdefault((_storage_key(x), _storage_key(y)), []).append((x, y))
+        state_only: Dict[Tuple[int, int], bool] = {}
+        for (x, y), sf in zip(carry, state_field):
+            key = (_storage_key(x), _storage_key(y))
+            groups.setdefault(key, []).append((x, y))
+            state_only[key] = state_only.get(key, True) and sf
         dst, src = [], []
-        for (_, _), pairs in groups.items():
+        state_pair = None  # (the whole-storage copy of the engine's state buffer: k_world can write it back)
+        for key, pairs in groups.items():
             x0, y0 = pairs[0]
             sx, sy = x0.untyped_storage(), y0.untyped_storage()
             whole = (len(pairs) > 1 and sx.nbytes() == sy.nbytes()
@@ -1067,6 +1128,8 @@ class StepGraph:
             if whole:
                 dst.append(torch.empty(0, dtype=torch.uint8, device=x0.device).set_(sx))
                 src.append(torch.empty(0, dtype=torch.uint8, device=y0.device).set_(sy))
+                if state_only[key] and state_pair is None:
+                    state_pair = (dst[-1], src[-1])
             else:
                 for x, y in pairs:
                     dst.append(x)
@@ -1074,8 +1137,11 @@ class StepGraph:
         # one multi-tensor copy kernel: contiguous pairs as flat byte views (one dtype), the rest
         # (non-contiguous views) copied one by one
         self._carry_dst, self._carry_src, self._carry_other = [], [], []
+        self._state_idx, self._wb = None, None
         for x, y in zip(dst, src):
             if x.is_contiguous() and y.is_contiguous() and x.dtype == y.dtype:
+                if state_pair is not None and x is state_pair[0]:
+                    self._state_idx = len(self._carry_dst)
                 self._carry_dst.append(_bytes(x))
                 self._carry_src.append(_bytes(y))
             else:
@@ -1102,7 +1168,7 @@ class StepGraph:
         return self.env.world.engine.graph_token() == self._sig
 
     # ---- replay ---------------------------------------------------------------------------------
-    def _launch(self, defer_chain: bool = False):
+    def _launch(self, defer_chain: bool = False, wb: bool = False):
         """One replay.  The first goes through torch (its prologue refreshes the generator state
         that captured random ops read); if it did not advance the device generator, the graph
         draws no random numbers and later replays launch the instantiated graph directly
@@ -1121,8 +1187,7 @@ class StepGraph:
         if self._chain is not None:  # the graph's kernels as plain launches (_KernelChain)
             if defer_chain:  # (launched by the post-replay call: _post_replay(chain=...))
                 return self._chain
-            N.check(N.load_library().vmas_graph_chain_launch(self._chain.handle, N.stream_ptr(self._dev_index())),
-                    "vmas_graph_chain_launch")
+            self._launch_chain(self._chain, wb)
             return
         if self._raw_exec is not None:
             N.check(N.load_library().vmas_graph_launch(self._raw_exec, N.stream_ptr(self._dev_index())),
@@ -1199,11 +1264,41 @@ class StepGraph:
         that has no device asserts (rollback_free): the speculative replay without its backups and
         generator snapshot, which only a rollback reads."""
         self._first_replay = False
-        chain = self._launch(defer_chain=self._CHAIN_IN_POST)
+        wb = self._writeback_ready()
+        chain = self._launch(defer_chain=self._CHAIN_IN_POST, wb=wb)
         self.replays += 1
-        out = self._post_replay(chain=chain)
+        out = self._post_replay(chain=chain, wb=wb)
         self._finish_deferred(out=out)
         return out
+
+    # The state write-back (a rollback-free replay only): the chain's k_world writes the integrated
+    # state into its own inputs X as well as into the outputs Y (vmas_graph_chain_set_writeback; a
+    # re-run fixed-point pass reads the pre-step state from a backup the first pass stores), so the
+    # post-replay launch drops the whole-storage carry Y -> X of the engine's state buffer -- at C2 4.46
+    # of its 5.8 MB (VERDICT r5 "Next" #2).  Only when that carry group holds nothing but entity
+    # states' pos / vel / rot / ang_vel (exactly what k_world integrates and writes back) and the replay
+    # is a kernel chain.  A speculative replay (a rollback restores Y from X) keeps the carry.  Only for
+    # the trusted (benchmark) scenarios: X is overwritten INSIDE the step, so no kernel after k_world
+    # may read the pre-step state -- their programs read the integrated state only; a user's reward
+    # may keep last step's position (self.prev = agent.state.pos) and read it after World.step.
+    _WRITEBACK = os.environ.get("VMAS_GRAPH_WRITEBACK", "1") != "0"  # (A/B knob)
+
+    def _writeback_ready(self) -> bool:
+        w = self._wb
+        if w is not None and w is not False and w["chain"] is self._chain:
+            return True
+        if w is False or self._chain is None:
+            return False
+        self._wb = False
+        if (not self._WRITEBACK or self._state_idx is None or self._carry_other
+                or not _trusted_scenario(self.env.scenario)):
+            return False
+        x = self._carry_dst[self._state_idx]
+        backup = torch.empty_like(x)  # (the first pass's copy of the pre-step state, same offsets)
+        if not self._chain.set_writeback(backup.data_ptr() - x.data_ptr()):
+            return False
+        self._wb = {"chain": self._chain, "backup": backup}
+        return True
 
     def replay_speculative(self, flags_ok):
         """Replays the step while the action kernel's flags are still in flight, then waits for
@@ -1251,17 +1346,18 @@ class StepGraph:
         torch.cuda.set_rng_state(rng, self.env.device)
 
     # ---- copies after a replay -----------------------------------------------------------------
-    def _launch_chain(self, chain) -> None:
-        N.check(N.load_library().vmas_graph_chain_launch(chain.handle, N.stream_ptr(self._dev_index())),
-                "vmas_graph_chain_launch")
+    def _launch_chain(self, chain, wb: bool = False) -> None:
+        lib = N.load_library()
+        fn = lib.vmas_graph_chain_launch_wb if wb else lib.vmas_graph_chain_launch
+        N.check(fn(chain.handle, N.stream_ptr(self._dev_index())), "vmas_graph_chain_launch")
 
     _chain_fn_addr = None
 
     @classmethod
-    def _chain_fn(cls) -> int:
+    def _chain_fn(cls, wb: bool = False) -> int:
         if cls._chain_fn_addr is None:
-            cls._chain_fn_addr = N.fn_addr("vmas_graph_chain_launch")
-        return cls._chain_fn_addr
+            cls._chain_fn_addr = (N.fn_addr("vmas_graph_chain_launch"), N.fn_addr("vmas_graph_chain_launch_wb"))
+        return cls._chain_fn_addr[1 if wb else 0]
 
     def _dev_index(self) -> int:
         dev = torch.device(self.env.device)
@@ -1282,13 +1378,14 @@ class StepGraph:
         return (p is not None and p["bk_n"] >= n and self._carry_current()
                 and p["bk_ver"] == tuple(map(_VERSION, self._inplace)))
 
-    def _post_spans(self):
+    def _post_spans(self, wb: bool = False):
         """Per capture: the carry spans (Y -> X, contiguous byte views) and the backup spans of
         the next step (in-place tensors and the action buffer -> their backups; a backup whose
         tensor lies inside a carry destination X is taken from the matching bytes of Y, which
         is what X holds once the carry has run).  None if a backup straddles a carry destination
         or is not contiguous (then the backups stay in backup())."""
-        carry = [(y.data_ptr(), x.data_ptr(), x.numel()) for x, y in zip(self._carry_dst, self._carry_src)]
+        carry = [(y.data_ptr(), x.data_ptr(), x.numel()) for i, (x, y) in enumerate(zip(self._carry_dst, self._carry_src))
+                 if not (wb and i == self._state_idx)]  # (wb: k_world wrote the state back itself)
         bk = []
         n = len(self._bk_src) if self._bk_dst else 0
         for t, d in zip(self._bk_src[:n], self._bk_dst[:n]):
@@ -1312,16 +1409,16 @@ class StepGraph:
         views, rest = self._clone_alloc(t)
         return t, views, rest
 
-    def _post_replay(self, prep=None, chain=None):
+    def _post_replay(self, prep=None, chain=None, wb: bool = False):
         """After a replay, in ONE native launch (vmas_copy_spans): the fresh copies of the
         outputs, the carry of the re-bound state to the next step (Y -> X, which before_actions
         then skips while no Y changes) and the next step's backups (which backup() then skips
         while no in-place tensor changes).  The outputs are copied before the carry when one
         of them lies in a carry destination (two launches).  The span table is built once per
         (capture, backup buffers): a step only writes its fresh outputs' addresses into it."""
-        t = self._post_table() if prep is None else None
+        t = self._post_table(wb) if prep is None else None
         if chain is not None and (t is None or t["plain"] or t.get("host") is None):
-            self._launch_chain(chain)  # (a replay's kernel chain not yet launched: now, before anything else)
+            self._launch_chain(chain, wb)  # (a replay's kernel chain not yet launched: now, before anything else)
             chain = None
         if t is not None and not t["plain"]:
             # the common case in one C++ call (csrc/vmas_host.cpp OutputAlloc.post): the replay's
@@ -1330,7 +1427,7 @@ class StepGraph:
             if t["steps_row"] is not None:
                 self._steps_current(t)
             host = t.get("host") or self._host_alloc(t)
-            ch = (chain.addr, self._chain_fn()) if chain is not None else (0, 0)
+            ch = (chain.addr, self._chain_fn(wb)) if chain is not None else (0, 0)
             mid, hi = (t["n_out"] if t["clash"] else 0), t["n_all"]
             # (with a deferred launch -- discovery's respawn, whose host side advances the generator
             # after this -- the draw reads its offset where the respawn launch leaves it)
@@ -1371,14 +1468,15 @@ class StepGraph:
         fn, consts = self._clone_build
         return fn(views, consts)
 
-    def _post_table(self):
+    def _post_table(self, wb: bool = False):
         """The post-replay span table (N.COPY_SPAN_DTYPE rows): the contiguous outputs (their
         destinations are filled per step by _clone_alloc), then the carry and backup spans."""
         ts = self._out_tensors
         if getattr(self, "_clone_src_of", None) is not ts:
             self._clone_plan()
             self._clone_src_of = ts
-        c = getattr(self, "_post_cache", None)  # (objects compared by identity, not id())
+        cname = "_post_cache_wb" if wb else "_post_cache"  # (a table per variant: with / without the state carry)
+        c = getattr(self, cname, None)  # (objects compared by identity, not id())
         if (c is not None and c[0] is ts and c[1] is self._bk_dst and c[2] == len(self._bk_dst)
                 and c[3] == len(self._bk_src)):
             return c[4]
@@ -1394,7 +1492,7 @@ class StepGraph:
             st = self.env.steps
             steps_row = len(out_rows)
             out_rows.append((0, st.data_ptr(), st.numel() * 4))
-        carry, bk, n_bk = self._post_spans()
+        carry, bk, n_bk = self._post_spans(wb)
         plain = bool(self._carry_other) or bk is None
         extra = [] if plain else carry + bk
         tbl = np.zeros(len(out_rows) + len(extra), dtype=N.COPY_SPAN_DTYPE)
@@ -1406,7 +1504,7 @@ class StepGraph:
              "clash": clash, "n_bk": n_bk, "steps_row": steps_row, "steps": self.env.steps if self._steps_folded else None,
              "direct_rows": direct_rows,
              "contig": [[x.is_contiguous() for x in srcs] for _, _, srcs in self._clone_group_srcs]}
-        self._post_cache = (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t)
+        setattr(self, cname, (ts, self._bk_dst, len(self._bk_dst), len(self._bk_src), t))
         return t
 
     def _steps_current(self, t) -> None:
