@@ -556,6 +556,11 @@ int32_t vmas_balance_outputs(int32_t device, const VmasBalanceIO* io, void* stre
  * IEEE division a / b (csrc/vmas_balance.hpp xdiv), out[n, 2n) = this build's `/`, out[2n, 3n) =
  * xsqrt(a), out[3n, 4n) = sqrtf(a) -- equal bit for bit (tests/test_fused.py). */
 int32_t vmas_test_exact_math(int32_t device, const float* a, const float* b, float* out, int64_t n, void* stream);
+/* Test entry point (no reference counterpart): the fast LIDAR programs' ray-direction instructions
+ * (hardware sin / cos, as k_flocking_fast and k_discovery_obs_fast use them below |x| 16) over x:
+ * out[i] = sin, out[n + i] = cos -- the parity tests' scan certification derives its angle bound
+ * from them (tests/_scenario_parity.py SCAN_DELTA). */
+int32_t vmas_test_fast_trig(int32_t device, const float* x, float* out, int64_t n, void* stream);
 
 /* flocking (reference vmas/scenarios/flocking.py:149-206): replaces, for every policy agent at
  * once, Scenario.reward (the first policy agent's `t += 1` and pairwise collision rewards over

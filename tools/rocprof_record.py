@@ -35,6 +35,10 @@ if trace.exists():
     split = {"avg_us": round(sum(dur[-timer_n:]) / timer_n, 3), "timer_launches": timer_n,
              "in_step_us": round(sum(dur[w:w + n]) / max(1, len(dur[w:w + n])), 3), "in_step_launches": len(dur[w:w + n]),
              "avg_all_us": avg_all, "trace": str(trace)}
+    if (rf.get("plain") or {}).get("kernel_us"):  # (bench.py time_fused_chain: 5 warm + 50 right after the steps)
+        fz = dur[w + n + 5:w + n + 55]
+        split["fused_timer_us"] = round(sum(fz) / max(1, len(fz)), 3)
+        split["fused_timer_launches"] = len(fz)
 rec = {
     "kernel": kernel,
     "workload": bench["config"]["workload"],

@@ -68,6 +68,7 @@ EXPORTED_SYMBOLS = (
     "vmas_test_hold",
     "vmas_balance_outputs",
     "vmas_test_exact_math",
+    "vmas_test_fast_trig",
     "vmas_copy_spans",
     "vmas_spawn_targets",
     "vmas_spawn_scratch_words",
@@ -547,6 +548,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_balance_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_test_exact_math.restype = _i32
     lib.vmas_test_exact_math.argtypes = [_i32, _vp, _vp, _vp, ctypes.c_int64, _vp]
+    lib.vmas_test_fast_trig.restype = _i32
+    lib.vmas_test_fast_trig.argtypes = [_i32, _vp, _vp, ctypes.c_int64, _vp]
     lib.vmas_discovery_outputs.restype = _i32
     lib.vmas_discovery_outputs.argtypes = [_i32, _vp, _vp]
     lib.vmas_transport_outputs.restype = _i32

@@ -213,6 +213,12 @@ struct Gen {
     int n_split = 0;
     // LDS rows (64 floats each)
     std::vector<int> r_p, r_rot, r_trig, r_res;
+    // balance's epilogue reads the group's state from the rows (epi_src): velocity rows of the
+    // dynamic entities, published after the last substep; Q (its scratch) then sits on the pair
+    // result rows, dead by then
+    std::vector<int> r_v, r_w;
+    int res_first = 0, res_end = 0;
+    bool epi_src = false;  // (VMAS_JIT_EPI_SRC=1, A/B: measured slower so far, profiles/r06/)
     int n_rows = 0;
     // argument block
     std::vector<std::pair<int, int>> ptr_src, str_src;  // (Src, index); strides: (Src*4 + k, index)
@@ -369,7 +375,17 @@ struct Gen {
             if (need_rot[e]) r_rot[e] = rows(1);
             if (need_trig[e]) r_trig[e] = rows(4);
         }
+        res_first = n_rows;
         for (int p = 0; p < P; ++p) r_res[p] = rows(split[p] ? 4 * parts(pd[p].cls) + 8 : res_rows(p));
+        res_end = n_rows;
+        r_v.assign(E, -1);
+        r_w.assign(E, -1);
+        if (use_src())
+            for (int e = 0; e < E; ++e)
+                if (dyn[e]) {
+                    r_v[e] = rows(2);
+                    r_w[e] = rows(1);
+                }
         // rows + FL + DONE + the pass's mask words + the fixed point's reduction words (in the
         // row buffer when it is large enough)
         const long red = (!global_rows && (long)std::max(n_rows, 1) * 64 * ng >= nfl + 2) ? 0 : nfl + 2;
@@ -421,12 +437,18 @@ struct Gen {
     const char* epi_type() const { return cfg.epilogue == VMAS_EPILOGUE_BALANCE ? "VmasBalanceIO" : "VmasTransportIO"; }
     // the call running the program for group g (vmas_programs.hpp balance_group / transport_group)
     std::string epi_call(const std::string& io, const std::string& g, const std::string& wave, const std::string& lane,
-                         const std::string& q) const {
+                         const std::string& q, const std::string& src = "") const {
         if (cfg.epilogue == VMAS_EPILOGUE_BALANCE)
-            return "balance_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ", " + q + ")";
+            return "balance_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ", " + q + src + ")";
         return "transport_group(" + io + ", " + g + ", " + wave + ", " + it(nw) + ", " + lane + ")";
     }
-    bool epi_q_in_rows() const { return !global_rows && n_rows >= kEpiQRows; }
+    bool epi_q_in_rows() const {
+        return !global_rows && (use_src() ? res_end - res_first >= kEpiQRows : n_rows >= kEpiQRows);
+    }
+    // the epilogue's state from the rows (balance only; not with rows in global memory)
+    bool use_src() const { return epi_src && cfg.epilogue == VMAS_EPILOGUE_BALANCE && !global_rows; }
+    // Q's first row in the row buffer (epi_q_in_rows)
+    long epi_q_row() const { return use_src() ? res_first : 0; }
     // byte offset of Args.epi (after the fixed pointers: the value slots follow it)
     size_t epi_offset() const { return 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0)); }
     // byte offset of Args.wbd (after epi): the state write-back's backup delta (0: off; see wb_text)
@@ -772,10 +794,12 @@ struct Gen {
     }
 
     void wave_body(std::string& o, int w) {
-        o += "template <> __device__ __forceinline__ void run<" + it(w) +
+        o += "template <> __device__ __forceinline__ bool run<" + it(w) +
              ">(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, "
-             "bool valid, long long rbd, bool bk, bool wbk) {\n";
+             "bool valid, long long rbd, bool bk, bool wbk, bool spec, bool spec_ok, uint32_t* QL" +
+             std::string(use_src() ? ", const VmasBalanceIO* prog" : "") + ") {\n";
         // prologue: static pair entities (loaded once), dynamic entities into registers
+        std::string bk_code;  // the state write-back's backup stores (wb_helpers)
         for (int e : wave_static[w]) {
             o += "    {  // static entity " + it(e) + "\n";
             o += "        const V2 p" + it(e) + " = " + ld2(S_POS, e) + ";\n";
@@ -792,16 +816,14 @@ struct Gen {
             const bool lin = d.out_lin >= 0, rotf = d.out_rot >= 0;  // (the fields a write-back overwrites)
             o += "    V2 p" + s + " = " + ld2(S_POS, e, lin) + ", v" + s + " = " + ld2(S_VEL, e, lin) + ";\n";
             o += "    float r" + s + " = " + ld1(S_ROT, e, rotf) + ", w" + s + " = " + ld1(S_ANG, e, rotf) + ";\n";
-            if (lin || rotf) {
-                o += "    if (bk && valid) {\n";
+            if (lin || rotf) {  // (stored after the first barrier, once the group is known to be ours)
                 if (lin)
-                    o += "        bk2(" + P_(S_POS, e) + ", " + S_(S_POS, 0, e) + ", " + S_(S_POS, 1, e) + ", bb, a.wbd, p" + s +
-                         ");\n        bk2(" + P_(S_VEL, e) + ", " + S_(S_VEL, 0, e) + ", " + S_(S_VEL, 1, e) +
-                         ", bb, a.wbd, v" + s + ");\n";
+                    bk_code += "        bk2(" + P_(S_POS, e) + ", " + S_(S_POS, 0, e) + ", " + S_(S_POS, 1, e) + ", bb, a.wbd, p" + s +
+                               ");\n        bk2(" + P_(S_VEL, e) + ", " + S_(S_VEL, 0, e) + ", " + S_(S_VEL, 1, e) +
+                               ", bb, a.wbd, v" + s + ");\n";
                 if (rotf)
-                    o += "        bk1(" + P_(S_ROT, e) + ", " + S_(S_ROT, 0, e) + ", bb, a.wbd, r" + s + ");\n        bk1(" +
-                         P_(S_ANG, e) + ", " + S_(S_ANG, 0, e) + ", bb, a.wbd, w" + s + ");\n";
-                o += "    }\n";
+                    bk_code += "        bk1(" + P_(S_ROT, e) + ", " + S_(S_ROT, 0, e) + ", bb, a.wbd, r" + s + ");\n        bk1(" +
+                               P_(S_ANG, e) + ", " + S_(S_ANG, 0, e) + ", bb, a.wbd, w" + s + ");\n";
             }
             if (d.agent_index >= 0)
                 o += "    V2 af" + s + " = " + ld2(S_FORCE, d.agent_index) + "; float at" + s + " = " +
@@ -819,8 +841,15 @@ struct Gen {
             o += runtime_desc(e, "    ");
         }
         const std::string pro = it((long)cfg.max_substeps * 4);
+        // the speculative first claim (loop_text): its result, waited for only here -- after this
+        // wave's state loads are in flight -- and handed to every wave by the barrier below
+        if (w == 0) o += "    if (spec && threadIdx.x == 0) QL[65] = spec_ok ? 1u : 0u;\n";
+        // the epilogue's row table (src_fns), behind the same barrier, after wave 0's loads are in flight
+        if (w == 0 && use_src()) o += "    if (prog) src_rows(a, prog, lane);\n";
         o += "    " + stamp(w, pro);
         o += "    __syncthreads();\n";
+        o += "    const bool own = !spec || QL[65] != 0u;  // (a lost speculative claim: compute, store nothing)\n";
+        if (!bk_code.empty()) o += "    if (bk && valid && own) {\n" + bk_code + "    }\n";
         o += "    " + stamp(w, pro + " + 1");
         std::vector<char> rp, rt, rr;
         if (pair_preload) {
@@ -915,9 +944,18 @@ struct Gen {
         o += "        __syncthreads();\n";
         o += "        " + stamp(w, "s * 4 + 3");
         o += "    }\n";
+        // the velocity rows balance's epilogue reads (use_src)
+        if (use_src()) {
+            std::string vr;
+            for (int e : wave_ents[w])
+                if (r_v[e] >= 0)
+                    vr += "        " + row(r_v[e]) + " = v" + it(e) + ".x; " + row(r_v[e], 1) + " = v" + it(e) + ".y; " +
+                          row(r_w[e]) + " = w" + it(e) + ";\n";
+            if (!vr.empty()) o += "    if (a.epi) {\n" + vr + "    }\n";
+        }
         // epilogue: the integrated fields into the fresh output tensors
         if (!wave_ents[w].empty()) {
-            o += "    if (valid) {\n";
+            o += "    if (valid && own) {\n";
             for (int e : wave_ents[w]) {
                 const VmasEntityDesc& d = ed[e];
                 const std::string s = it(e);
@@ -953,7 +991,7 @@ struct Gen {
             }
             o += "    }\n";
         }
-        o += "}\n\n";
+        o += "    return own;\n}\n\n";
     }
 
     // The state write-back (Args.wbd != 0; graph mode's rollback-free replays, vmas_graph_chain_set_writeback):
@@ -978,12 +1016,75 @@ struct Gen {
                "    float* q = const_cast<float*>(p);\n    q[(long)b * s0] = v.x;\n    q[(long)b * s0 + s1] = v.y;\n}\n\n";
     }
 
+    // Balance's epilogue reads the group's state from the rows (use_src): which row holds the
+    // tensor an argument-block pointer names -- a dynamic entity's output (the fresh output buffer,
+    // this launch's a.out) or a static entity's input (a.ptr) -- compared pointer and strides, once
+    // per workgroup by thread 0 (prologue); -1: not held in a row, the program reads the tensor.
+    std::string src_fns() const {
+        std::string rp = "__device__ __forceinline__ int row_pos(const Args& a, const float* p, int s0, int s1) {\n";
+        std::string rv = "__device__ __forceinline__ int row_vel(const Args& a, const float* p, int s0, int s1) {\n";
+        std::string rr = "__device__ __forceinline__ int row_rot(const Args& a, const float* p, int s0) {\n";
+        std::string rw = "__device__ __forceinline__ int row_ang(const Args& a, const float* p, int s0) {\n";
+        for (int e = 0; e < E; ++e) {
+            const VmasEntityDesc& d = ed[e];
+            if (r_p[e] >= 0) {
+                if (dyn[e] && d.out_lin >= 0)
+                    rp += "    if (p == a.out[0] + (size_t)" + it(d.out_lin) + " * a.B * 2 && s0 == 2 && s1 == 1) return " +
+                          it(r_p[e]) + ";\n";
+                else if (!dyn[e] || d.out_lin < 0)
+                    rp += "    if (p == " + P_(S_POS, e) + " && s0 == " + S_(S_POS, 0, e) + " && s1 == " + S_(S_POS, 1, e) +
+                          ") return " + it(r_p[e]) + ";\n";
+            }
+            if (r_rot[e] >= 0) {
+                if (dyn[e] && d.out_rot >= 0)
+                    rr += "    if (p == a.out[2] + (size_t)" + it(d.out_rot) + " * a.B && s0 == 1) return " + it(r_rot[e]) + ";\n";
+                else if (!dyn[e] || d.out_rot < 0)
+                    rr += "    if (p == " + P_(S_ROT, e) + " && s0 == " + S_(S_ROT, 0, e) + ") return " + it(r_rot[e]) + ";\n";
+            }
+            if (r_v[e] >= 0 && d.out_lin >= 0)
+                rv += "    if (p == a.out[1] + (size_t)" + it(d.out_lin) + " * a.B * 2 && s0 == 2 && s1 == 1) return " +
+                      it(r_v[e]) + ";\n";
+            if (r_w[e] >= 0 && d.out_rot >= 0)
+                rw += "    if (p == a.out[3] + (size_t)" + it(d.out_rot) + " * a.B && s0 == 1) return " + it(r_w[e]) + ";\n";
+        }
+        const std::string end = "    return -1;\n}\n";
+        return rp + end + rv + end + rr + "    (void)a; (void)p; (void)s0;\n" + end + rw + "    (void)a; (void)p; (void)s0;\n" + end +
+               "__shared__ int ESRC[kBalFields];\n"
+               "// (wave 0, a field per lane: thread 0 alone walking the fields held every workgroup ~3 us)\n"
+               "__device__ __forceinline__ void src_rows(const Args& a, const VmasBalanceIO* io, int lane) {\n"
+               "    for (int f = lane; f < kBalFields; f += 64) {\n"
+               "        const float* p = nullptr;\n"
+               "        int s0 = 0, s1 = 0, kind = 0;  // 0 position, 1 velocity, 2 rotation, 3 angular velocity\n"
+               "        if (f < kBalLineRot) {\n"
+               "            const VmasShapeRef* x = f == kBalPkgPos ? &io->package : f == kBalGoalPos ? &io->goal\n"
+               "                                   : f == kBalLinePos ? &io->line : &io->floor;\n"
+               "            p = x->pos; s0 = x->pos_s0; s1 = x->pos_s1;\n"
+               "        } else if (f <= kBalFloorRot) {\n"
+               "            const VmasShapeRef* x = f == kBalLineRot ? &io->line : &io->floor;\n"
+               "            p = x->rot; s0 = x->rot_s0; kind = 2;\n"
+               "        } else if (f < kBalAgPos) {\n"
+               "            const VmasVec* v = f == kBalPkgVel ? &io->package_vel : f == kBalLineVel ? &io->line_vel : &io->line_ang_vel;\n"
+               "            p = v->p; s0 = v->s0; s1 = v->s1; kind = f == kBalLineAng ? 3 : 1;\n"
+               "        } else {\n"
+               "            const int i = f < kBalAgVel ? f - kBalAgPos : f - kBalAgVel;\n"
+               "            if (i < io->n_agents) {\n"
+               "                const VmasVec* v = f < kBalAgVel ? &io->agent_pos[i] : &io->agent_vel[i];\n"
+               "                p = v->p; s0 = v->s0; s1 = v->s1; kind = f < kBalAgVel ? 0 : 1;\n"
+               "            }\n"
+               "        }\n"
+               "        ESRC[f] = !p ? -1 : kind == 0 ? row_pos(a, p, s0, s1) : kind == 1 ? row_vel(a, p, s0, s1)\n"
+               "                              : kind == 2 ? row_rot(a, p, s0) : row_ang(a, p, s0);\n"
+               "    }\n}\n\n";
+    }
+
     // The group loop: one copy per wave (loop_per_wave, the default), each calling its own run<w>,
     // or one loop around a switch over the waves (VMAS_JIT_LOOP_PER_WAVE=0).  With one loop the
     // compiler hoists the loop-invariant address / stride values of EVERY wave's body above it,
     // all live at once (balance: 106 SGPRs and 163 v_writelane spills of them into VGPR lanes,
     // read back with v_readlane -- VALU instructions); with a loop per wave only that wave's are.
     bool loop_per_wave = true;  // (required by ng > 1)
+    // the launch's first group run before its claim is confirmed (loop_text; VMAS_JIT_SPEC_CLAIM=0: claimed first)
+    bool spec_claim = true;
     // the scenario program's argument block copied into LDS at the launch's start (epi_lds, the
     // default; VMAS_JIT_EPI_LDS=0: read through Args.epi): the epilogue's field reads are LDS reads
     // instead of a cold scalar-cache miss per group
@@ -996,18 +1097,29 @@ struct Gen {
         // agent-scope fences here write back L2 per group: 38 -> 159 us per launch) -- each pass of
         // the fixed point re-running it after its group, the final pass's writes last (as the
         // state outputs).  Q: the row buffer, idle between groups.
-        const std::string q = epi_q_in_rows() ? (ng > 1 ? "Ls" : "L")
+        const std::string lb = ng > 1 ? "Ls" : "L";
+        const std::string q = epi_q_in_rows() ? lb + (epi_q_row() ? " + " + it(epi_q_row() * 64) : std::string())
                                                : (ng > 1 ? "EQ + sub * " + it((long)kEpiQRows * 64) : "EQ");
+        // (balance: the group's state from the rows -- use_src, BalRows)
+        const std::string src = use_src() ? ", &SRC" : "";
         return "        if (a.epi) {\n"
                "            __syncthreads();\n"
-               "            " + (ng > 1 ? epi_call(io, "g * " + it(ng) + " + sub", "WAVE", "lane", q)
-                                        : epi_call(io, "g", "wave", "lane", q)) + ";\n"
+               + std::string(use_src() ? "            const BalRows SRC{" + lb + ", ESRC, lane};\n" : "") +
+               "            " + (ng > 1 ? epi_call(io, "g * " + it(ng) + " + sub", "WAVE", "lane", q, src)
+                                        : epi_call(io, "g", "wave", "lane", q, src)) + ";\n"
                "            __syncthreads();\n"
                "        }\n";
     }
     std::string loop_text(const std::string& run, const std::string& cur, const std::string& io) const {
-        return "    for (;;) {\n"
-               "        const int g = grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, " + cur + ", QL);\n"
+        // The launch's first group is this workgroup's own (g = blockIdx.x), run speculatively: its
+        // claim's compare-and-swap is issued here and its result read only after the group's state
+        // loads (run<0>), so the claim's round trip overlaps them; a lost claim (another workgroup
+        // stole the group before this one started) discards the group -- no store, no epilogue, no
+        // completion.  The cursor already points past it (world_body).
+        return "    bool spec = persistent && spec_first, spec_ok = true, own = true;\n"
+               "    if (spec && threadIdx.x == 0) spec_ok = grid_claim(claim, (int)blockIdx.x, (" + cur + ")->base);\n"
+               "    for (;;) {\n"
+               "        const int g = spec ? (int)blockIdx.x : grid_next(persistent, a.ctl, claim, a.mask, MSK, nwords, ngrp, " + cur + ", QL);\n"
                "        if (g < 0) break;\n" + block_stamp(4, "__builtin_amdgcn_s_memrealtime()") +
                "        if (persistent) {\n"
                "            for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
@@ -1020,7 +1132,9 @@ struct Gen {
                "            // the state write-back (Args.wbd, wb_text): this pass's inputs, its backup\n"
                "            const bool wbx = persistent && a.wbd != 0;\n"
                "            const long long rbd = (wbx && (" + cur + ")->pass > 0) ? a.wbd : 0ll;\n"
-               "            const bool bk = wbx && (" + cur + ")->pass == 0;\n" + run + "        }\n" + epi_text(io) +
+               "            const bool bk = wbx && (" + cur + ")->pass == 0;\n" + run + "        }\n"
+               "        spec = false;\n"
+               "        if (!own) continue;\n" + epi_text(io) +
                "        if (persistent && grid_finish(g, FL, nfl, a.blk, a.mask, MSK, a.ctl, a.err, a.herr, nwords, ngrp, " + cur + ",\n"
                "                                      a.max_pass, RED, &QL[65], a.tm, t0s.rt, t0s.sc))\n"
                "            poison_outputs(a);\n" + block_stamp(5, "__builtin_amdgcn_s_memrealtime()") +
@@ -1073,8 +1187,11 @@ struct Gen {
         o += "constexpr bool HAS_XS = " + bl(cfg.has_x_semidim) + ", HAS_YS = " + bl(cfg.has_y_semidim) + ";\n";
         for (int e = 0; e < E; ++e)
             if (dyn[e]) o += "constexpr VmasEntityDesc D" + it(e) + "c" + desc(e) + ";\n";
-        o += "\ntemplate <int WAVE>\n__device__ __forceinline__ void run(const Args& a, float* L, uint32_t* FL, "
-             "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid, long long rbd, bool bk, bool wbk);\n\n";
+        o += "\ntemplate <int WAVE>\n__device__ __forceinline__ bool run(const Args& a, float* L, uint32_t* FL, "
+             "uint32_t* DONE, const uint32_t* MSK, int lane, int b, int bb, bool valid, long long rbd, bool bk, bool wbk, "
+             "bool spec, bool spec_ok, uint32_t* QL" + std::string(use_src() ? ", const VmasBalanceIO* prog" : "") +
+             ");\n\n";
+        if (use_src()) o += src_fns();
         for (int w = 0; w < nw; ++w) wave_body(o, w);
         // waves per SIMD the register budget must allow: 2 workgroups per CU (4) or 1 (2)
         const int waves_per_eu = (lds_budget <= kLdsTwoPerCu ? 2 : 1) * nw * ng / 4;
@@ -1095,14 +1212,14 @@ struct Gen {
         if (loop_per_wave) {
             o += "template <int WAVE>\n__device__ __forceinline__ void group_loop(const Args& a, float* L, uint32_t* FL, uint32_t* DONE, "
                  "uint32_t* MSK, uint32_t* QL, uint32_t* RED, float* EQ, GridCursor* CURP, uint32_t* claim, TimerStart t0s, "
-                 "bool persistent, int nfl, int nwords, int ngrp, int lane, int wave" +
+                 "bool persistent, bool spec_first, int nfl, int nwords, int ngrp, int lane, int wave" +
                  std::string(ng > 1 ? ", int sub" : "") +
                  std::string(has_epi() ? std::string(", const ") + epi_type() + "* PROG_IOP" : std::string()) + ") {\n    (void)EQ;\n";
             if (ng > 1)  // (this wave's group: its rows and split-pair counters)
                 o += "    float* const Ls = L + sub * " + it((long)std::max(n_rows, 1) * 64) + ";\n"
                      "    uint32_t* const DONEs = DONE + sub * " + it(n_split) + ";\n    (void)Ls;\n";
-            o += loop_text(ng > 1 ? "            run<WAVE>(a, Ls, FL, DONEs, MSK, lane, b, bb, valid, rbd, bk, wbx);\n"
-                                  : "            run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx);\n",
+            o += loop_text(ng > 1 ? "            own = run<WAVE>(a, Ls, FL, DONEs, MSK, lane, b, bb, valid, rbd, bk, wbx, spec, spec_ok, QL" + std::string(use_src() ? ", a.epi ? PROG_IOP : nullptr" : "") + ");\n"
+                                  : "            own = run<WAVE>(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx, spec, spec_ok, QL" + std::string(use_src() ? ", a.epi ? PROG_IOP : nullptr" : "") + ");\n",
                            "CURP", "*PROG_IOP");
             o += "}\n\n";
         }
@@ -1140,7 +1257,10 @@ struct Gen {
              "    uint32_t* claim = a.mask + " + it(vmas::grid_claim_offset((long)cfg.max_substeps * W)) + ";\n"
              "    const TimerStart t0s = device_timer_start(persistent ? a.tm : nullptr, true);\n"
              "    __shared__ GridCursor CUR;\n"
-             "    if (threadIdx.x == 0) CUR = GridCursor{0, (int)blockIdx.x, 0, 0, 0, persistent ? ld64(&a.ctl[kGridEpoch]) : 0ull};\n"
+             "    const bool spec_first = " + std::string(spec_claim ? "persistent && (int)blockIdx.x < ngrp" : "false") +
+             ";  // (the speculative first group: loop_text)\n"
+             "    if (threadIdx.x == 0)\n"
+             "        CUR = GridCursor{0, (int)blockIdx.x + (spec_first ? (int)gridDim.x : 0), 0, 0, 0, persistent ? ld64(&a.ctl[kGridEpoch]) : 0ull};\n"
              "    for (int i = threadIdx.x; i < nfl; i += blockDim.x) FL[i] = 0u;\n"
              "    for (int i = threadIdx.x; i < nwords; i += blockDim.x) MSK[i] = ~ld_agent(&a.mask[i]);\n" +
              std::string(has_epi() && epi_lds ?
@@ -1165,14 +1285,14 @@ struct Gen {
             for (int w = 0; w < nw; ++w)
                 sw += "        case " + it(w) + ": group_loop<" + it(w) + ">(a, L, FL, DONE, MSK, QL, RED, " +
                       std::string(has_epi() && !epi_q_in_rows() ? "EQ" : "nullptr") +
-                      ", &CUR, claim, t0s, persistent, nfl, nwords, ngrp, lane, wave" +
+                      ", &CUR, claim, t0s, persistent, spec_first, nfl, nwords, ngrp, lane, wave" +
                       std::string(ng > 1 ? ", wave / " + it(nw) : "") +
                       std::string(has_epi() ? (epi_lds ? ", &PROG_IO" : ", a.epi") : "") + "); break;\n";
             o += sw + "        default: break;\n    }\n";
         } else {
             std::string sw = "            switch (wave) {\n";
             for (int w = 0; w < nw; ++w)
-                sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx); break;\n";
+                sw += "                case " + it(w) + ": run<" + it(w) + ">(a, L, FL, DONE, MSK, lane, b, bb, valid, rbd, bk, wbx, spec, spec_ok, QL" + std::string(use_src() ? (epi_lds ? ", a.epi ? &PROG_IO : nullptr" : ", a.epi") : "") + "); break;\n";
             o += loop_text(sw + "                default: break;\n            }\n", "&CUR", epi_lds ? "PROG_IO" : "*a.epi");
         }
         o += block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
@@ -1201,6 +1321,7 @@ void codegen_knobs(Gen& g) {
     if (const char* pp = getenv("VMAS_JIT_PAIR_PRELOAD")) g.pair_preload = atoi(pp) != 0;
     if (const char* lw = getenv("VMAS_JIT_LOOP_PER_WAVE")) g.loop_per_wave = atoi(lw) != 0 || g.ng > 1;
     if (const char* el = getenv("VMAS_JIT_EPI_LDS")) g.epi_lds = atoi(el) != 0;
+    if (const char* sc = getenv("VMAS_JIT_SPEC_CLAIM")) g.spec_claim = atoi(sc) != 0;
 }
 
 // Plan a world: box pairs split with two workgroups per CU, else unsplit, else unsplit with the
@@ -1226,6 +1347,7 @@ std::unique_ptr<Gen> make_plan(const VmasWorldConfig& cfg, const std::vector<Vma
         if (ng > 1 && t.global_rows) continue;
         std::unique_ptr<Gen> g(new Gen(cfg, ed, pd, jd));
         g->ng = ng;
+        if (const char* es = getenv("VMAS_JIT_EPI_SRC")) g->epi_src = atoi(es) != 0;  // (read before plan: rows)
         if (const char* pm = getenv("VMAS_JIT_PRM_MASK")) g->prm_mask = (unsigned)strtoul(pm, nullptr, 0) & 0xFFFu;
         if ((size_t)cfg.max_substeps * g->W > 1024) {
             *why = "too many substeps x pairs";

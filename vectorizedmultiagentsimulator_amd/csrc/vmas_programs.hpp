@@ -173,21 +173,68 @@ __device__ __forceinline__ float xdist_spheres(const VmasShapeRef& a, const Vmas
 constexpr int kBalQRows = 28;
 __device__ __forceinline__ float* bal_q(float* Q, int row) { return Q + row * 64; }
 
+// Where the program reads the step's state.  Every launch outside k_world: the argument block's
+// tensors.  As k_world's epilogue (vmas_jit.hip epi_text): the LDS rows k_world already holds the
+// group's integrated state in (positions, rotations, velocities; a row index per field, -1 = read
+// the tensor), found by comparing the argument block's pointers with k_world's own output / input
+// tensors -- the same fp32 values, without the round trip to HBM that re-reading the step's just
+// written (write-through) outputs costs.
+enum BalField {
+    kBalPkgPos, kBalGoalPos, kBalLinePos, kBalFloorPos, kBalLineRot, kBalFloorRot, kBalPkgVel, kBalLineVel,
+    kBalLineAng, kBalAgPos, kBalAgVel = kBalAgPos + VMAS_SCN_MAX_AGENTS, kBalFields = kBalAgVel + VMAS_SCN_MAX_AGENTS
+};
+struct BalRows {
+    const float* L;  // the row buffer ([row][lane], 64 floats per row)
+    const int* row;  // kBalFields row indices
+    int lane;
+};
+template <class IO>
+__device__ __forceinline__ V2 bal_v2(IO& io, const BalRows* s, int f, int b) {
+    if (s) {
+        const int r = __builtin_amdgcn_readfirstlane(s->row[f]);  // (one value for the workgroup)
+        if (r >= 0) return mk(s->L[r * 64 + s->lane], s->L[(r + 1) * 64 + s->lane]);
+    }
+    switch (f) {
+        case kBalPkgPos: { const VmasShapeRef x = io.package; return ref_pos(x, b); }
+        case kBalGoalPos: { const VmasShapeRef x = io.goal; return ref_pos(x, b); }
+        case kBalLinePos: { const VmasShapeRef x = io.line; return ref_pos(x, b); }
+        case kBalFloorPos: { const VmasShapeRef x = io.floor; return ref_pos(x, b); }
+        case kBalPkgVel: { const VmasVec v = io.package_vel; return ld_vec2(v, b); }
+        case kBalLineVel: { const VmasVec v = io.line_vel; return ld_vec2(v, b); }
+        default:
+            if (f >= kBalAgVel) { const VmasVec v = io.agent_vel[f - kBalAgVel]; return ld_vec2(v, b); }
+            { const VmasVec v = io.agent_pos[f - kBalAgPos]; return ld_vec2(v, b); }
+    }
+}
+template <class IO>
+__device__ __forceinline__ float bal_f1(IO& io, const BalRows* s, int f, int b) {
+    if (s) {
+        const int r = __builtin_amdgcn_readfirstlane(s->row[f]);
+        if (r >= 0) return s->L[r * 64 + s->lane];
+    }
+    switch (f) {
+        case kBalLineRot: { const VmasShapeRef x = io.line; return ref_rot(x, b); }
+        case kBalFloorRot: { const VmasShapeRef x = io.floor; return ref_rot(x, b); }
+        default: { const VmasVec v = io.line_ang_vel; return ld_vec1(v, b); }
+    }
+}
+
 // side `side` of both box queries, env bb
 template <class IO>
-__device__ __forceinline__ void bal_side(IO& io, int bb, int side, int lane, float* Q) {
-    const VmasShapeRef fl = io.floor, ln = io.line, pk = io.package;
-    const float rb = ref_rot(ln, bb);
-    const V2 pf = ref_pos(fl, bb);
-    const Trig tf = xtrig(ref_rot(fl, bb));
+__device__ __forceinline__ void bal_side(IO& io, int bb, int side, int lane, float* Q, const BalRows* src = nullptr) {
+    const VmasShapeRef fl = io.floor, ln = io.line;
+    const float rb = bal_f1(io, src, kBalLineRot, bb);
+    const V2 pf = bal_v2(io, src, kBalFloorPos, bb);
+    const Trig tf = xtrig(bal_f1(io, src, kBalFloorRot, bb));
     const Seg sd = box_side(pf, tf, fl.length * 0.5f, fl.width * 0.5f, side);
     Pts q;
-    xclosest_points_line_line(sd, Seg{ref_pos(ln, bb), mk(cosf(rb), sinf(rb)), ln.length * 0.5f}, &q.p1, &q.p2);
+    xclosest_points_line_line(sd, Seg{bal_v2(io, src, kBalLinePos, bb), mk(cosf(rb), sinf(rb)), ln.length * 0.5f}, &q.p1,
+                              &q.p2);
     bal_q(Q, 4 * side + 0)[lane] = q.p1.x;
     bal_q(Q, 4 * side + 1)[lane] = q.p1.y;
     bal_q(Q, 4 * side + 2)[lane] = q.p2.x;
     bal_q(Q, 4 * side + 3)[lane] = q.p2.y;
-    const V2 ps = ref_pos(pk, bb);  // closest_point_box (physics.py:262-294), this side's candidate
+    const V2 ps = bal_v2(io, src, kBalPkgPos, bb);  // closest_point_box (physics.py:262-294), this side's candidate
     const V2 p = closest_point_line(sd.p, sd.dir, sd.half, ps, true);
     bal_q(Q, 16 + 3 * side + 0)[lane] = p.x;
     bal_q(Q, 16 + 3 * side + 1)[lane] = p.y;
@@ -196,9 +243,11 @@ __device__ __forceinline__ void bal_side(IO& io, int bb, int side, int lane, flo
 
 // done = on_the_ground + is_overlapping(package, goal)
 template <class IO>
-__device__ __forceinline__ void bal_done(IO& io, int b, bool og, const OutDelta& od) {
+__device__ __forceinline__ void bal_done(IO& io, int b, bool og, const OutDelta& od, const BalRows* src = nullptr) {
     const VmasShapeRef pk = io.package, gl = io.goal;
-    moved(io.done, od.done)[b] = (og || xdist_spheres(pk, gl, b) < 0.f) ? 1 : 0;
+    // xdist_spheres' arithmetic: (|pa - pb| - r_a) - r_b
+    const float d = (xnorm(bal_v2(io, src, kBalPkgPos, b) - bal_v2(io, src, kBalGoalPos, b)) - pk.radius) - gl.radius;
+    moved(io.done, od.done)[b] = (og || d < 0.f) ? 1 : 0;
 }
 
 // (an A/B knob of the package / floor preload: -DVMAS_BAL_PRELOAD_POS=0 through VMAS_JIT_CFLAGS)
@@ -213,9 +262,9 @@ struct BalPre {
     V2 goal, pkg, pf;
 };
 template <class IO>
-__device__ __forceinline__ BalPre bal_preload(IO& io, int bb) {
-    const VmasShapeRef gl = io.goal, pk = io.package, fl = io.floor;
-    return BalPre{io.global_shaping[(long)bb * io.gs_s0], ref_pos(gl, bb), ref_pos(pk, bb), ref_pos(fl, bb)};
+__device__ __forceinline__ BalPre bal_preload(IO& io, int bb, const BalRows* src = nullptr) {
+    return BalPre{io.global_shaping[(long)bb * io.gs_s0], bal_v2(io, src, kBalGoalPos, bb), bal_v2(io, src, kBalPkgPos, bb),
+                  bal_v2(io, src, kBalFloorPos, bb)};
 }
 
 // The reward block of env b from the sides in Q: closest_line_box's and closest_point_box's
@@ -271,16 +320,13 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
 
 // agent i's 16-entry observation in env b
 template <class IO>
-__device__ __forceinline__ void bal_obs(IO& io, int b, int i, const OutDelta& od) {
-    const VmasShapeRef pk = io.package, gl = io.goal, ln = io.line;
-    const VmasVec pvv = io.package_vel, lvv = io.line_vel, lav = io.line_ang_vel, apv = io.agent_pos[i],
-                  avv = io.agent_vel[i];
-    const V2 pkg = ref_pos(pk, b), goal = ref_pos(gl, b);
-    const V2 lpos = ref_pos(ln, b), pv = ld_vec2(pvv, b), lv = ld_vec2(lvv, b);
-    const float law = ld_vec1(lav, b);
-    const float lrot = torch_remainder(ref_rot(ln, b), io.pi);
+__device__ __forceinline__ void bal_obs(IO& io, int b, int i, const OutDelta& od, const BalRows* src = nullptr) {
+    const V2 pkg = bal_v2(io, src, kBalPkgPos, b), goal = bal_v2(io, src, kBalGoalPos, b);
+    const V2 lpos = bal_v2(io, src, kBalLinePos, b), pv = bal_v2(io, src, kBalPkgVel, b), lv = bal_v2(io, src, kBalLineVel, b);
+    const float law = bal_f1(io, src, kBalLineAng, b);
+    const float lrot = torch_remainder(bal_f1(io, src, kBalLineRot, b), io.pi);
     const V2 pg = pkg - goal;
-    const V2 p = ld_vec2(apv, b), v = ld_vec2(avv, b);
+    const V2 p = bal_v2(io, src, kBalAgPos + i, b), v = bal_v2(io, src, kBalAgVel + i, b);
     const V2 dp = p - pkg, dl = p - lpos;
     float4* dst = reinterpret_cast<float4*>(moved(io.obs[i], od.obs) + (long)b * 16);
     dst[0] = make_float4(p.x, p.y, v.x, v.y);
@@ -293,20 +339,21 @@ __device__ __forceinline__ void bal_obs(IO& io, int b, int i, const OutDelta& od
 // barrier inside): waves 0-3 the four box sides, waves 4.. the observations, then wave 0 the
 // reward block and done.  Q: kBalQRows x 64 floats of LDS.
 template <class IO>
-__device__ __forceinline__ void balance_group(IO& io, int g, int wave, int nwave, int lane, float* Q) {
+__device__ __forceinline__ void balance_group(IO& io, int g, int wave, int nwave, int lane, float* Q,
+                                              const BalRows* src = nullptr) {
     const int b = g * 64 + lane;
     const bool valid = b < io.batch;
     const int bb = valid ? b : io.batch - 1;
     const OutDelta od = load_out_delta(io);
     const bool rew = io.what & VMAS_SCN_REWARD;
-    const BalPre pre = rew && wave == 0 ? bal_preload(io, bb) : BalPre{0.f, mk(0.f, 0.f), mk(0.f, 0.f), mk(0.f, 0.f)};
-    if (rew && wave < 4) bal_side(io, bb, wave, lane, Q);
+    const BalPre pre = rew && wave == 0 ? bal_preload(io, bb, src) : BalPre{0.f, mk(0.f, 0.f), mk(0.f, 0.f), mk(0.f, 0.f)};
+    if (rew && wave < 4) bal_side(io, bb, wave, lane, Q, src);
     if ((io.what & VMAS_SCN_OBS) && wave >= 4 && valid)
-        for (int i = wave - 4; i < io.n_agents; i += nwave - 4) bal_obs(io, b, i, od);
+        for (int i = wave - 4; i < io.n_agents; i += nwave - 4) bal_obs(io, b, i, od, src);
     __syncthreads();
     if (wave != 0 || !valid) return;
     if (rew) bal_reward(io, b, lane, od, Q, pre);
-    else if (io.what & VMAS_SCN_DONE) bal_done(io, b, io.on_the_ground[b] != 0, od);
+    else if (io.what & VMAS_SCN_DONE) bal_done(io, b, io.on_the_ground[b] != 0, od, src);
 }
 
 // ---- transport (transport.py:130-190; restated in scenarios/transport.py) -------------------------

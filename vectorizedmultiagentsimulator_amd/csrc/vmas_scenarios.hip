@@ -804,9 +804,26 @@ __global__ void k_test_exact_math(const float* a, const float* b, float* out, lo
     out[3 * n + i] = sqrtf(a[i]);
 }
 
+// The fast LIDAR programs' direction instructions (v_sin_f32 / v_cos_f32 through __sinf / __cosf,
+// as k_flocking_fast / k_discovery_obs_fast compute a ray's (cos, sin)): out[i] = sin, out[n + i] = cos.
+__global__ void k_test_fast_trig(const float* x, float* out, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = __sinf(x[i]);
+    out[n + i] = __cosf(x[i]);
+}
+
 }  // namespace
 
 extern "C" {
+
+int32_t vmas_test_fast_trig(int32_t device, const float* x, float* out, int64_t n, void* stream) {
+    if (device < 0 || !x || !out || n <= 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_test_fast_trig: bad arguments");
+    VMAS_AUX_HIP(hipSetDevice(device));
+    hipLaunchKernelGGL(k_test_fast_trig, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, out, (long)n);
+    VMAS_AUX_HIP(hipGetLastError());
+    return VMAS_OK;
+}
 
 int32_t vmas_test_exact_math(int32_t device, const float* a, const float* b, float* out, int64_t n, void* stream) {
     if (device < 0 || !a || !b || !out || n <= 0) return vmas_aux::fail(VMAS_E_INVALID, "vmas_test_exact_math: bad arguments");

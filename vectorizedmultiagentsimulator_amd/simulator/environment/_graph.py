@@ -91,16 +91,21 @@ def _tracked_objects(env) -> List[Any]:
     return out
 
 
-def _own_scenario(scenario) -> bool:
-    """The scenario is one of this package's own classes, unmodified (its make_world defined in
-    the class itself, in a file of the package's scenarios directory): only then does the step's
-    code hold the contracts DirectOutputs and the write-only attributes rely on.  (make_env loads
-    scenario modules afresh, without a package name: by source file.)"""
+def _package_scenario_class(scenario) -> bool:
+    """The scenario's class is one of this package's own (its make_world defined in the class
+    itself, in a file of the package's scenarios directory).  (make_env loads scenario modules
+    afresh, without a package name: by source file.)"""
     scn_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                            "scenarios") + os.sep
     cls = type(scenario)
-    if not (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
-            and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir)):
+    return (cls.__qualname__ == "Scenario" and "make_world" in cls.__dict__
+            and os.path.abspath(cls.make_world.__code__.co_filename).startswith(scn_dir))
+
+
+def _own_scenario(scenario) -> bool:
+    """The scenario is one of this package's own classes, unmodified: only then does the step's
+    code hold the contracts DirectOutputs and the write-only attributes rely on."""
+    if not _package_scenario_class(scenario):
         return False
     # a step-time method overridden on the instance (a monkeypatched reward / post_step ...) may
     # read a write-only attribute before the class's own code re-binds it (ADVICE r4)
@@ -745,7 +750,15 @@ class StepGraph:
                     self.drop(f"attribute {k} re-bound to a tensor of another shape")
                     return
                 with torch.no_grad():
-                    t.copy_(cur)
+                    try:
+                        t.copy_(cur)
+                    except RuntimeError:
+                        # the captured tensor is a broadcast view (a user's set_pos(t.expand(B, 2))
+                        # keeps the expanded tensor): not writable per element -- the same values
+                        # keep the capture, others drop it (the env recaptures)
+                        if not torch.equal(cur, t):
+                            self.drop(f"attribute {k} re-bound: its captured tensor is a broadcast view")
+                            return
                 d[k] = t
                 self.copied = True
         if not self._first_replay and not self._carry_current():
@@ -825,7 +838,9 @@ class StepGraph:
 
             self.env.world._hole_sink = hole
             objs = _tracked_objects(self.env)
-            strict = not _trusted_scenario(self.env.scenario)
+            # (strict for a class outside the package: the package's scenarios keep their own
+            # Python-side caches of the fused programs, keyed by tensor versions, which are not step state)
+            strict = not _package_scenario_class(self.env.scenario)
             plain0 = _plain_attrs(objs, strict)
             try:
                 with consts:
