@@ -6,7 +6,12 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports 1/2 
 wide coalesced reads -> doubled; WRITE_SIZE is taken as reported.  Both counters are KiB.
 
 The bench JSON line that each pass's log holds gives the workload and the generated kernel's
-source sha256 (roofline.kernel_source_sha256); every pass must agree.  The counter CSVs are
+source sha256 (roofline.kernel_source_sha256); every pass must agree.  When that line's headline
+is the fused variant (roofline.plain set: a graph-mode run whose replay launches k_world with the
+scenario program as its epilogue), the record's per-launch figures are those of the fused timer's
+launches -- k_world dispatches [warmup+steps+5, warmup+steps+55) in dispatch order, as
+tools/rocprof_record.py splits them -- and `plain` holds the last 50 launches (the step kernel
+alone, bench.py's graph timer); `all_launches` averages every k_world dispatch.  The counter CSVs are
 copied under profiles/<dest>/ so that the record's evidence is tracked.
 
 usage: python tools/pmc_traffic.py <pmc dir: p1/, p1.log, p2/, ...> <profiles dest dir> [kernel]
@@ -21,16 +26,28 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def per_launch(d, counter, kernel):
+SLICE = None  # (lo, hi) over the kernel's dispatches in order, or None for all of them
+
+
+def per_launch(d, counter, kernel, sl=None):
     vals = {}
     for f in glob.glob(f"{d}/**/pmc_counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             name = row["Kernel_Name"].split("(")[0].strip()
             if name == kernel and row["Counter_Name"] == counter:
-                vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+                k = int(row["Dispatch_Id"])
+                vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} under {d}")
-    return sum(vals.values()) / len(vals), len(vals)
+    v = [vals[k] for k in sorted(vals)]
+    sl = SLICE if sl is None else sl
+    if sl == "all":
+        sl = None
+    if sl is not None:
+        v = v[sl[0]:sl[1]]
+        if not v:
+            raise SystemExit(f"{counter}: no {kernel} dispatches in slice {sl} under {d}")
+    return sum(v) / len(v), len(v)
 
 
 def bench_line(log):
@@ -50,6 +67,23 @@ def main():
         raise SystemExit(f"passes disagree: {hashes} {workloads}")
     b = lines[0]
     alg = b["roofline"]["alg_bytes_per_env_step"] * b["config"]["num_envs_per_gpu"]
+    global SLICE
+    fused = bool(b["roofline"].get("plain"))
+    if fused:
+        w, n = int(b.get("warmup", 0)), int(b.get("steps", 0))
+        SLICE = (w + n + 5, w + n + 55)
+    plain = all_l = None
+    if fused:
+        pf, pw = per_launch(d, "FETCH_SIZE", kernel, (-50, None))[0], per_launch(d, "WRITE_SIZE", kernel, (-50, None))[0]
+        plain = {"slice": "last 50 k_world dispatches (bench.py graph timer: the step kernel alone)",
+                 "hbm_bytes_per_launch": round(2 * pf * 1024 + pw * 1024),
+                 "traffic_over_alg": round((2 * pf * 1024 + pw * 1024) / alg, 3)}
+        try:
+            plain["valu_insts_per_launch"] = per_launch(d, "SQ_INSTS_VALU", kernel, (-50, None))[0]
+        except SystemExit:
+            pass
+        af, aw = per_launch(d, "FETCH_SIZE", kernel, "all")[0], per_launch(d, "WRITE_SIZE", kernel, "all")[0]
+        all_l = {"hbm_bytes_per_launch": round(2 * af * 1024 + aw * 1024)}
     fetch_kib, n1 = per_launch(d, "FETCH_SIZE", kernel)
     write_kib, n2 = per_launch(d, "WRITE_SIZE", kernel)
     extra = {}
@@ -69,6 +103,8 @@ def main():
         "workload": b["config"]["workload"],
         "kernel": kernel,
         "kernel_source_sha256": hashes.pop(),
+        "variant": ("fused: k_world + the scenario program as its epilogue, dispatches "
+                    f"[{SLICE[0]}, {SLICE[1]}) (bench.py's fused timer)" if fused else "the step kernel alone"),
         "launches_sampled": [n1, n2],
         "fetch_size_kib_per_launch": round(fetch_kib, 1),
         "write_size_kib_per_launch": round(write_kib, 1),
@@ -77,6 +113,8 @@ def main():
         "traffic_over_alg": round(hbm / alg, 3),
         "valu_insts_per_launch": extra.get("sq_insts_valu_per_launch"),
         **{k: v for k, v in extra.items() if k != "sq_insts_valu_per_launch"},
+        "plain": plain,
+        "all_launches": all_l,
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads), WRITE_SIZE x1; KiB -> B",
         "source": str(dest.relative_to(ROOT)),
     }
