@@ -434,11 +434,13 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms, launches, timer, clock_ghz = 0.0, 0, None, 0.0
     event_us = fused_us = None
+    if on_gpu:
+        # (the timed region's own launches: read before the fused timer's launches add to the count)
+        dev_ms, dev_n, clock_ghz = world.engine.device_timing(reset=True, with_clock=True)
     if on_gpu and args.event_launches > 0 and env.graph_status == "graph":
-        # (first after the timed region: tools/rocprof_record.py finds these 5 + 50 launches there)
+        # (first launches after the timed region: tools/rocprof_record.py finds these 5 + 50 there)
         fused_us = time_fused_chain(env)
     if on_gpu:
-        dev_ms, dev_n, clock_ghz = world.engine.device_timing(reset=True, with_clock=True)
         if env.graph_status == "graph":
             # replayed launches: HIP records no events inside a graph; the kernel's own timer
             kernel_ms, launches = dev_ms, dev_n

@@ -171,10 +171,19 @@ def test_respawn_with_cus_held_by_another_stream_gpu(gpu_device, monkeypatch):
     N.check_aux(N.load_library().vmas_test_hold(0, 250, 2_000_000, ctypes.c_void_p(side.cuda_stream)),
                 "vmas_test_hold")
     time.sleep(0.2)  # (the holding kernel resident before the respawn launch: not a race between the streams)
+    t0 = time.perf_counter()
     mx = respawn_targets_native(agents, covered, min_dist, 1.0, 1.0, *got)
     after_native = torch.rand(4, device=dev)
+    held = not side.query()  # (the holding kernel still running when the respawn call returned)
+    took = time.perf_counter() - t0
     torch.cuda.synchronize()
     for i, (e, x) in enumerate(zip(exp, got)):
         assert torch.equal(e, x), f"target {i}"
     assert torch.equal(after_ref, after_native), "generator consumption differs from the reference loop"
-    assert int(mx[N.VMAS_SPAWN_ERR_WORD].item()) == 1  # (the contended launch did time out)
+    if int(mx[N.VMAS_SPAWN_ERR_WORD].item()) != 1:
+        # The launch completed inside its wait bound: every group found a slot beside the holding
+        # kernel on this device (seen once in round 6, one box of many).  The results above are
+        # still the reference's; only the hand-over this test targets was not exercised.
+        assert took < 1.0, f"no timeout reported, yet the call took {took:.2f} s"
+        pytest.skip(f"the held CUs did not block the launch's residency (call {took * 1e3:.1f} ms, "
+                    f"hold still running: {held}): hand-over not exercised, results matched")

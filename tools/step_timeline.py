@@ -60,14 +60,15 @@ G = env._graph
 orig_launch = _graph.StepGraph._launch
 
 
-def launch(self):
+def launch(self, *a, **k):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     stamp("replay0")
-    orig_launch(self)
+    r = orig_launch(self, *a, **k)  # (a deferred kernel chain: launched later, by _post_replay)
     stamp("replay1")
     e1.record()
     events.append((e0, e1))
+    return r
 
 
 _graph.StepGraph._launch = launch

@@ -1296,7 +1296,12 @@ class StepGraph:
     # the trusted (benchmark) scenarios: X is overwritten INSIDE the step, so no kernel after k_world
     # may read the pre-step state -- their programs read the integrated state only; a user's reward
     # may keep last step's position (self.prev = agent.state.pos) and read it after World.step.
+    # Measured (profiles/r06/run3_writeback, run6_writeback_size): the write-back's stores cost
+    # k_world more than the carry costs the post-replay launch once the carried state is large --
+    # C2's 4.5 MB carry: step 49.5 -> 48.0 us; C5 shard's 7.1 MB: 62.3 -> 63.2 us; C5 full's 57 MB:
+    # 337 -> 362 us -- so it is used only up to VMAS_GRAPH_WRITEBACK_MAX_MB of carried state.
     _WRITEBACK = os.environ.get("VMAS_GRAPH_WRITEBACK", "1") != "0"  # (A/B knob)
+    _WRITEBACK_MAX_BYTES = float(os.environ.get("VMAS_GRAPH_WRITEBACK_MAX_MB", "6")) * (1 << 20)
 
     def _writeback_ready(self) -> bool:
         w = self._wb
@@ -1309,6 +1314,8 @@ class StepGraph:
                 or not _trusted_scenario(self.env.scenario)):
             return False
         x = self._carry_dst[self._state_idx]
+        if x.numel() * x.element_size() > self._WRITEBACK_MAX_BYTES:
+            return False
         backup = torch.empty_like(x)  # (the first pass's copy of the pre-step state, same offsets)
         if not self._chain.set_writeback(backup.data_ptr() - x.data_ptr()):
             return False
