@@ -570,6 +570,20 @@ def main():
             "kernel_source_sha256": src_hash,
             "pmc_record": ("profiles/pmc_traffic.json" if traffic else pmc.get("stale", "none")),
         }
+        if plain:
+            # the fused launch's own algorithmic bytes: the physics step's (above) plus the scenario
+            # program's outputs (observations, rewards, done; its state inputs are the step's own
+            # outputs, read back inside the launch) -- what its PMC traffic compares with
+            b_fused = b_env + program_bytes_per_env_step(env) - 20 * len(world.entities)
+            roofline["fused_alg"] = {
+                "bytes_per_env_step": b_fused,
+                "achieved": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9, 2),
+                "frac": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "traffic_over_alg": round(traffic / (b_fused * args.envs), 3) if traffic else None,
+                "note": ("roofline.achieved / frac keep SURVEY 8(d)'s physics bytes (384 B) over the fused "
+                         "launch's time; this adds the epilogue's outputs.  PMC traffic above it = the state "
+                         "write-back's two extra stores (inputs + first-pass backup, DESIGN.md)"),
+            }
         if rp.get("avg_us"):
             # the same command under rocprofv3 --kernel-trace (committed record, same kernel sha):
             # the profiler's own dispatch handling slows the kernel itself (DESIGN.md Measurement).

@@ -75,7 +75,17 @@ CASES = [
     # every respawn handed over to the reference loop (VMAS_SPAWN_TEST_MAX_TRIES=1): undone from the
     # launch's backup and redone after the replay, the step's observations recomputed
     ("discovery-redo", dict(n_agents=4), None, "graph"),
+    # the package's debug worlds, which the default graph step (graph_step=None) also replays
+    # (ADVICE r5): joints in exact math, a world needing several fixed-point passes, masses re-drawn
+    # by every reset (a parameter change between replays: recaptured), every physics feature
+    ("waterfall", {}, None, "graph"),
+    # (45 entities: the step's fixed point is host-driven here, a host wait per pass -- the watched
+    # step sees it, so the env stays eager; every step still equal to the eager env's)
+    ("pollock", {}, None, "eager"),
+    ("het_mass", {}, None, "graph"),  # (recaptured after each reset: the masses change)
+    ("features", {}, None, "eager"),  # (communication actions: the per-agent action path)
 ]
+MIN_REPLAYS = {"het_mass": 2}  # (replays since its last recapture, after the reset of step 10)
 
 
 # fused scenarios whose outputs the replays write directly: categories (obs, rewards, done)
@@ -132,10 +142,14 @@ def test_graph_replay_matches_eager_gpu(gpu_device, monkeypatch, name, kw, subst
     # scenarios' obs / rewards / done -- tensors the replay wrote directly, DirectOutputs)
     assert all(torch.equal(v, x) for v, x in held)
     assert graph.graph_status == expect, graph.graph_reason
+    if name == "pollock":
+        assert "host wait" in graph.graph_reason, graph.graph_reason
+    if name == "features":
+        assert "communication actions" in graph.graph_reason, graph.graph_reason
     if name in DIRECT and not hole:  # (every category of the fused launch written directly)
         assert len(graph._graph._direct.enabled) == DIRECT[name], [r["dtype"] for r in graph._graph._direct.enabled]
     if expect == "graph":
-        assert graph._graph.replays >= 5
+        assert graph._graph.replays >= MIN_REPLAYS.get(name, 5)
         if name in DIRECT:  # (each declares write-only attributes: none of them carried)
             wo = {id(t) for t in graph._graph._write_only_ys}
             assert wo and not wo & {id(y) for y in graph._graph._carry_ys}

@@ -111,6 +111,9 @@ def main():
         "hbm_bytes_per_launch": round(hbm),
         "alg_bytes_per_launch": round(alg),
         "traffic_over_alg": round(hbm / alg, 3),
+        "alg_note": ("alg = SURVEY 8(d)'s physics bytes; the fused launch also writes the scenario "
+                     "program's outputs and the state write-back's stores: bench.py reports "
+                     "roofline.fused_alg.traffic_over_alg against the fused launch's own bytes") if fused else None,
         "valu_insts_per_launch": extra.get("sq_insts_valu_per_launch"),
         **{k: v for k, v in extra.items() if k != "sq_insts_valu_per_launch"},
         "plain": plain,

@@ -414,6 +414,12 @@ class Environment(TorchVectorizedObject):
         if self._graph is not None and self.continuous_actions:
             if self._apply_continuous_actions(actions, persistent=True):
                 return self._graph.step()
+            g, c = self._graph, self._apply_cache
+            if g.graph is None and g.status == "warming" and c is not None and c[1] is None:
+                # (the world's own configuration -- communication actions of non-silent agents -- keeps
+                # the actions on the per-agent path: every step runs eagerly; report it)
+                g.status = "eager"
+                g.why = "communication actions (dim_c > 0, non-silent agents) take the per-agent action path"
         return self._step_eager(actions)
 
     def _check_action_list(self, actions):
