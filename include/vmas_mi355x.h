@@ -729,6 +729,17 @@ int32_t vmas_copy_spans_draw(int32_t device, const VmasCopySpan* spans, int32_t 
                              const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed, uint64_t offset,
                              const uint64_t* offset_dev, int32_t mode, int64_t u_snap_delta, uint64_t* increment,
                              void* stream);
+/* (round 6, no reference counterpart) The same items as vmas_copy_spans_draw run as the tail of a
+ * graph replay's single fused k_world launch (csrc/vmas_tail.hpp), by its workgroups once the
+ * broadphase fixed point's final pass is decided -- one launch per step instead of two.  wb: the
+ * chain's write-back variant (vmas_graph_chain_set_writeback).  Returns 1 when the launch is
+ * queued, 0 when the chain or the items do not admit a tail (nothing queued: launch the chain and
+ * vmas_copy_spans_draw), < 0 on error.  The caller passes only copies whose sources the launch
+ * writes through (k_world's state outputs, the scenario program's write-through outputs). */
+int32_t vmas_graph_chain_launch_tail(const VmasKernelChain* chain, int32_t wb, const VmasCopySpan* spans,
+                                     int32_t n_spans, int64_t numel, const VmasUniformColumn* cols, int32_t n_cols,
+                                     uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int32_t mode,
+                                     int64_t u_snap_delta, uint64_t* increment, void* stream);
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);

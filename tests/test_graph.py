@@ -400,9 +400,10 @@ def test_graph_refuses_host_side_step_state_gpu(gpu_device, kind):
                                                ("discovery-redo", dict(n_agents=4), None),
                                                ("balance-2pass", dict(n_agents=4), 10),
                                                ("transport-2pass", dict(n_agents=4), None),
-                                               ("balance-carry", dict(n_agents=4), 10)],
+                                               ("balance-carry", dict(n_agents=4), 10),
+                                               ("balance-notail", dict(n_agents=4), 10)],
                          ids=["balance", "flocking", "discovery", "discovery-redo", "balance-2pass", "transport-2pass",
-                              "balance-carry"])
+                              "balance-carry", "balance-notail"])
 def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name, kw, substeps):
     """env.step(env.get_random_actions()) in graph mode: the draw kernel also writes the applied
     actions into the graph's action buffer, and the step launches no action kernel.  Bit-identical
@@ -417,11 +418,17 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name
     if redo:
         monkeypatch.setenv("VMAS_SPAWN_TEST_MAX_TRIES", "1")
         name = "discovery"
+    from vectorizedmultiagentsimulator_amd import _native as N
+    from vectorizedmultiagentsimulator_amd.simulator.environment._graph import StepGraph
     carry = name.endswith("-carry")
     if carry:  # (a carried state above the write-back's size limit: the post-replay carry instead)
-        from vectorizedmultiagentsimulator_amd.simulator.environment._graph import StepGraph
         monkeypatch.setattr(StepGraph, "_WRITEBACK_MAX_BYTES", 0)
         name = name[:-len("-carry")]
+    notail = name.endswith("-notail")
+    if notail:  # (the post-replay launch of its own, VMAS_GRAPH_TAIL=0)
+        monkeypatch.setattr(StepGraph, "_TAIL", False)
+        name = name[:-len("-notail")]
+    tails0 = N.load_host().tail_launches()
     two_pass = name.endswith("-2pass")
     if two_pass:
         monkeypatch.setenv("VMAS_JIT_TEST_PASSES", "2")
@@ -477,6 +484,13 @@ def test_preapplied_random_actions_match_eager_gpu(gpu_device, monkeypatch, name
     if two_pass:
         assert "VMAS_GRID_MIN_PASSES 2" in graph.world.engine.jit_source()
         assert graph.world.engine.last_iterations == 2
+    # balance's post-replay work ran as the tail of its one fused launch (csrc/vmas_tail.hpp): the
+    # draws made ahead, the carry (the state too, without the write-back) and the info copies
+    tails = N.load_host().tail_launches() - tails0
+    if name == "balance" and not notail:
+        assert tails >= 3, tails  # (as drawn_ahead: the steps after the warm-up and the capture)
+    elif name == "balance":
+        assert tails == 0
 
 
 @pytest.mark.gpu

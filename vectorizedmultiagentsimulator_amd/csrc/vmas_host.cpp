@@ -47,6 +47,8 @@ using CopySpansDrawFn = int32_t (*)(int32_t, const VmasCopySpan*, int32_t, int64
                                     uint64_t, uint64_t, const uint64_t*, int32_t, int64_t, uint64_t*, void*);
 using LastErrorFn = const char* (*)(void);
 using ChainLaunchFn = int32_t (*)(const void*, void*);
+using ChainTailFn = int32_t (*)(const void*, int32_t, const VmasCopySpan*, int32_t, int64_t, const VmasUniformColumn*,
+                                int32_t, uint64_t, uint64_t, const uint64_t*, int32_t, int64_t, uint64_t*, void*);
 
 void* current_stream(int device) {
     return (void*)c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
@@ -377,14 +379,21 @@ struct HostTiming {
     }
 };
 HostTiming g_timing;
+int64_t g_tail_launches = 0;  // (post_draw calls whose launch ran the tail: tests, diagnostics)
 inline double now_ns() {
     return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // chain / chain_fn: the replay's kernel chain, launched first (OutputAlloc.launch_chain; 0: none).
+// tail_fn (vmas_graph_chain_launch_tail; 0: none) with wb (the chain's write-back variant): the chain's
+// one fused launch also runs these copies and the draw as its tail (csrc/vmas_tail.hpp) -- the
+// outputs and the draw's buffers are then prepared before that launch is queued; a chain that does
+// not admit the tail falls back to the two launches.
 py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, int64_t snap_base, int64_t snap_numel,
-                    int64_t copy_draw_fn, int64_t off_dev, int64_t chain, int64_t chain_fn) {
-    oa.launch_chain(chain, chain_fn);
+                    int64_t copy_draw_fn, int64_t off_dev, int64_t chain, int64_t chain_fn, int64_t tail_fn,
+                    int64_t wb) {
+    const bool tail = tail_fn && chain && mid == 0;
+    if (!tail) oa.launch_chain(chain, chain_fn);
     const bool tm = g_timing.on;
     double t0 = tm ? now_ns() : 0.0, t1 = 0.0;
     std::vector<at::Tensor> outs = oa.alloc();
@@ -401,11 +410,21 @@ py::tuple post_draw(OutputAlloc& oa, UniformDraw& d, int64_t mid, int64_t hi, in
         seed = impl->current_seed();
         off = off_dev ? 0 : impl->get_offset();
     }
-    const int32_t rc = ((CopySpansDrawFn)copy_draw_fn)(d.device(), oa.table() + lo, (int32_t)(hi - lo), d.batch(),
-                                                       d.cols(), (int32_t)d.n_cols(), seed, off,
-                                                       (const uint64_t*)off_dev, d.mode(), delta, &inc,
-                                                       current_stream(d.device()));
-    if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
+    int32_t rc = 0;
+    if (tail) {
+        rc = ((ChainTailFn)tail_fn)((const void*)chain, (int32_t)wb, oa.table() + lo, (int32_t)(hi - lo), d.batch(),
+                                    d.cols(), (int32_t)d.n_cols(), seed, off, (const uint64_t*)off_dev, d.mode(), delta,
+                                    &inc, current_stream(d.device()));
+        if (rc < 0) throw std::runtime_error(std::string("vmas_graph_chain_launch_tail failed: ") + oa.last_error());
+        if (rc == 0) oa.launch_chain(chain, chain_fn);
+    }
+    if (rc != 1) {
+        rc = ((CopySpansDrawFn)copy_draw_fn)(d.device(), oa.table() + lo, (int32_t)(hi - lo), d.batch(), d.cols(),
+                                             (int32_t)d.n_cols(), seed, off, (const uint64_t*)off_dev, d.mode(), delta,
+                                             &inc, current_stream(d.device()));
+        if (rc != VMAS_OK) throw std::runtime_error(std::string("vmas_copy_spans_draw failed: ") + oa.last_error());
+    }
+    g_tail_launches += tail && rc == 1 ? 1 : 0;
     if (tm) g_timing.ns[2] += (t1 = now_ns()) - t0;
     oa.commit();
     if (tm) g_timing.ns[3] += (t0 = now_ns()) - t1;
@@ -442,6 +461,7 @@ PYBIND11_MODULE(_vmas_host, m) {
         .def("draw", &UniformDraw::draw);
     m.def("post_draw", &post_draw, py::arg("oa"), py::arg("d"), py::arg("mid"), py::arg("hi"), py::arg("snap_base"),
           py::arg("snap_numel"), py::arg("copy_draw_fn"), py::arg("off_dev"), py::arg("chain") = 0,
-          py::arg("chain_fn") = 0);
+          py::arg("chain_fn") = 0, py::arg("tail_fn") = 0, py::arg("wb") = 0);
+    m.def("tail_launches", []() { return g_tail_launches; });
     m.def("versions", &versions);
 }

@@ -420,6 +420,11 @@ struct Gen {
             if (pd[p].cls == VMAS_PAIR_JOINT) ptr(S_JFIX, pd[p].joint), str(S_JFIX, 0, pd[p].joint);
         if (str_src.size() % 2) str_src.push_back({-1, 0});  // keep the int block 8-byte aligned
         plan_params();
+        {
+            const char* tl = getenv("VMAS_JIT_TAIL");
+            tail = has_epi() && !(tl && tl[0] == '0');
+            if (tail && arg_bytes() > kMaxArgBytes) tail = false;
+        }
         if (arg_bytes() > kMaxArgBytes) {
             *why = "kernel argument block too large (" + it(arg_bytes()) + " B)";
             return false;
@@ -454,12 +459,15 @@ struct Gen {
     // byte offset of Args.wbd (after epi): the state write-back's backup delta (0: off; see wb_text)
     size_t wbd_offset() const { return epi_offset() + (has_epi() ? 8 : 0); }
 
-    size_t arg_bytes() const {  // layout of the generated struct Args
+    size_t tail_offset() const {  // byte offset of Args.tail (after the value slots)
         // (+4 ints: B, S, sdt, max_pass; then the value slots; padded to the 8-byte alignment)
         const size_t n = 8 * (std::max<size_t>(ptr_src.size(), 1) + n_out() + 7 + (global_rows ? 1 : 0) + (has_epi() ? 1 : 0) + 1) +
                          4 * (std::max<size_t>(str_src.size(), 2) + 4) +
-                         4 * prm_src.size();
+                         4 * std::max<size_t>(prm_src.size(), 1);
         return (n + 7) & ~(size_t)7;
+    }
+    size_t arg_bytes() const {  // layout of the generated struct Args
+        return tail_offset() + (tail ? sizeof(VmasTail) : 0);
     }
 
     // expressions for entity e as seen by wave w (registers when w owns it)
@@ -1085,6 +1093,10 @@ struct Gen {
     bool loop_per_wave = true;  // (required by ng > 1)
     // the launch's first group run before its claim is confirmed (loop_text; VMAS_JIT_SPEC_CLAIM=0: claimed first)
     bool spec_claim = true;
+    // Args.tail (vmas_tail.hpp): a replay's post-replay work run after the final decision, for the
+    // modules whose k_world a kernel chain can fuse into one launch (a scenario program); dropped
+    // when the argument block would outgrow kMaxArgBytes.  VMAS_JIT_TAIL=0: none (A/B).
+    bool tail = false;
     // the scenario program's argument block copied into LDS at the launch's start (epi_lds, the
     // default; VMAS_JIT_EPI_LDS=0: read through Args.epi): the epilogue's field reads are LDS reads
     // instead of a cold scalar-cache miss per group
@@ -1163,7 +1175,8 @@ struct Gen {
              std::string(has_epi() ? std::string("    const ") + epi_type() + "* epi;\n" : std::string()) +
              "    long long wbd;\n" +
              "    int str[" + it(std::max<size_t>(str_src.size(), 2)) + "];\n    int B, S;\n    float sdt;\n    int max_pass;\n"
-             "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n};\n"
+             "    float prm[" + it(std::max<size_t>(prm_src.size(), 1)) + "];\n" +
+             std::string(tail ? "    VmasTail tail;\n" : "") + "};\n"
              "static_assert(sizeof(Args) == " + it((long)arg_bytes()) + ", \"argument block layout\");\n\n";
         o += "__device__ __forceinline__ V2 ld2(const float* p, int s0, int s1, int b) {\n"
              "    return mk(p[(long)b * s0], p[(long)b * s0 + s1]);\n}\n\n";
@@ -1296,6 +1309,8 @@ struct Gen {
             o += loop_text(sw + "                default: break;\n            }\n", "&CUR", epi_lds ? "PROG_IO" : "*a.epi");
         }
         o += block_stamp(3, "__builtin_amdgcn_s_memrealtime()") +
+             std::string(tail ? "    // the replay's post-replay work (vmas_tail.hpp): every group's final pass is decided\n"
+                                "    if (persistent && a.tail.n_items > 0) vmas_tail::run(a.tail);\n" : "") +
              "    if (!persistent) {\n"
              "        if (!a.blk) return;\n"
              "        __syncthreads();\n"
@@ -1680,6 +1695,7 @@ int32_t vmas_jit_world_create(const VmasWorldConfig* cfg, const VmasEntityDesc* 
         info.arg_bytes = W->arg_bytes;
         info.epi_offset = W->fn_prog ? (long)W->epi_offset : -1L;
         info.wbd_offset = (long)g.wbd_offset();
+        info.tail_offset = g.tail ? (long)g.tail_offset() : -1L;
         info.batch = cfg->batch;
         info.epilogue = g.has_epi() ? cfg->epilogue : VMAS_EPILOGUE_NONE;
         info.io_bytes = cfg->epilogue == VMAS_EPILOGUE_BALANCE ? sizeof(VmasBalanceIO)
@@ -1886,6 +1902,7 @@ int32_t vmas_jit_world_step(VmasJitWorld* W, const VmasStepIO* io, void* stream_
     }
     size_t size = ((size_t)(p - buf.data()) + 7) & ~(size_t)7;
     if (size > buf.size()) return jfail(VMAS_E_INVALID, "kernel argument block overflow");
+    size = buf.size();  // (Args.tail, when the module has one: zero -- no tail; a chain replay sets it)
     void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, buf.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
 

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "vmas_physics.hpp"
+#include "vmas_tail.hpp"
 
 namespace vmas {
 

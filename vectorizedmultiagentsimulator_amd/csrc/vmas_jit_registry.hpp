@@ -18,6 +18,7 @@ struct JitFnInfo {
     size_t arg_bytes;     // k_world's argument block
     long epi_offset;      // byte offset of Args.epi in it (-1: no epilogue)
     long wbd_offset;      // byte offset of Args.wbd (the state write-back's backup delta, vmas_jit.hip wb_helpers)
+    long tail_offset;     // byte offset of Args.tail (a VmasTail, vmas_tail.hpp; -1: the module has none)
     int batch;
     int epilogue;         // VMAS_EPILOGUE_*
     size_t io_bytes;      // the program's argument block (VmasBalanceIO / VmasTransportIO)

@@ -33,6 +33,8 @@
 #include "vmas_physics.hpp"
 #include "vmas_query.hpp"
 #include "vmas_jit_registry.hpp"
+#include "vmas_tail.hpp"
+#include "vmas_uniform.hpp"
 
 using namespace vmas;
 
@@ -963,6 +965,10 @@ struct VmasKernelChain {
     const char* world_args = nullptr;
     vmas::JitFnInfo world_info{};
     std::unique_ptr<FusedArgs> wb;
+    // (vmas_graph_chain_launch_tail: the argument block of the launch being queued, Args.tail set)
+    mutable std::vector<char> tail_buf;
+    mutable size_t tail_size = 0;
+    mutable void* tail_extra[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -1233,6 +1239,108 @@ int32_t vmas_graph_chain_launch(const VmasKernelChain* c, void* stream) { return
 
 // The chain with its write-back variant of the k_world launch (vmas_graph_chain_set_writeback).
 int32_t vmas_graph_chain_launch_wb(const VmasKernelChain* c, void* stream) { return chain_launch(c, stream, true); }
+
+// The chain (one fused k_world launch) with the replay's post-replay work as its tail: the spans of
+// vmas_copy_spans and the draw of vmas_uniform_columns_snap (the arguments of
+// vmas_copy_spans_draw), run by k_world's workgroups once the fixed point's final pass is decided
+// (vmas_tail.hpp).  Returns 1 when the launch is queued, 0 when this chain or these items cannot take
+// the tail (nothing queued: the caller launches the chain and vmas_copy_spans_draw), < 0 on error.
+// The caller admits only copies whose sources the launch writes through (vmas_tail.hpp).
+int32_t vmas_graph_chain_launch_tail(const VmasKernelChain* c, int32_t wb, const VmasCopySpan* spans, int32_t n_spans,
+                                     int64_t numel, const VmasUniformColumn* cols, int32_t n_cols, uint64_t seed,
+                                     uint64_t offset, const uint64_t* offset_dev, int32_t mode, int64_t u_snap_delta,
+                                     uint64_t* increment, void* stream) {
+    if (!c || !increment || n_spans < 0 || (n_spans > 0 && !spans) || n_cols < 0 || (n_cols > 0 && !cols) || mode < 0 ||
+        mode > 3)
+        return fail(VMAS_E_INVALID, "vmas_graph_chain_launch_tail: bad arguments");
+    *increment = 0;
+    static const bool off = getenv("VMAS_GRAPH_TAIL") && getenv("VMAS_GRAPH_TAIL")[0] == '0';  // (A/B knob)
+    const vmas::JitFnInfo& a = c->world_info;
+    if (off || c->n != 1 || c->world != 0 || c->fused != 1 || c->args.empty() || a.tail_offset <= 0 ||
+        (size_t)a.tail_offset + sizeof(VmasTail) > a.arg_bytes || n_cols > kTailCols || (wb && !c->wb))
+        return 0;
+    VmasTail t;
+    memset(&t, 0, sizeof t);
+    int n = 0;
+    for (int i = 0; i < n_spans; ++i) {
+        const VmasCopySpan& sp = spans[i];
+        if (sp.nbytes == 0 || (sp.nbytes > 0 && sp.src == sp.dst)) continue;
+        if (sp.nbytes == VMAS_COPY_STORE64) {
+            if (!sp.dst || ((uintptr_t)sp.dst & 7)) return 0;
+        } else if (sp.nbytes < 0 || !sp.dst || (((uintptr_t)sp.src | (uintptr_t)sp.dst | (uintptr_t)sp.nbytes) & 3)) {
+            return 0;  // (copies and increments in whole 4-byte words)
+        }
+        if (n == kTailSpans) return 0;
+        t.s[n++] = sp;
+    }
+    int gx = 0;
+    unsigned long long inc = 0;
+    if (n_cols > 0) {
+        if (numel <= 0) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch_tail: numel %lld", (long long)numel);
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+            (void)hipGetLastError();
+            return fail(VMAS_E_HIP, "vmas_graph_chain_launch_tail: device");
+        }
+        static int max_blocks[64] = {0};
+        if (!max_blocks[dev]) {
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(VMAS_E_HIP, "vmas_graph_chain_launch_tail: device properties");
+            }
+            max_blocks[dev] = prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / vmas_uniform::kThreads);
+        }
+        vmas_uniform::grid_for(numel, max_blocks[dev], &gx, &inc);  // (torch's grid: vmas_copy_spans_draw)
+    }
+    for (int i = 0; i < n_cols; ++i) {
+        if (!cols[i].out) return fail(VMAS_E_INVALID, "vmas_graph_chain_launch_tail: null column %d", i);
+        t.c[i] = cols[i];
+        t.c[i].offset = offset + inc * (unsigned long long)i;
+    }
+    t.seed = seed;
+    t.numel = numel;
+    t.snap = u_snap_delta;
+    t.off_dev = reinterpret_cast<const unsigned long long*>(offset_dev);
+    t.n_spans = n;
+    t.gx_draw = gx;
+    t.mode = mode;
+    t.n_items = n + n_cols;
+    if (t.n_items == 0) return 0;
+    // the items' units (vmas_tail.hpp): a copy's 8-byte (or 4-byte) words, an increment's floats,
+    // one store word, a column's elements -- spread over every thread of the launch
+    int64_t total = 0;
+    for (int y = 0; y < n; ++y) {
+        t.first[y] = (int)total;
+        const VmasCopySpan& sp = t.s[y];
+        const bool w8 = sp.src && ((((uintptr_t)sp.src | (uintptr_t)sp.dst | (uintptr_t)sp.nbytes) & 7) == 0);
+        total += sp.nbytes == VMAS_COPY_STORE64 ? 1 : sp.nbytes / (w8 ? 8 : 4);
+    }
+    for (int y = n; y < n + n_cols; ++y) {
+        t.first[y] = (int)total;
+        total += numel;
+    }
+    if (total >= (int64_t)1 << 30) return 0;
+    t.first[n + n_cols] = (int)total;
+    const FusedArgs* base = wb ? c->wb.get() : c->args.front().get();
+    c->tail_buf.assign(base->buf.begin(), base->buf.begin() + a.arg_bytes);
+    memcpy(c->tail_buf.data() + a.tail_offset, &t, sizeof t);
+    c->tail_size = a.arg_bytes;
+    c->tail_extra[0] = HIP_LAUNCH_PARAM_BUFFER_POINTER;
+    c->tail_extra[1] = c->tail_buf.data();
+    c->tail_extra[2] = HIP_LAUNCH_PARAM_BUFFER_SIZE;
+    c->tail_extra[3] = &c->tail_size;
+    c->tail_extra[4] = HIP_LAUNCH_PARAM_END;
+    const ChainNode& d = c->node[0];
+    const hipError_t e = hipModuleLaunchKernel(d.fn, d.grid.x, d.grid.y, d.grid.z, d.block.x, d.block.y, d.block.z,
+                                               d.shmem, (hipStream_t)stream, nullptr, c->tail_extra);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(VMAS_E_HIP, "vmas_graph_chain_launch_tail: %s", hipGetErrorString(e));
+    }
+    *increment = inc * (unsigned long long)n_cols;
+    return 1;
+}
 
 int32_t vmas_graph_chain_nodes(const VmasKernelChain* c) { return c ? c->n : 0; }
 

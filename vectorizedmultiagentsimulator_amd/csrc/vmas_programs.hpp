@@ -47,6 +47,15 @@ template <class T>
 __device__ __forceinline__ T* moved(T* p, long long d) {
     return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + d);
 }
+// A store written through to memory (sc1): an output that graph mode carries or copies after the
+// replay -- in a fused launch its tail (vmas_tail.hpp) does that inside the same launch, possibly on
+// another XCD, loading the value at agent scope.  The same value as a plain store.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<unsigned int*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt8(uint8_t* p, uint8_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---- flag-independent IEEE arithmetic ---------------------------------------------------------------
 // A world module is compiled with the relaxed options (-fno-hip-fp32-correctly-rounded-divide-sqrt,
@@ -304,12 +313,12 @@ __device__ __forceinline__ void bal_reward(IO& io, int b, int lane, const OutDel
     const float dist = xnorm(pkg - goal);  // vector_norm(package.pos - goal.pos, dim=1)
     io.package_dist[b] = dist;
     const float ground = og ? io.fall_reward : 0.f;  // zeros, masked_fill_(on_the_ground, fall)
-    io.ground_rew[b] = ground;
+    st_wt(io.ground_rew + b, ground);  // (ground_rew, global_shaping, pos_rew: copied after the replay)
     const float gs = dist * io.shaping_factor;
     const float pos_rew = pre.gs - gs;
-    io.global_shaping_out[b] = gs;
+    st_wt(io.global_shaping_out + b, gs);
     if (io.pos_rew_prev) io.pos_rew_prev[b] = 0.f;  // pos_rew[:] = 0 on the tensor being replaced
-    io.pos_rew[b] = pos_rew;
+    st_wt(io.pos_rew + b, pos_rew);
     const float r = ground + pos_rew;  // reward(agent) = ground_rew + pos_rew
     for (int i = 0; i < io.n_agents; ++i) moved(io.rewards[i], od.rew)[b] = r;
     if (io.what & VMAS_SCN_DONE) {  // bal_done on the loaded positions (xdist_spheres' arithmetic)
@@ -369,15 +378,16 @@ __device__ __forceinline__ void tr_reward_done(IO& io, int b, const OutDelta& od
             const VmasShapeRef pk = io.package[i], gl = io.goal[i];
             const float dist = xnorm(ref_pos(pk, b) - ref_pos(gl, b));
             const bool on = xoverlap_box_sphere(pk, gl, b);
-            io.dist_to_goal[i][b] = dist;
-            io.on_goal[i][b] = on ? 1 : 0;
+            // (dist_to_goal, on_goal, colour, global_shaping: carried after the replay, written through)
+            st_wt(io.dist_to_goal[i] + b, dist);
+            st_wt8(io.on_goal[i] + b, on ? 1 : 0);
             float* col = io.color[i] + (long)b * 3;  // where(on_goal, green, red)
-            col[0] = on ? io.green[0] : io.red[0];
-            col[1] = on ? io.green[1] : io.red[1];
-            col[2] = on ? io.green[2] : io.red[2];
+            st_wt(col, on ? io.green[0] : io.red[0]);
+            st_wt(col + 1, on ? io.green[1] : io.red[1]);
+            st_wt(col + 2, on ? io.green[2] : io.red[2]);
             const float shaping = dist * io.shaping_factor;
             rew = rew + (on ? 0.f : io.global_shaping[i][(long)b * io.gs_s0[i]] - shaping);
-            io.global_shaping_out[i][b] = shaping;
+            st_wt(io.global_shaping_out[i] + b, shaping);
             all_on = all_on && on;
         }
         moved(io.rew, od.rew)[b] = rew;

@@ -320,6 +320,11 @@ class Scenario(BaseScenario):
     def info(self, agent: Agent):
         return {"pos_rew": self.pos_rew, "ground_rew": self.ground_rew}
 
+    def _vmas_tail_sources(self):
+        """The tensors the fused program writes through (sc1, csrc/vmas_programs.hpp bal_reward): a
+        graph replay may copy them inside the same launch (environment/_graph.py _tail_ok)."""
+        return [self.global_shaping, self.pos_rew, self.ground_rew]
+
 
 class HeuristicPolicy(BaseHeuristicPolicy):
     """Push the line up while the package is below its goal (balance.py:225-253)."""

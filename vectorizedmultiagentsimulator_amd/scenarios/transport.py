@@ -226,6 +226,11 @@ class Scenario(BaseScenario):
             return d
         return self._run_fused(N.VMAS_SCN_DONE)["done"]
 
+    def _vmas_tail_sources(self):
+        """The tensors the fused program writes through (sc1, csrc/vmas_programs.hpp tr_reward_done):
+        a graph replay may copy them inside the same launch (environment/_graph.py _tail_ok)."""
+        return [t for p in self.packages for t in (p.dist_to_goal, p.on_goal, p.color, p.global_shaping)]
+
 
 class HeuristicPolicy(BaseHeuristicPolicy):
     """Hermite-spline "dribbling" towards a hit point behind the package."""

@@ -1458,8 +1458,11 @@ class StepGraph:
                      else None)
             if ahead is not None:  # (+ the next step's random actions in the same launch)
                 st, drawer, P = ahead
+                # (a single fused launch: these items as its tail, _tail_ok)
+                tail = N.fn_addr("vmas_graph_chain_launch_tail") if ch[0] and not mid and self._tail_ok(t) else 0
                 views, acts, snap, seed, off, inc = N.load_host().post_draw(
-                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"), off_dev, *ch)
+                    host, drawer, mid, hi, P.data_ptr(), P.numel(), N.fn_addr("vmas_copy_spans_draw"), off_dev, *ch,
+                    tail, int(wb))
                 self.env._drew_ahead(st, acts, snap, seed, off, inc)
             else:
                 views = host.post(mid, hi, *ch)
@@ -1489,6 +1492,43 @@ class StepGraph:
                           "bk_ver": tuple(map(_VERSION, self._inplace)), "bk_n": t["n_bk"]}
         fn, consts = self._clone_build
         return fn(views, consts)
+
+    # The post-replay launch's items as the tail of the replay's one fused k_world launch
+    # (csrc/vmas_tail.hpp, vmas_graph_chain_launch_tail): one launch per step instead of two.  A copy
+    # then runs inside the launch that wrote its source, possibly on another XCD, so it is admitted
+    # only when that source is written through: k_world's state outputs (stored sc1) and the
+    # tensors a trusted scenario's program writes through (`_vmas_tail_sources()`: balance's global
+    # shaping, position and ground rewards; transport's per-package distance, on-goal flag, colour and
+    # shaping).  Store words and the step counter need nothing.
+    _TAIL = os.environ.get("VMAS_GRAPH_TAIL", "1") != "0"  # (A/B knob)
+
+    def _tail_ok(self, t) -> bool:
+        ok = t.get("tail_ok")
+        if ok is None:
+            ok = t["tail_ok"] = self._tail_admit(t)
+        return ok
+
+    def _tail_admit(self, t) -> bool:
+        ch, sc = self._chain, self.env.scenario
+        srcs = getattr(sc, "_vmas_tail_sources", None)
+        if (not self._TAIL or ch is None or ch.n_nodes != 1 or not ch.fused or srcs is None or t["plain"]
+                or not _trusted_scenario(sc)):
+            return False
+        ranges = []
+        for v in srcs():
+            if not isinstance(v, Tensor) or not v.is_contiguous():
+                return False
+            ranges.append((v.data_ptr(), v.data_ptr() + v.numel() * v.element_size()))
+        if self._state_idx is not None:  # (the engine's output buffer: k_world's sc1 stores)
+            y = self._carry_src[self._state_idx]
+            ranges.append((y.data_ptr(), y.data_ptr() + y.numel()))
+        for r in t["tbl"]:
+            n, src = int(r["nbytes"]), int(r["src"])
+            if n == N.VMAS_COPY_STORE64 or src == 0 or n == 0:
+                continue
+            if not any(lo <= src and src + n <= hi for lo, hi in ranges):
+                return False
+        return True
 
     def _post_table(self, wb: bool = False):
         """The post-replay span table (N.COPY_SPAN_DTYPE rows): the contiguous outputs (their
