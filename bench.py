@@ -101,6 +101,12 @@ def make_world_env(args, device, seed):
     return env
 
 
+def _tail_launches() -> int:
+    """Graph steps whose post-replay work ran as the tail of their fused launch (csrc/vmas_tail.hpp)."""
+    from vectorizedmultiagentsimulator_amd import _native as N
+    return int(N.load_host().tail_launches())
+
+
 def alg_bytes_per_env_step(world) -> int:
     """SURVEY.md §8d, the physics step's share: read pos/vel/rot/ang_vel of every entity (24 B),
     write them for every movable-or-rotatable entity (24 B), read every agent's force + torque
@@ -425,6 +431,7 @@ def main():
     sync()
     handovers = type(env.scenario).make_world.__globals__.get("HANDOVERS", [0])  # (discovery's respawn)
     h0 = handovers[0]
+    tails0 = _tail_launches() if on_gpu else 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         env.step(env.get_random_actions())
@@ -432,6 +439,7 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    tails = (_tail_launches() - tails0) if on_gpu else 0
     kernel_ms, launches, timer, clock_ghz = 0.0, 0, None, 0.0
     event_us = fused_us = None
     if on_gpu:
@@ -509,6 +517,8 @@ def main():
                       + (f" ({g._chain.fused} scenario program as k_world's epilogue)" if g._chain.fused else "")
                       if g._chain is not None
                       else f"; replay: hipGraphLaunch ({g.chain_why or 'torch replay'})")
+        if tails:  # (csrc/vmas_tail.hpp: the post-replay work inside the same launch)
+            step_mode += f"; post-replay work as that launch's tail in {tails} of {args.steps} timed steps"
     if json.loads(args.kw):
         workload += f", {args.kw}"
     b_env = alg_bytes_per_env_step(world)
