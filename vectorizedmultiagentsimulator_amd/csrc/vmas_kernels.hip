@@ -1261,10 +1261,16 @@ int32_t vmas_graph_chain_launch_tail(const VmasKernelChain* c, int32_t wb, const
         return 0;
     VmasTail t;
     memset(&t, 0, sizeof t);
+    // (diagnostic only, VMAS_TAIL_DIAG=nocopy / nodraw: drop the copies / the draw from the tail to
+    // time its parts -- the step's results are then wrong; never set outside a timing probe)
+    static const char* diag = getenv("VMAS_TAIL_DIAG");
+    const bool no_copy = diag && strcmp(diag, "nocopy") == 0, no_draw = diag && strcmp(diag, "nodraw") == 0;
+    if (no_draw) n_cols = 0;
     int n = 0;
     for (int i = 0; i < n_spans; ++i) {
         const VmasCopySpan& sp = spans[i];
         if (sp.nbytes == 0 || (sp.nbytes > 0 && sp.src == sp.dst)) continue;
+        if (no_copy && sp.src && sp.nbytes != VMAS_COPY_STORE64) continue;
         if (sp.nbytes == VMAS_COPY_STORE64) {
             if (!sp.dst || ((uintptr_t)sp.dst & 7)) return 0;
         } else if (sp.nbytes < 0 || !sp.dst || (((uintptr_t)sp.src | (uintptr_t)sp.dst | (uintptr_t)sp.nbytes) & 3)) {
