@@ -1515,8 +1515,12 @@ class StepGraph:
                 or not _trusted_scenario(sc)):
             return False
         ranges = []
-        for v in srcs():
-            if not isinstance(v, Tensor) or not v.is_contiguous():
+        try:
+            tensors = list(srcs())
+        except Exception:  # noqa: BLE001 -- (an attribute the declaration names is not bound: no tail)
+            return False
+        for v in tensors:
+            if not isinstance(v, Tensor) or not v.is_contiguous() or v.device.type != "cuda":
                 return False
             ranges.append((v.data_ptr(), v.data_ptr() + v.numel() * v.element_size()))
         if self._state_idx is not None:  # (the engine's output buffer: k_world's sc1 stores)
