@@ -740,6 +740,10 @@ int32_t vmas_graph_chain_launch_tail(const VmasKernelChain* chain, int32_t wb, c
                                      int32_t n_spans, int64_t numel, const VmasUniformColumn* cols, int32_t n_cols,
                                      uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int32_t mode,
                                      int64_t u_snap_delta, uint64_t* increment, void* stream);
+/* (round 6, test utility) The tail's draw alone: n_cols columns of numel elements at (seed, offset),
+ * as vmas_uniform_columns draws them (its unit test compares the two bit for bit). */
+int32_t vmas_test_tail_draw(int32_t device, const VmasUniformColumn* cols, int32_t n_cols, int64_t numel, uint64_t seed,
+                            uint64_t offset, int32_t mode, uint64_t* increment, void* stream);
 
 /* Error message of the last failed auxiliary call (vmas_spawn_resolve). */
 const char* vmas_aux_last_error(void);

@@ -101,3 +101,39 @@ def test_copy_spans_draw_matches_copies_and_the_standalone_draw_gpu(gpu_device, 
         assert not dst[:off].any()
     assert torch.equal(steps, torch.arange(3000, dtype=torch.float32, device=gpu_device) + 2.0)  # (two launches)
     assert int(word.item()) == 0x123456789A
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numel", [1000, 65536, 3_000_000])
+def test_tail_draw_matches_the_standalone_draw_gpu(gpu_device, numel):
+    """The post-replay tail's draw (csrc/vmas_tail.hpp: any thread computes any element from its
+    philox subsequence, round and offset residue) equals vmas_uniform_columns -- itself held to
+    torch's uniform_ -- bit for bit, in every mode, at every offset residue (offset % 4: rocrand's
+    interleave into the next block) and over several rounds (3 M elements: q >= 4)."""
+    import ctypes
+
+    import numpy as np
+
+    lib = N.load_library()
+    n_cols = 3
+
+    def columns(out):
+        cols = np.zeros(n_cols, dtype=N.UNIFORM_COLUMN_DTYPE)
+        for k in range(n_cols):
+            cols[k]["out"], cols[k]["stride"] = out[k].data_ptr(), 1
+            cols[k]["from_"], cols[k]["to"] = -1.0 - 0.25 * k, 1.0 + 0.5 * k
+        return cols
+
+    got = torch.full((n_cols, numel), float("nan"), device=gpu_device)
+    want = torch.full((n_cols, numel), float("nan"), device=gpu_device)
+    cg, cw = columns(got), columns(want)
+    for mode in range(4):
+        for offset in (0, 1, 2, 3, 4, 40, 4097):
+            inc, inc2 = ctypes.c_uint64(0), ctypes.c_uint64(0)
+            assert lib.vmas_test_tail_draw(0, cg.ctypes.data, n_cols, numel, 987654321, offset, mode, ctypes.byref(inc),
+                                           N.stream_ptr(0)) == 0, lib.vmas_last_error()
+            assert lib.vmas_uniform_columns(0, numel, cw.ctypes.data, n_cols, 987654321, offset, mode, ctypes.byref(inc2),
+                                            N.stream_ptr(0)) == 0, lib.vmas_aux_last_error()
+            torch.cuda.synchronize()
+            assert inc.value == inc2.value
+            assert torch.equal(got, want), (mode, offset, (got - want).abs().max().item())

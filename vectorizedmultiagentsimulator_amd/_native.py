@@ -101,6 +101,7 @@ EXPORTED_SYMBOLS = (
     "vmas_uniform_columns_snap",
     "vmas_copy_spans_draw",
     "vmas_graph_chain_launch_tail",
+    "vmas_test_tail_draw",
     "vmas_assert_create",
     "vmas_assert_destroy",
     "vmas_assert_publish",
@@ -602,6 +603,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     lib.vmas_graph_chain_set_writeback.argtypes = [_vp, ctypes.c_int64]
     lib.vmas_graph_chain_launch_wb.restype = _i32
     lib.vmas_graph_chain_launch_wb.argtypes = [_vp, _vp]
+    lib.vmas_test_tail_draw.restype = _i32
+    lib.vmas_test_tail_draw.argtypes = [_i32, _vp, _i32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, _i32, _vp, _vp]
     lib.vmas_graph_chain_launch_tail.restype = _i32
     lib.vmas_graph_chain_launch_tail.argtypes = [_vp, _i32, _vp, _i32, ctypes.c_int64, _vp, _i32, ctypes.c_uint64,
                                                  ctypes.c_uint64, _vp, _i32, ctypes.c_int64, _vp, _vp]

@@ -1348,6 +1348,44 @@ int32_t vmas_graph_chain_launch_tail(const VmasKernelChain* c, int32_t wb, const
     return 1;
 }
 
+namespace {
+__global__ void __launch_bounds__(256) k_test_tail(VmasTail t) { vmas_tail::run(t); }
+}  // namespace
+
+// (test utility) The tail's draw items alone (vmas_tail.hpp run / prep / finish) launched by a plain
+// 1-D grid: `n_cols` columns of `numel` elements at (seed, offset), as vmas_uniform_columns draws them
+// -- its unit test compares the two bit for bit at every offset residue and over several rounds.
+int32_t vmas_test_tail_draw(int32_t device, const VmasUniformColumn* cols, int32_t n_cols, int64_t numel, uint64_t seed,
+                            uint64_t offset, int32_t mode, uint64_t* increment, void* stream) {
+    if (device < 0 || device >= 64 || !cols || n_cols < 1 || n_cols > kTailCols || numel <= 0 || !increment || mode < 0 ||
+        mode > 3 || numel * n_cols >= ((int64_t)1 << 30))
+        return fail(VMAS_E_INVALID, "vmas_test_tail_draw: bad arguments");
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    int gx = 0;
+    unsigned long long inc = 0;
+    vmas_uniform::grid_for(numel, prop.multiProcessorCount * (prop.maxThreadsPerMultiProcessor / vmas_uniform::kThreads),
+                           &gx, &inc);
+    VmasTail t;
+    memset(&t, 0, sizeof t);
+    for (int i = 0; i < n_cols; ++i) {
+        t.c[i] = cols[i];
+        t.c[i].offset = offset + inc * (unsigned long long)i;
+        t.first[i] = (int)(numel * i);
+    }
+    t.first[n_cols] = (int)(numel * n_cols);
+    t.seed = seed;
+    t.numel = numel;
+    t.gx_draw = gx;
+    t.mode = mode;
+    t.n_items = n_cols;
+    hipLaunchKernelGGL(k_test_tail, dim3(512), dim3(256), 0, (hipStream_t)stream, t);
+    HIP_TRY(hipGetLastError());
+    *increment = inc * (unsigned long long)n_cols;
+    return VMAS_OK;
+}
+
 int32_t vmas_graph_chain_nodes(const VmasKernelChain* c) { return c ? c->n : 0; }
 
 int32_t vmas_graph_chain_fused(const VmasKernelChain* c) { return c ? c->fused : 0; }
