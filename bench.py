@@ -432,14 +432,26 @@ def main():
     handovers = type(env.scenario).make_world.__globals__.get("HANDOVERS", [0])  # (discovery's respawn)
     h0 = handovers[0]
     tails0 = _tail_launches() if on_gpu else 0
+    ev_region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if on_gpu else None
+    if ev_region:
+        ev_region[0].record()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         env.step(env.get_random_actions())
+    if ev_region:
+        ev_region[1].record()
     sync()
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
     tails = (_tail_launches() - tails0) if on_gpu else 0
+    # the GPU time of the timed region itself (HIP events on the step stream around the loop); per
+    # launch when every step was exactly one launch (a one-launch kernel chain that also ran the
+    # post-replay work as its tail: nothing else is queued per step)
+    region_us = ev_region[0].elapsed_time(ev_region[1]) * 1e3 / args.steps if ev_region else None
+    gch = getattr(getattr(env, "_graph", None), "_chain", None)
+    one_launch = bool(on_gpu and env.graph_status == "graph" and gch is not None and gch.n_nodes == 1
+                      and tails == args.steps)
     kernel_ms, launches, timer, clock_ghz = 0.0, 0, None, 0.0
     event_us = fused_us = None
     if on_gpu:
@@ -533,7 +545,7 @@ def main():
         # timed region's launch mode; includes the dispatch ramp and completion between kernel
         # nodes).  Beside it: events on eager launches (an idle GPU between launches) and the
         # in-kernel timer of the timed region itself (workgroup 0 start -> final pass decided).
-        plain = None
+        plain = fused_no_tail = None
         if graph_us:
             per_launch_ms, headline_timer = graph_us * 1e-3, (
                 f"HIP events around {graph_n} back-to-back launches replayed from a HIP graph of "
@@ -549,6 +561,20 @@ def main():
                     "HIP events around 50 back-to-back launches of the replay's one-launch kernel chain "
                     "(k_world with the scenario program as its epilogue: what the timed steps launch), "
                     "after the timed region")
+                if one_launch and region_us:
+                    # every timed step was ONE k_world launch (physics + the program as its epilogue +
+                    # the post-replay work as its tail, csrc/vmas_tail.hpp): the headline is that
+                    # launch, timed over the timed region itself; the chain without the tail beside it
+                    fused_no_tail = {"kernel_us": round(fused_us, 3),
+                                     "achieved": round(b_env * args.envs / (fused_us * 1e-6) / 1e9, 2),
+                                     "frac": round(b_env * args.envs / (fused_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+                                     "timer": headline_timer.replace("(k_world with the scenario program as its "
+                                                                     "epilogue: what the timed steps launch)",
+                                                                     "(k_world with the scenario program as its "
+                                                                     "epilogue, without the tail)")}
+                    per_launch_ms, headline_timer = region_us * 1e-3, (
+                        f"HIP events on the step stream around the timed region / {args.steps} steps: one "
+                        f"k_world launch per step, back to back (nothing else queued)")
         elif event_us:
             per_launch_ms, headline_timer = event_us * 1e-3, "HIP events on the dispatch packets of eager launches"
         else:
@@ -566,11 +592,14 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic,
             "kernel": world.engine.kernel_name,
-            "variant": ("k_world + the scenario program as its epilogue (the timed steps' launch)" if plain
+            "variant": ("k_world + the scenario program as its epilogue + the post-replay tail (the timed "
+                        "steps' one launch)" if fused_no_tail else
+                        "k_world + the scenario program as its epilogue (the timed steps' launch)" if plain
                         else "the step kernel alone"),
             "kernel_us_per_launch": round(per_launch_ms * 1e3, 3),
             "timer": headline_timer,
             "plain": plain,
+            "fused_no_tail": fused_no_tail,
             "kernel_us_eager_events": round(event_us, 3) if event_us else None,
             "launches_per_step": round(launches / args.steps, 3),
             "alg_bytes_per_env_step": b_env,
@@ -590,16 +619,19 @@ def main():
                 "achieved": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9, 2),
                 "frac": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "traffic_over_alg": round(traffic / (b_fused * args.envs), 3) if traffic else None,
-                "note": ("roofline.achieved / frac keep SURVEY 8(d)'s physics bytes (384 B) over the fused "
-                         "launch's time; this adds the epilogue's outputs.  PMC traffic above it = the state "
-                         "write-back's two extra stores (inputs + first-pass backup, DESIGN.md)"),
+                "note": ("roofline.achieved / frac keep SURVEY 8(d)'s physics bytes (384 B) over the launch's "
+                         "time; this adds the epilogue's outputs.  PMC traffic above it = the state write-back's "
+                         "two extra stores (inputs + first-pass backup) and, in a launch with the post-replay "
+                         "tail, the tail's own items (the next step's draw and its snapshot, the carry; "
+                         "DESIGN.md)"),
             }
         if rp.get("avg_us"):
             # the same command under rocprofv3 --kernel-trace (committed record, same kernel sha):
             # the profiler's own dispatch handling slows the kernel itself (DESIGN.md Measurement).
             # Headline = the fused variant: compared with the record's fused-timer launches
             # (fused_timer_us), else the timed steps' (in_step_us); the plain figure with avg_us.
-            rp_us = (rp.get("fused_timer_us") or rp.get("in_step_us")) if plain else rp["avg_us"]
+            rp_us = (rp.get("in_step_us") if fused_no_tail else
+                     (rp.get("fused_timer_us") or rp.get("in_step_us")) if plain else rp["avg_us"])
             roofline["rocprof"] = {"kernel_us": rp_us, "calls": rp.get("calls"),
                                    "frac": round(b_env * args.envs / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
                                    "ratio_to_headline": round(rp_us / (per_launch_ms * 1e3), 4),

@@ -69,8 +69,11 @@ def main():
     alg = b["roofline"]["alg_bytes_per_env_step"] * b["config"]["num_envs_per_gpu"]
     global SLICE
     fused = bool(b["roofline"].get("plain"))
-    if fused:
-        w, n = int(b.get("warmup", 0)), int(b.get("steps", 0))
+    in_step = bool(b["roofline"].get("fused_no_tail"))  # (the headline: the timed steps' own launches)
+    w, n = int(b.get("warmup", 0)), int(b.get("steps", 0))
+    if in_step:
+        SLICE = (w, w + n)
+    elif fused:
         SLICE = (w + n + 5, w + n + 55)
     plain = all_l = None
     if fused:
@@ -84,6 +87,10 @@ def main():
             pass
         af, aw = per_launch(d, "FETCH_SIZE", kernel, "all")[0], per_launch(d, "WRITE_SIZE", kernel, "all")[0]
         all_l = {"hbm_bytes_per_launch": round(2 * af * 1024 + aw * 1024)}
+        if in_step:  # (the chain without the tail: bench.py's fused timer launches)
+            sl = (w + n + 5, w + n + 55)
+            ff, fw = per_launch(d, "FETCH_SIZE", kernel, sl)[0], per_launch(d, "WRITE_SIZE", kernel, sl)[0]
+            all_l["fused_no_tail_hbm_bytes_per_launch"] = round(2 * ff * 1024 + fw * 1024)
     fetch_kib, n1 = per_launch(d, "FETCH_SIZE", kernel)
     write_kib, n2 = per_launch(d, "WRITE_SIZE", kernel)
     extra = {}
@@ -103,7 +110,9 @@ def main():
         "workload": b["config"]["workload"],
         "kernel": kernel,
         "kernel_source_sha256": hashes.pop(),
-        "variant": ("fused: k_world + the scenario program as its epilogue, dispatches "
+        "variant": (f"the timed steps' launches (k_world + epilogue + post-replay tail), dispatches "
+                    f"[{SLICE[0]}, {SLICE[1]})" if in_step else
+                    "fused: k_world + the scenario program as its epilogue, dispatches "
                     f"[{SLICE[0]}, {SLICE[1]}) (bench.py's fused timer)" if fused else "the step kernel alone"),
         "launches_sampled": [n1, n2],
         "fetch_size_kib_per_launch": round(fetch_kib, 1),
