@@ -253,7 +253,8 @@ def kernel_source_hash(world) -> str:
     # include/): the kernel's identity is the source AND their text
     h = hashlib.sha256(src.encode())
     for f in ("vectorizedmultiagentsimulator_amd/csrc/vmas_jit_ops.hpp",
-              "vectorizedmultiagentsimulator_amd/csrc/vmas_physics.hpp", "include/vmas_mi355x.h") + (
+              "vectorizedmultiagentsimulator_amd/csrc/vmas_physics.hpp",
+              "vectorizedmultiagentsimulator_amd/csrc/vmas_tail.hpp", "include/vmas_mi355x.h") + (
             ("vectorizedmultiagentsimulator_amd/csrc/vmas_programs.hpp",
              "vectorizedmultiagentsimulator_amd/csrc/vmas_query.hpp") if '#include "vmas_programs.hpp"' in src else ()):
         h.update((ROOT / f).read_bytes())

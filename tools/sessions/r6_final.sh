@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6 closing evidence on the committed tree: smoke, the whole -m gpu suite, the bench lines,
 # rocprofv3 kernel trace of the default bench command, and the PMC passes of the same (graph-mode)
-# command -- tools/pmc_traffic.py splits the fused timer's k_world launches from the plain ones.
+# command (10 warm-up steps: every timed step a replay) -- tools/pmc_traffic.py splits the timed steps'
+# k_world launches from the fused-timer and plain ones.
 set -u
 OUT=${OUT:-gpurun_out/r6final}; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -26,6 +27,6 @@ step bench_c2_eager 600 python bench.py --graph off --cpu-steps 0
 fi
 if [ "$PART" != A ]; then
 step prof_c2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --cpu-steps 0
-TAG=r6final BENCH_ARGS="--steps 10 --warmup 3 --cpu-steps 0" bash tools/pmc_session.sh || exit $?
+TAG=${PMC_TAG:-r6final} BENCH_ARGS="--steps 10 --warmup 10 --cpu-steps 0" bash tools/pmc_session.sh || exit $?
 fi
 echo "session done"
