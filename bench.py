@@ -107,6 +107,24 @@ def _tail_launches() -> int:
     return int(N.load_host().tail_launches())
 
 
+def tail_bytes_per_env_step(env) -> int:
+    """Algorithmic bytes of the post-replay tail per env-step (csrc/vmas_tail.hpp): every copy's
+    read + write, every increment's read + write, the store words, and the next step's random
+    actions drawn ahead -- each drawn element written to the returned tensor and to the action
+    buffer, whose previous value is read and written to the snapshot (16 B per element)."""
+    g = getattr(env, "_graph", None)
+    t = None if g is None else getattr(g, "_post_cache_wb" if g._wb else "_post_cache", None)
+    if t is None:
+        return 0
+    from vectorizedmultiagentsimulator_amd import _native as N
+    n = 0
+    for r in t[4]["tbl"]:
+        nb = int(r["nbytes"])
+        n += 8 if nb == N.VMAS_COPY_STORE64 else 2 * max(nb, 0)
+    elems = sum(int(env.get_agent_action_size(a)) for a in env.agents) * env.num_envs  # (the draw's elements)
+    return round((n + 16 * elems) / env.num_envs)
+
+
 def alg_bytes_per_env_step(world) -> int:
     """SURVEY.md §8d, the physics step's share: read pos/vel/rot/ang_vel of every entity (24 B),
     write them for every movable-or-rotatable entity (24 B), read every agent's force + torque
@@ -615,16 +633,19 @@ def main():
             # program's outputs (observations, rewards, done; its state inputs are the step's own
             # outputs, read back inside the launch) -- what its PMC traffic compares with
             b_fused = b_env + program_bytes_per_env_step(env) - 20 * len(world.entities)
+            b_tail = tail_bytes_per_env_step(env) if fused_no_tail else 0
+            b_fused += b_tail
             roofline["fused_alg"] = {
                 "bytes_per_env_step": b_fused,
+                "tail_bytes_per_env_step": b_tail,
                 "achieved": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9, 2),
                 "frac": round(b_fused * args.envs / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "traffic_over_alg": round(traffic / (b_fused * args.envs), 3) if traffic else None,
                 "note": ("roofline.achieved / frac keep SURVEY 8(d)'s physics bytes (384 B) over the launch's "
-                         "time; this adds the epilogue's outputs.  PMC traffic above it = the state write-back's "
-                         "two extra stores (inputs + first-pass backup) and, in a launch with the post-replay "
-                         "tail, the tail's own items (the next step's draw and its snapshot, the carry; "
-                         "DESIGN.md)"),
+                         "time; this adds the epilogue's outputs and the post-replay tail's items (the next "
+                         "step's draw and its snapshot, the carry, the step counter).  PMC traffic above it = "
+                         "the state write-back's two extra stores (inputs + first-pass backup; DESIGN.md) and "
+                         "the FETCH_SIZE x2 correction applied to narrow reads"),
             }
         if rp.get("avg_us"):
             # the same command under rocprofv3 --kernel-trace (committed record, same kernel sha):
