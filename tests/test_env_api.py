@@ -311,3 +311,29 @@ def test_strict_watch_sees_python_containers_changed_in_place():
         change()
         assert _plain_attrs([o], strict=True) != b0
         assert _plain_attrs([o]) == _plain_attrs([o])  # (the non-strict view ignores containers)
+
+
+@pytest.mark.gpu
+def test_eager_infos_are_fresh_copies_gpu(gpu_device):
+    """The eager step's infos (balance: every agent's pos_rew / ground_rew) are clones: equal to the
+    scenario's tensors, one distinct tensor per agent and key, none aliasing the scenario's
+    attributes or another info (reference vmas/simulator/environment/environment.py:293)."""
+    env = make_env("balance", num_envs=256, device=gpu_device, seed=0, graph_step=False, n_agents=4)
+    for _ in range(3):
+        obs, rews, dones, infos = env.step(env.get_random_actions())
+    sc = env.scenario
+    ptrs = set()
+    for info in infos:
+        assert set(info) == {"pos_rew", "ground_rew"}
+        for k, v in info.items():
+            assert torch.equal(v, getattr(sc, k))
+            assert v.data_ptr() != getattr(sc, k).data_ptr()
+            ptrs.add(v.data_ptr())
+    assert len(ptrs) == 2 * len(infos)
+    before = [{k: v.clone() for k, v in i.items()} for i in infos]
+    sc.pos_rew.add_(1.0)  # (the scenario's tensor changes; the returned copies do not)
+    infos[0]["ground_rew"].add_(5.0)  # (nor does one copy change another)
+    for i, (info, b) in enumerate(zip(infos, before)):
+        assert torch.equal(info["pos_rew"], b["pos_rew"])
+        if i:
+            assert torch.equal(info["ground_rew"], b["ground_rew"])
