@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6: the tail's store kind (VMAS_JIT_TAIL_STORE: 0 plain, 1 non-temporal, 2 agent-scope
 # write-through) -- graph parity of balance / transport under each, C2 A/B/C x3, kernel traces.
+# (The knob was measured without gain and removed: profiles/r06/run16_tail_stores.)
 set -u
 OUT=${OUT:-gpurun_out/r6n}; mkdir -p $OUT
 export TMPDIR=/tmp

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 6: plain vs non-temporal tail stores (VMAS_JIT_TAIL_STORE 0 / 1), C2 x5 interleaved pairs.
+# (The knob was measured without gain and removed: profiles/r06/run16_tail_stores.)
 set -u
 OUT=${OUT:-gpurun_out/r6o2}; mkdir -p $OUT
 export TMPDIR=/tmp
